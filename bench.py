@@ -1,0 +1,184 @@
+"""Headline benchmark: k-skip MrR (k = 4) on the 512^3 7-point Poisson CSR system.
+
+BASELINE.json metric: "solver iterations/sec + achieved HBM GB/s, k-skip MrR
+k=4 on 512^3 Poisson CSR" (configs[3]; it fits one MI355X: ~27 GB).
+
+One "step" = one outer k-skip iteration = k+1 solver iterations over the
+whole system (3k+1 SpMVs incl. k two-vector ones, the Gram reduction, k+1
+fused vector updates). The matrix and b are generated on the device before the
+timed region. N GPUs (torchrun, one rank per GPU) solve the SAME global system
+row-partitioned (strong scaling); the halo exchange and the Gram all-gather go
+over RCCL.
+
+Prints ONE JSON line on rank 0 (see DESIGN.md §Measurement for the roofline
+accounting).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--n-side", type=int, default=512)
+    p.add_argument("--k", type=int, default=4)
+    p.add_argument("--method", default="kskipmrr")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-n-side", type=int, default=256,
+                   help="grid side of the CPU-baseline sample")
+    p.add_argument("--no-profile", action="store_true",
+                   help="skip the per-kernel HIP-event timing")
+    return p.parse_args()
+
+
+def cpu_baseline(n_side: int, k: int, method: str):
+    """The oracle (numpy/scipy restatement of v3/cpu, bitwise the reference) on
+    the host cores: one outer iteration on an n_side^3 sample, reported as
+    iterations/s scaled to the 512^3 workload by the row ratio (SpMV and dots
+    are linear in N and memory-bound at these sizes)."""
+    import numpy as np
+    from oracle import matrices, v3cpu
+    try:
+        from threadpoolctl import threadpool_info
+        blas_threads = max([i.get("num_threads", 1) for i in threadpool_info()
+                            if i.get("user_api") == "blas"] or [1])
+    except Exception:  # pragma: no cover
+        blas_threads = None
+    A = matrices.poisson(n_side, 3)
+    b = matrices.rhs(A.shape[0], 1)
+    fn = v3cpu.METHODS[method]
+    kw = dict(tol=0.0, maxiter=(k + 2) if "kskip" in method else 6)
+    if "kskip" in method:
+        kw["k"] = k
+    t0 = time.perf_counter()
+    _, info = fn(A, b, **kw)
+    wall = time.perf_counter() - t0
+    its = int(info["nosl"][-1])
+    rate = its / info["time"]
+    cores = len(os.sched_getaffinity(0))
+    return dict(value=rate * (n_side ** 3) / (512 ** 3), unit="iterations/s",
+                cores=blas_threads if blas_threads else cores,
+                kind="port",
+                sample=(f"oracle.v3cpu.{method} (numpy/scipy restatement of v3/cpu, bitwise "
+                        f"the reference) on {n_side}^3 Poisson, {its} iterations in "
+                        f"{info['time']:.2f} s ({rate:.3f} it/s), scaled x{(n_side/512)**3:.4f} "
+                        f"to 512^3; scipy SpMV 1 thread, OpenBLAS dot {blas_threads} threads, "
+                        f"{cores} affinity cores; wall {wall:.1f} s"))
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    from parallel_krylov_amd.system import Communicator, KrylovSystem, balanced_partition
+
+    comm = None
+    if world > 1:
+        dist.init_process_group("gloo")
+        comm = Communicator.from_torch(None, local)
+    n = args.n_side ** 3
+    part = balanced_partition(n, world)
+    sysm = KrylovSystem(n, [part[rank], part[rank + 1]], [local], comm)
+    sysm.gen_poisson(args.n_side, 3)
+    sysm.finalize()
+    info = sysm.shard_info(0)
+    b = sysm.rhs(1)
+    k = args.k if "kskip" in args.method else 0
+    per_step = (k + 1) if "kskip" in args.method else 1
+    maxiter = (args.warmup + args.steps + 4) * per_step + 2
+    sysm.begin(args.method, b, None, tol=0.0, maxiter=maxiter, k=k,
+               profile=not args.no_profile)
+    sysm.step(args.warmup)
+    sysm.reset_kernel_stats()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sysm.step(args.steps)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    stats = sysm.kernel_stats()
+    out = sysm.finish(args.method)
+    iterations = args.steps * per_step
+    value = iterations / elapsed
+
+    roofline = None
+    kernels = {}
+    if stats:
+        for s in stats:
+            if s["launches"]:
+                avg = s["total_ms"] / s["launches"]
+                kernels[s["name"]] = dict(launches=s["launches"], avg_ms=round(avg, 5),
+                                          gbs=round(s["bytes_per_launch"] / avg / 1e6, 1),
+                                          total_ms=round(s["total_ms"], 3))
+        spmv = {n_: v for n_, v in kernels.items() if n_.startswith("spmv")}
+        dom = max(spmv or kernels, key=lambda n_: kernels[n_]["total_ms"])
+        d = kernels[dom]
+        ach = d["gbs"]
+        roofline = dict(bound="hbm", kernel=dom, achieved=ach, peak=HBM_PEAK_GBS, unit="GB/s",
+                        frac=round(ach / HBM_PEAK_GBS, 4), traffic=None,
+                        bytes_per_launch=next(s["bytes_per_launch"] for s in stats
+                                              if s["name"] == dom),
+                        avg_ms=d["avg_ms"])
+    base = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        base = cpu_baseline(args.cpu_n_side, args.k, args.method)
+    if rank == 0:
+        rec = {
+            "metric": "solver iterations/sec, k-skip MrR k=4 on 512^3 Poisson CSR",
+            "value": round(value, 3),
+            "unit": "iterations/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (7-point Poisson CSR and b = 2u-1 generated on device)",
+            "config": {"workload": f"{args.method} k={k} on {args.n_side}^3 7-point Poisson CSR "
+                                   f"(N={n}, nnz/shard={info['nnz']}), tol=0 fixed iterations",
+                       "method": args.method, "k": k, "n_side": args.n_side,
+                       "step": f"one outer iteration = {per_step} solver iterations",
+                       "parallelism": f"row-partitioned x{world}, RCCL halo + Gram all-gather"},
+            "roofline": roofline,
+            "cpu_baseline": base,
+            "kernels": kernels,
+            "residual_tail": [float(v) for v in out.info["residual"][-3:-1]],
+        }
+        print(json.dumps(rec))
+    sysm.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

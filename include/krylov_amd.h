@@ -1,0 +1,222 @@
+/*
+ * krylov_amd.h -- C ABI of the MI355X-native Krylov inner loop.
+ *
+ * This is the drop-in boundary for the reference's GPU solver families
+ * (5enxia/parallel-krylov, v3/gpu and v3/gpu/mpi). The reference binds its
+ * device work through cupy (cuBLAS ddot, cuSPARSE csrmv, elementwise ufuncs)
+ * and its communication through mpi4py; every entry point below names the
+ * reference interface it replaces (file:line under the reference tree).
+ *
+ * Conventions
+ *  - Plain pointers and sizes only; no torch or HIP types in signatures.
+ *    `stream` arguments are a hipStream_t passed as void* (NULL = default).
+ *  - Every function returns KR_OK (0) or a negative KR_ERR_* code; the
+ *    message of the last failure on the calling thread is kr_last_error().
+ *    Nothing throws across the ABI.
+ *  - All vectors and matrices are fp64 values with int32 column indices;
+ *    row pointers are int32 or int64 (flag `rowptr64`).
+ *  - Device pointers are "dev"; host pointers are "host".
+ */
+#ifndef KRYLOV_AMD_H
+#define KRYLOV_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KR_OK 0
+#define KR_ERR_INVALID -1 /* bad argument / shape */
+#define KR_ERR_HIP -2     /* HIP runtime failure */
+#define KR_ERR_RCCL -3    /* RCCL failure */
+#define KR_ERR_NOMEM -4   /* device allocation failed */
+#define KR_ERR_STATE -5   /* call out of order (e.g. step before begin) */
+
+/* Solver methods (reference modules v3/gpu/{cg,mrr,kskipcg,kskipmrr,adaptivekskipmrr}.py). */
+#define KR_METHOD_CG 0
+#define KR_METHOD_MRR 1
+#define KR_METHOD_KSKIPCG 2
+#define KR_METHOD_KSKIPMRR 3
+#define KR_METHOD_ADAPTIVE_KSKIPMRR 4
+
+/* Library identification. */
+int kr_version(void);
+const char* kr_last_error(void);
+/* Number of HIP devices visible to this process (0 when none). */
+int kr_device_count(int* count);
+
+/* ------------------------------------------------------------------------
+ * Primitive kernels (async on `stream`; operands on one device).
+ * ------------------------------------------------------------------------ */
+
+/* y[i] = sum_j val[j] * x[col[j]] over row i, summed sequentially in stored
+ * order without FMA contraction (bitwise equal to scipy's csr_matvec).
+ * Replaces cupyx csr_matrix.dot called at v3/gpu/common.py:119 and
+ * v3/gpu/mpi/common.py:150. `x` is indexed by `col` directly. */
+int kr_spmv_csr_f64(const void* rowptr_dev, int rowptr64, const int32_t* col_dev,
+                    const double* val_dev, int64_t n_rows, const double* x_dev,
+                    double* y_dev, void* stream);
+
+/* Two right-hand sides in one pass over A: y1 = A x1, y2 = A x2 (each row
+ * summed as in kr_spmv_csr_f64). Replaces the pairs of MultiGpu.dot calls of
+ * the k-skip basis loops (v3/gpu/kskipmrr.py:47-50, v3/gpu/kskipcg.py:39-42). */
+int kr_spmv2_csr_f64(const void* rowptr_dev, int rowptr64, const int32_t* col_dev,
+                     const double* val_dev, int64_t n_rows, const double* x1_dev,
+                     const double* x2_dev, double* y1_dev, double* y2_dev, void* stream);
+
+/* *out_dev = <u, v>, deterministic two-stage reduction.
+ * Replaces cupy.dot (cuBLAS ddot), e.g. v3/gpu/cg.py:32. */
+int kr_dot_f64(const double* u_dev, const double* v_dev, int64_t n, double* out_dev,
+               void* stream);
+
+/* out_dev[0..count) = Gram coefficients of `count` vector pairs
+ * (u_ptrs[i], v_ptrs[i]) in ONE pass over the distinct vectors.
+ * Replaces the 6k+5 cupy.dot calls of v3/gpu/kskipmrr.py:53-61 and the 6k+7 of
+ * v3/gpu/kskipcg.py:44-52. count <= 64. */
+int kr_multidot_f64(const double* const* u_ptrs_host, const double* const* v_ptrs_host,
+                    int count, int64_t n, double* out_dev, void* stream);
+
+/* Fused k-skip MrR / MrR vector step (v3/gpu/kskipmrr.py:67-71):
+ *   y = eta*y + zeta*ar1 ; z = eta*z - zeta*r ; r -= y ; x -= z
+ * rounded exactly like the numpy statements (no FMA). first != 0 selects the
+ * initial step (v3/gpu/kskipmrr.py:30-33): y = zeta*ar1 ; z = (-zeta)*r. */
+int kr_update_mrr_f64(double eta, double zeta, int first, double* y_dev,
+                      const double* ar1_dev, double* z_dev, double* r_dev,
+                      double* x_dev, int64_t n, void* stream);
+
+/* Fused CG vector step (v3/gpu/cg.py:34-35): x += alpha*p ; r -= alpha*v. */
+int kr_update_cg_f64(double alpha, double* x_dev, const double* p_dev, double* r_dev,
+                     const double* v_dev, int64_t n, void* stream);
+
+/* Host scalar recurrences, statement-for-statement with the reference
+ * (libm pow for `**2`, left-to-right, no FMA). They take and return the Gram
+ * coefficient arrays exactly as the reference holds them.
+ *
+ * k-skip MrR (v3/gpu/kskipmrr.py:64-66, 74-90): given alpha[2k+3],
+ * beta[2k+2], delta[2k+1] from the basis, writes zeta[k+1], eta[k+1] for
+ * the k+1 vector steps of one outer iteration (arrays are consumed). */
+int kr_kskipmrr_recurrence(int k, double* alpha, double* beta, double* delta,
+                           double* zeta_out, double* eta_out);
+/* k-skip CG (v3/gpu/kskipcg.py:55-56, 64-72): a[2k+2], f[2k+4], c[2k+2] in,
+ * alpha[k+1], beta[k+1] out (arrays are consumed). */
+int kr_kskipcg_recurrence(int k, double* a, double* f, double* c, double* alpha_out,
+                          double* beta_out);
+
+/* ------------------------------------------------------------------------
+ * Communicator (replaces mpi4py comm.Allgather on the hot path,
+ * v3/gpu/mpi/common.py:163, and the P2P copies of v3/gpu/common.py:117,122).
+ * RCCL over xGMI, one rank per GPU.
+ * ------------------------------------------------------------------------ */
+typedef struct kr_comm kr_comm;
+#define KR_UNIQUE_ID_BYTES 128
+/* Rank 0 creates the id; the caller broadcasts it (e.g. torch.distributed). */
+int kr_comm_unique_id(uint8_t* id_out /* KR_UNIQUE_ID_BYTES */);
+int kr_comm_init(kr_comm** comm, const uint8_t* id, int nranks, int rank, int device);
+int kr_comm_destroy(kr_comm* comm);
+
+/* ------------------------------------------------------------------------
+ * Distributed system: A and every vector row-partitioned into contiguous
+ * shards (replaces MultiGpu.init/alloc, v3/gpu/common.py:62-109 and
+ * v3/gpu/mpi/common.py:73-134). A process owns `nshards` shards; with a
+ * communicator it owns exactly one and its peers own the rest.
+ * ------------------------------------------------------------------------ */
+typedef struct kr_system kr_system;
+
+/* row_begin[0..nshards] are GLOBAL row offsets of this process's shards
+ * (contiguous, increasing). devices[s] is the HIP device of shard s. */
+int kr_system_create(kr_system** sys, int64_t n_global, int nshards, const int* devices,
+                     const int64_t* row_begin, kr_comm* comm);
+int kr_system_destroy(kr_system* sys);
+
+/* Adopt a CSR block already resident on the shard's device: rows
+ * row_begin[s]..row_begin[s+1], GLOBAL column indices, rowptr starting at
+ * rowptr[0] (need not be 0). The caller keeps the buffers alive until
+ * kr_system_destroy; column indices are rewritten IN PLACE to the shard's
+ * local (halo-extended) numbering by kr_system_finalize. */
+int kr_system_adopt_csr(kr_system* sys, int shard, const void* rowptr_dev, int rowptr64,
+                        int32_t* col_dev, const double* val_dev);
+
+/* Generate this shard's rows of a synthetic SPD matrix on the device.
+ * dim = 2 or 3: 5-/7-point Poisson on an n_side^dim grid, lexicographic
+ * order, diagonal 2*dim, off-diagonals -1 (scipy kronsum of tridiag(-1,2,-1)).
+ * Banded: h distinct offsets in [1,W] drawn from `seed`, a(i,i+-o) = -u,
+ * diagonal = sum|off| + 1 (see DESIGN.md for the exact definition). */
+int kr_system_gen_poisson(kr_system* sys, int dim, int64_t n_side);
+int kr_system_gen_banded(kr_system* sys, int h, int64_t width, uint64_t seed,
+                         int rowptr64);
+/* Column remap, halo plan, row blocks and workspaces. Call once after the
+ * matrix of every shard is set. */
+int kr_system_finalize(kr_system* sys);
+/* Info: n_local, halo_lo, halo_hi, nnz of shard s. */
+int kr_system_shard_info(kr_system* sys, int shard, int64_t* n_local, int64_t* halo_lo,
+                         int64_t* halo_hi, int64_t* nnz);
+
+/* Halo exchange plan (pure host arithmetic, no device; test hook and the
+ * planner kr_system_finalize uses). part[0..nshards] is the global row
+ * partition, need_lo[t]..need_hi[t] the global rows shard t's SpMV reads
+ * (its own rows included). For shard `me`, writes (peer, first_row, count)
+ * triples of the rows it receives (recv_out) and sends (send_out), up to
+ * `cap` each; *nrecv / *nsend return the full counts. Replaces the full-vector
+ * broadcast + gather of MultiGpu.dot (v3/gpu/common.py:115-122). */
+int kr_halo_plan(int nshards, const int64_t* part, const int64_t* need_lo,
+                 const int64_t* need_hi, int me, int64_t* recv_out, int* nrecv,
+                 int64_t* send_out, int* nsend, int cap);
+
+/* Synthetic right-hand side b[i] = 2*u(seed,i) - 1 (exact in fp64) for this
+ * shard's rows, written to b_dev (n_local doubles). */
+int kr_fill_rhs(kr_system* sys, int shard, uint64_t seed, double* b_dev);
+
+/* Distributed SpMV of one vector through the halo exchange (test hook):
+ * x_dev / y_dev hold the shard's own rows (n_local each). */
+int kr_system_spmv(kr_system* sys, const double* const* x_dev, double* const* y_dev);
+
+/* ------------------------------------------------------------------------
+ * Solver session: the iteration loops of v3/gpu/<method>.py and
+ * v3/gpu/mpi/<method>.py, run natively.
+ * ------------------------------------------------------------------------ */
+typedef struct {
+  int method;      /* KR_METHOD_* */
+  int k;           /* k-skip depth (ignored by CG/MrR) */
+  double tol;      /* relative residual tolerance */
+  int64_t maxiter; /* <= 0: n_global (reference default, v3/gpu/common.py:35) */
+  int profile;     /* != 0: per-kernel HIP-event timing */
+} kr_solve_params;
+
+typedef struct {
+  double time_s;        /* iteration-loop wall time, as info['time'] */
+  int64_t iterations;   /* final i (info['nosl'][-1]) */
+  int64_t entries;      /* len(info['residual']) */
+  int converged;        /* residual < tol reached */
+  int final_k;          /* adaptive: final k */
+  double final_residual;
+} kr_solve_result;
+
+/* Set up vectors, r0 = b - A x0 and ||b||; b_dev[s]/x0_dev[s] hold shard s's
+ * own rows (x0 may be NULL for zeros). Starts the timer. */
+int kr_solve_begin(kr_system* sys, const kr_solve_params* params,
+                   const double* const* b_dev, const double* const* x0_dev);
+/* Run up to `max_outer` further outer iterations (CG/MrR: iterations).
+ * *done = 1 once converged or maxiter reached. */
+int kr_solve_step(kr_system* sys, int64_t max_outer, int* done);
+/* Finish: final residual bookkeeping, stop the timer, copy x out. */
+int kr_solve_end(kr_system* sys, double* const* x_dev, kr_solve_result* result);
+/* Copy the histories (residual, nosl, khistory; khistory may be NULL). */
+int kr_solve_history(kr_system* sys, double* residual_host, int64_t* nosl_host,
+                     int64_t* khistory_host, int64_t capacity);
+
+/* Per-kernel-class timing (profile != 0): fills up to `cap` records. */
+typedef struct {
+  char name[32];
+  int64_t launches;
+  double total_ms;
+  double bytes_per_launch; /* algorithmic bytes, see DESIGN.md */
+} kr_kernel_stat;
+int kr_solve_kernel_stats(kr_system* sys, kr_kernel_stat* stats, int cap, int* count);
+/* Zero the per-kernel statistics (e.g. after warm-up). */
+int kr_solve_kernel_stats_reset(kr_system* sys);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KRYLOV_AMD_H */

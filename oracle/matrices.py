@@ -1,0 +1,138 @@
+"""Synthetic SPD systems on the host (TEST INFRASTRUCTURE ONLY).
+
+This module belongs to the oracle: only ``tests/``, ``__graft_entry__.smoke()``
+and ``bench.py``'s ``cpu_baseline`` leg may import it. The product path
+(``parallel-krylov_amd``) generates the same matrices on the device
+(``kr_system_gen_poisson`` / ``kr_system_gen_banded``); the definitions below
+are the specification both follow, integer for integer, so the host and device
+CSR arrays are bit-identical (checked in tests/test_gpu_kernels.py).
+
+The reference ships no matrices (``.gitignore:14-17`` drops ``*.npz``/``*.mtx``);
+SURVEY.md §8d defines the synthetic families:
+
+* Poisson: ``kronsum`` of ``tridiag(-1, 2, -1)`` (2D 5-point / 3D 7-point),
+  row-major lexicographic order, sorted columns.
+* Symmetric random banded: one set of ``h`` distinct offsets in ``[1, W]``
+  shared by all rows, ``a(i, i±o) = -u``, diagonal ``= sum|off| + 1``.
+"""
+from __future__ import annotations
+
+import numpy as np
+import scipy.sparse as sp
+
+_MASK = (1 << 64) - 1
+_K1, _K2, _K3 = 0x9E3779B97F4A7C15, 0xC2B2AE3D27D4EB4F, 0x165667B19E3779F9
+
+
+def _mix64_np(x: np.ndarray) -> np.ndarray:
+    x = x + np.uint64(0x9E3779B97F4A7C15)
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def mix64(x: int) -> int:
+    """Scalar splitmix64 finaliser (kr_hash.h ``mix64``)."""
+    x = (x + 0x9E3779B97F4A7C15) & _MASK
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & _MASK
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & _MASK
+    return x ^ (x >> 31)
+
+
+def unit_uniform(seed: int, a, b) -> np.ndarray:
+    """u in [0, 1) with 53 random bits (kr_hash.h ``unit_uniform``)."""
+    with np.errstate(over="ignore"):
+        a = np.asarray(a, dtype=np.uint64)
+        b = np.asarray(b, dtype=np.uint64)
+        key = (np.uint64((seed * _K1) & _MASK) ^ (a * np.uint64(_K2)) ^ (b * np.uint64(_K3)))
+        return (_mix64_np(key) >> np.uint64(11)).astype(np.float64) * 2.0 ** -53
+
+
+def rhs(n: int, seed: int, row0: int = 0) -> np.ndarray:
+    """Synthetic right-hand side b_i = 2u - 1 (kr_hash.h ``rhs_value``)."""
+    i = np.arange(row0, row0 + n, dtype=np.uint64)
+    return 2.0 * unit_uniform(seed, i, 0xB5) - 1.0
+
+
+def poisson(n_side: int, dim: int, dtype_index=np.int32) -> sp.csr_matrix:
+    """5-point (dim=2) / 7-point (dim=3) Poisson matrix, sorted CSR."""
+    if dim not in (2, 3):
+        raise ValueError("dim must be 2 or 3")
+    N = n_side ** dim
+    strides = [n_side ** d for d in range(dim)]
+    g = np.arange(N, dtype=np.int64)
+    coords = [(g // s) % n_side for s in strides]
+    # column order: outer lower neighbours first, diagonal, inner upper first
+    cols, vals, masks = [], [], []
+    for d in reversed(range(dim)):
+        cols.append(g - strides[d]); vals.append(-1.0); masks.append(coords[d] > 0)
+    cols.append(g); vals.append(2.0 * dim); masks.append(np.ones(N, bool))
+    for d in range(dim):
+        cols.append(g + strides[d]); vals.append(-1.0); masks.append(coords[d] < n_side - 1)
+    C = np.stack(cols, axis=1)
+    M = np.stack(masks, axis=1)
+    V = np.broadcast_to(np.asarray(vals, dtype=np.float64), C.shape)
+    counts = M.sum(axis=1)
+    indptr = np.zeros(N + 1, dtype=np.int64)
+    np.cumsum(counts, out=indptr[1:])
+    A = sp.csr_matrix((V[M].copy(), C[M].astype(dtype_index), indptr.astype(dtype_index)),
+                      shape=(N, N))
+    A.has_sorted_indices = True
+    return A
+
+
+def banded_offsets(h: int, width: int, seed: int) -> np.ndarray:
+    """h distinct offsets in [1, width] (kr_capi.cpp ``banded_offsets``)."""
+    pool = list(range(1, width + 1))
+    for t in range(h):
+        r = mix64((seed * 0x2545F4914F6CDD1D + t) & _MASK)
+        j = t + r % (width - t)
+        pool[t], pool[j] = pool[j], pool[t]
+    return np.array(sorted(pool[:h]), dtype=np.int64)
+
+
+def banded(N: int, h: int, width: int, seed: int, dtype_index=np.int32) -> sp.csr_matrix:
+    """Symmetric random banded SPD matrix (device twin: banded_fill_kernel)."""
+    off = banded_offsets(h, width, seed)
+    g = np.arange(N, dtype=np.int64)
+    cols, vals, masks = [], [], []
+    for o in off[::-1]:  # lower part, ascending column
+        lo = g - o
+        m = lo >= 0
+        cols.append(lo)
+        vals.append(-unit_uniform(seed, np.where(m, lo, 0), o))
+        masks.append(m)
+    upper = []
+    for o in off:
+        hi = g + o
+        m = hi < N
+        upper.append((hi, -unit_uniform(seed, g, o), m))
+    # diagonal: sum of |off| in column order (lower then upper), then + 1
+    s = np.zeros(N)
+    for v, m in zip(vals, masks):
+        s = s + np.where(m, np.abs(v), 0.0)
+    for _, v, m in upper:
+        s = s + np.where(m, np.abs(v), 0.0)
+    cols.append(g); vals.append(s + 1.0); masks.append(np.ones(N, bool))
+    for c, v, m in upper:
+        cols.append(c); vals.append(v); masks.append(m)
+    C = np.stack(cols, axis=1)
+    V = np.stack(vals, axis=1)
+    M = np.stack(masks, axis=1)
+    counts = M.sum(axis=1)
+    indptr = np.zeros(N + 1, dtype=np.int64)
+    np.cumsum(counts, out=indptr[1:])
+    A = sp.csr_matrix((V[M].copy(), C[M].astype(dtype_index), indptr.astype(dtype_index)),
+                      shape=(N, N))
+    A.has_sorted_indices = True
+    return A
+
+
+def csr_digest(A: sp.csr_matrix) -> str:
+    """sha256 over (indptr as int64, indices as int64, data as float64)."""
+    import hashlib
+    h = hashlib.sha256()
+    h.update(np.ascontiguousarray(A.indptr, dtype=np.int64).tobytes())
+    h.update(np.ascontiguousarray(A.indices, dtype=np.int64).tobytes())
+    h.update(np.ascontiguousarray(A.data, dtype=np.float64).tobytes())
+    return h.hexdigest()

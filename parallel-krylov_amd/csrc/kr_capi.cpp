@@ -1,0 +1,625 @@
+// extern "C" entry points of libkrylov_amd.so (declared in include/krylov_amd.h).
+// Every entry point catches everything: nothing throws across the ABI.
+#include <cstring>
+#include <map>
+#include <mutex>
+
+#include "kr_engine.h"
+
+namespace kr {
+namespace {
+
+thread_local std::string g_last_error;
+
+template <class F>
+int guarded(F&& f) {
+  try {
+    f();
+    return KR_OK;
+  } catch (const Failure& e) {
+    g_last_error = e.what();
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    g_last_error = "host allocation failed";
+    return KR_ERR_NOMEM;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return KR_ERR_INVALID;
+  } catch (...) {
+    g_last_error = "unknown failure";
+    return KR_ERR_INVALID;
+  }
+}
+
+std::mutex g_scratch_mu;
+std::map<int, std::pair<double*, size_t>> g_scratch;
+
+}  // namespace
+
+double* primitive_scratch(size_t doubles) {
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  int dev = 0;
+  KR_HIP_CHECK(hipGetDevice(&dev));
+  auto& slot = g_scratch[dev];
+  if (slot.second < doubles) {
+    if (slot.first) KR_HIP_CHECK(hipFree(slot.first));
+    slot.first = nullptr;
+    if (hipMalloc(&slot.first, doubles * sizeof(double)) != hipSuccess)
+      throw Failure(KR_ERR_NOMEM, "scratch allocation failed");
+    slot.second = doubles;
+  }
+  return slot.first;
+}
+
+void banded_offsets(int h, int64_t width, uint64_t seed, int64_t* out_sorted);
+
+}  // namespace kr
+
+using namespace kr;
+
+extern "C" {
+
+int kr_version(void) { return 100; }
+
+const char* kr_last_error(void) { return g_last_error.c_str(); }
+
+int kr_device_count(int* count) {
+  return guarded([&] {
+    KR_REQUIRE(count, "count is NULL");
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    *count = c;
+  });
+}
+
+// ----------------------------------------------------------------- primitives
+int kr_spmv_csr_f64(const void* rowptr, int rowptr64, const int32_t* col, const double* val,
+                    int64_t n_rows, const double* x, double* y, void* stream) {
+  return guarded([&] {
+    KR_REQUIRE(n_rows >= 0, "n_rows < 0");
+    if (n_rows == 0) return;
+    KR_REQUIRE(rowptr && col && val && x && y, "NULL operand");
+    SpmvArgs a;
+    a.rowptr = rowptr;
+    a.rowptr64 = rowptr64;
+    a.col = col;
+    a.val = val;
+    a.n = n_rows;
+    a.x1 = x;
+    a.y1 = y;
+    a.grid = default_grid(n_rows);
+    a.partials = primitive_scratch(1);
+    launch_spmv(EPI_NONE, a, static_cast<hipStream_t>(stream));
+  });
+}
+
+int kr_spmv2_csr_f64(const void* rowptr, int rowptr64, const int32_t* col, const double* val,
+                     int64_t n_rows, const double* x1, const double* x2, double* y1,
+                     double* y2, void* stream) {
+  return guarded([&] {
+    KR_REQUIRE(n_rows >= 0, "n_rows < 0");
+    if (n_rows == 0) return;
+    KR_REQUIRE(rowptr && col && val && x1 && x2 && y1 && y2, "NULL operand");
+    SpmvArgs a;
+    a.rowptr = rowptr;
+    a.rowptr64 = rowptr64;
+    a.col = col;
+    a.val = val;
+    a.n = n_rows;
+    a.x1 = x1;
+    a.x2 = x2;
+    a.y1 = y1;
+    a.y2 = y2;
+    a.grid = default_grid(n_rows);
+    a.partials = primitive_scratch(1);
+    launch_spmv(EPI_DUAL_NONE, a, static_cast<hipStream_t>(stream));
+  });
+}
+
+int kr_dot_f64(const double* u, const double* v, int64_t n, double* out, void* stream) {
+  return guarded([&] {
+    KR_REQUIRE(n >= 0 && out, "bad arguments");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    EwArgs a;
+    a.p[0] = const_cast<double*>(u);
+    a.p[1] = const_cast<double*>(v);
+    a.n = n;
+    a.grid = default_grid(n);
+    a.partials = primitive_scratch(a.grid);
+    if (n > 0) KR_REQUIRE(u && v, "NULL operand");
+    launch_ew(EW_DOT, a, s);
+    launch_finalize(a.partials, a.grid, 1, out, s);
+  });
+}
+
+int kr_multidot_f64(const double* const* u_ptrs, const double* const* v_ptrs, int count,
+                    int64_t n, double* out, void* stream) {
+  return guarded([&] {
+    KR_REQUIRE(count >= 0 && count <= 64 && n >= 0 && out, "bad arguments");
+    if (count == 0) return;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    MultiDotArgs a{};
+    for (int i = 0; i < count; ++i) {
+      KR_REQUIRE(n == 0 || (u_ptrs[i] && v_ptrs[i]), "NULL operand");
+      a.u[i] = u_ptrs[i];
+      a.v[i] = v_ptrs[i];
+    }
+    a.count = count;
+    a.n = n;
+    a.grid = default_grid(n);
+    a.partials = primitive_scratch((size_t)count * a.grid);
+    launch_multidot(a, s);
+    launch_finalize(a.partials, a.grid, count, out, s);
+  });
+}
+
+int kr_update_mrr_f64(double eta, double zeta, int first, double* y, const double* ar1,
+                      double* z, double* r, double* x, int64_t n, void* stream) {
+  return guarded([&] {
+    KR_REQUIRE(n >= 0, "n < 0");
+    if (n == 0) return;
+    KR_REQUIRE(y && ar1 && z && r && x, "NULL operand");
+    EwArgs a;
+    a.c0 = eta;
+    a.c1 = zeta;
+    a.p[0] = y;
+    a.p[1] = const_cast<double*>(ar1);
+    a.p[2] = z;
+    a.p[3] = r;
+    a.p[4] = x;
+    a.p[5] = x;
+    a.n = n;
+    a.grid = default_grid(n);
+    a.partials = primitive_scratch(a.grid);
+    launch_ew(first ? EW_MRR_FIRST : EW_MRR, a, static_cast<hipStream_t>(stream));
+  });
+}
+
+int kr_update_cg_f64(double alpha, double* x, const double* p, double* r, const double* v,
+                     int64_t n, void* stream) {
+  return guarded([&] {
+    KR_REQUIRE(n >= 0, "n < 0");
+    if (n == 0) return;
+    KR_REQUIRE(x && p && r && v, "NULL operand");
+    EwArgs a;
+    a.c0 = alpha;
+    a.p[0] = x;
+    a.p[1] = const_cast<double*>(p);
+    a.p[2] = r;
+    a.p[3] = const_cast<double*>(v);
+    a.n = n;
+    a.grid = default_grid(n);
+    a.partials = primitive_scratch(a.grid);
+    launch_ew(EW_CG, a, static_cast<hipStream_t>(stream));
+  });
+}
+
+int kr_kskipmrr_recurrence(int k, double* alpha, double* beta, double* delta, double* zeta_out,
+                           double* eta_out) {
+  return guarded([&] {
+    KR_REQUIRE(k >= 0 && alpha && beta && delta && zeta_out && eta_out, "bad arguments");
+    kskipmrr_recurrence(k, alpha, beta, delta, zeta_out, eta_out);
+  });
+}
+
+int kr_kskipcg_recurrence(int k, double* a, double* f, double* c, double* alpha_out,
+                          double* beta_out) {
+  return guarded([&] {
+    KR_REQUIRE(k >= 0 && a && f && c && alpha_out && beta_out, "bad arguments");
+    kskipcg_recurrence(k, a, f, c, alpha_out, beta_out);
+  });
+}
+
+int kr_halo_plan(int nshards, const int64_t* part, const int64_t* need_lo,
+                 const int64_t* need_hi, int me, int64_t* recv_out, int* nrecv,
+                 int64_t* send_out, int* nsend, int cap) {
+  return guarded([&] {
+    KR_REQUIRE(nshards >= 1 && part && need_lo && need_hi && me >= 0 && me < nshards &&
+                   nrecv && nsend,
+               "bad arguments");
+    std::vector<HaloPiece> recv, send;
+    plan_halo(nshards, part, need_lo, need_hi, me, recv, send);
+    *nrecv = (int)recv.size();
+    *nsend = (int)send.size();
+    for (int q = 0; q < (int)recv.size() && q < cap; ++q) {
+      recv_out[3 * q] = recv[q].peer;
+      recv_out[3 * q + 1] = recv[q].g0;
+      recv_out[3 * q + 2] = recv[q].count;
+    }
+    for (int q = 0; q < (int)send.size() && q < cap; ++q) {
+      send_out[3 * q] = send[q].peer;
+      send_out[3 * q + 1] = send[q].g0;
+      send_out[3 * q + 2] = send[q].count;
+    }
+  });
+}
+
+// ----------------------------------------------------------------- comm
+struct kr_comm : Comm {};
+
+int kr_comm_unique_id(uint8_t* id_out) {
+  return guarded([&] {
+    KR_REQUIRE(id_out, "id_out is NULL");
+    static_assert(sizeof(ncclUniqueId) == KR_UNIQUE_ID_BYTES, "unique id size");
+    ncclUniqueId id;
+    KR_NCCL_CHECK(ncclGetUniqueId(&id));
+    std::memcpy(id_out, &id, sizeof(id));
+  });
+}
+
+int kr_comm_init(kr_comm** comm, const uint8_t* id, int nranks, int rank, int device) {
+  return guarded([&] {
+    KR_REQUIRE(comm && id && nranks >= 1 && rank >= 0 && rank < nranks, "bad arguments");
+    auto c = std::make_unique<kr_comm>();
+    c->rank = rank;
+    c->nranks = nranks;
+    c->device = device;
+    KR_HIP_CHECK(hipSetDevice(device));
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    KR_NCCL_CHECK(ncclCommInitRank(&c->nccl, nranks, uid, rank));
+    *comm = c.release();
+  });
+}
+
+int kr_comm_destroy(kr_comm* comm) {
+  return guarded([&] {
+    if (!comm) return;
+    if (comm->nccl) ncclCommDestroy(comm->nccl);
+    delete comm;
+  });
+}
+
+// ----------------------------------------------------------------- system
+struct kr_system : System {};
+
+int kr_system_create(kr_system** out, int64_t n_global, int nshards, const int* devices,
+                     const int64_t* row_begin, kr_comm* comm) {
+  return guarded([&] {
+    KR_REQUIRE(out && devices && row_begin && nshards >= 1 && n_global >= 0, "bad arguments");
+    if (comm) KR_REQUIRE(nshards == 1, "with a communicator a process owns one shard");
+    for (int s = 0; s < nshards; ++s)
+      KR_REQUIRE(row_begin[s] <= row_begin[s + 1], "row_begin must be non-decreasing");
+    auto sys = std::make_unique<kr_system>();
+    sys->n_global = n_global;
+    sys->comm = comm;
+    sys->shards.resize(nshards);
+    for (int s = 0; s < nshards; ++s) {
+      Shard& sh = sys->shards[s];
+      sh.dev = devices[s];
+      sh.row0 = row_begin[s];
+      sh.n = row_begin[s + 1] - row_begin[s];
+      KR_HIP_CHECK(hipSetDevice(sh.dev));
+      KR_HIP_CHECK(hipStreamCreateWithFlags(&sh.stream, hipStreamNonBlocking));
+    }
+    if (comm) {
+      // global partition from every rank's [row0, row1)
+      Shard& sh = sys->shards[0];
+      const int P = comm->nranks;
+      int64_t* d = nullptr;
+      KR_HIP_CHECK(hipMalloc(&d, sizeof(int64_t) * (2 + 2 * P)));
+      int64_t mine[2] = {sh.row0, sh.row0 + sh.n};
+      KR_HIP_CHECK(hipMemcpy(d, mine, sizeof(mine), hipMemcpyHostToDevice));
+      KR_NCCL_CHECK(ncclAllGather(d, d + 2, 2, ncclInt64, comm->nccl, sh.stream));
+      std::vector<int64_t> all(2 * P);
+      KR_HIP_CHECK(hipMemcpyAsync(all.data(), d + 2, sizeof(int64_t) * 2 * P,
+                                  hipMemcpyDeviceToHost, sh.stream));
+      KR_HIP_CHECK(hipStreamSynchronize(sh.stream));
+      KR_HIP_CHECK(hipFree(d));
+      sys->part.assign(P + 1, 0);
+      for (int r = 0; r < P; ++r) {
+        KR_REQUIRE(all[2 * r] == (r == 0 ? 0 : all[2 * r - 1]),
+                   "rank row blocks must be contiguous and in rank order");
+        sys->part[r] = all[2 * r];
+      }
+      sys->part[P] = all[2 * P - 1];
+      KR_REQUIRE(sys->part[P] == n_global, "rank row blocks must cover n_global");
+      sys->first_global = comm->rank;
+    } else {
+      KR_REQUIRE(row_begin[0] == 0 && row_begin[nshards] == n_global,
+                 "in-process shards must cover [0, n_global)");
+      sys->part.assign(row_begin, row_begin + nshards + 1);
+      sys->first_global = 0;
+      // peer access between distinct devices (best effort)
+      for (int a = 0; a < nshards; ++a)
+        for (int b = 0; b < nshards; ++b) {
+          const int da = devices[a], db = devices[b];
+          if (da == db) continue;
+          int can = 0;
+          if (hipDeviceCanAccessPeer(&can, da, db) == hipSuccess && can) {
+            (void)hipSetDevice(da);
+            hipError_t e = hipDeviceEnablePeerAccess(db, 0);
+            (void)e;
+            if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+          }
+        }
+    }
+    *out = sys.release();
+  });
+}
+
+int kr_system_destroy(kr_system* sys) {
+  return guarded([&] { delete sys; });
+}
+
+int kr_system_adopt_csr(kr_system* sys, int shard, const void* rowptr, int rowptr64,
+                        int32_t* col, const double* val) {
+  return guarded([&] {
+    KR_REQUIRE(sys && shard >= 0 && shard < (int)sys->shards.size(), "bad shard");
+    KR_REQUIRE(!sys->finalized, "system already finalized");
+    KR_REQUIRE(rowptr && col && val, "NULL CSR operand");
+    Shard& s = sys->shards[shard];
+    s.rowptr = rowptr;
+    s.rowptr64 = rowptr64;
+    s.col = col;
+    s.val = val;
+  });
+}
+
+}  // extern "C"
+
+namespace {
+void* dmalloc(Shard& s, size_t bytes) {
+  void* p = nullptr;
+  if (hipMalloc(&p, bytes ? bytes : 8) != hipSuccess)
+    throw Failure(KR_ERR_NOMEM, "matrix allocation failed");
+  s.owned.push_back(p);
+  return p;
+}
+
+template <class Count, class Fill>
+void generate(kr_system* sys, int rowptr64_req, int max_row_nnz, Count count, Fill fill) {
+  KR_REQUIRE(sys && !sys->finalized, "bad system state");
+  for (auto& s : sys->shards) {
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    const int rp64 = rowptr64_req || (double)s.n * max_row_nnz >= 2147483647.0;
+    const size_t rpb = rp64 ? 8 : 4;
+    void* rp = dmalloc(s, rpb * (size_t)(s.n + 1));
+    KR_HIP_CHECK(hipMemsetAsync(rp, 0, rpb, s.stream));
+    count(s, rp, rp64);
+    rowptr_scan(rp, rp64, s.n, s.stream);
+    int64_t nnz = 0;
+    if (rp64) {
+      KR_HIP_CHECK(hipMemcpy(&nnz, (int64_t*)rp + s.n, 8, hipMemcpyDeviceToHost));
+    } else {
+      int32_t v = 0;
+      KR_HIP_CHECK(hipMemcpy(&v, (int32_t*)rp + s.n, 4, hipMemcpyDeviceToHost));
+      nnz = v;
+    }
+    int32_t* col = (int32_t*)dmalloc(s, 4 * (size_t)nnz);
+    double* val = (double*)dmalloc(s, 8 * (size_t)nnz);
+    fill(s, rp, rp64, col, val);
+    KR_HIP_CHECK(hipStreamSynchronize(s.stream));
+    s.rowptr = rp;
+    s.rowptr64 = rp64;
+    s.col = col;
+    s.val = val;
+    s.nnz = nnz;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int kr_system_gen_poisson(kr_system* sys, int dim, int64_t n_side) {
+  return guarded([&] {
+    KR_REQUIRE(dim == 2 || dim == 3, "dim must be 2 or 3");
+    KR_REQUIRE(n_side >= 1, "n_side must be positive");
+    int64_t N = 1;
+    for (int d = 0; d < dim; ++d) N *= n_side;
+    KR_REQUIRE(N == sys->n_global, "n_side^dim must equal n_global");
+    generate(
+        sys, 0, 2 * dim + 1,
+        [&](Shard& s, void* rp, int rp64) {
+          launch_poisson_count(dim, n_side, s.row0, s.n, rp, rp64, s.stream);
+        },
+        [&](Shard& s, void* rp, int rp64, int32_t* col, double* val) {
+          launch_poisson_fill(dim, n_side, s.row0, s.n, rp, rp64, col, val, s.stream);
+        });
+  });
+}
+
+int kr_system_gen_banded(kr_system* sys, int h, int64_t width, uint64_t seed, int rowptr64) {
+  return guarded([&] {
+    KR_REQUIRE(h >= 1 && h <= 64 && width >= h, "need 1 <= h <= 64 and h <= width");
+    BandSpec b{};
+    b.h = h;
+    b.seed = seed;
+    b.n_global = sys->n_global;
+    banded_offsets(h, width, seed, b.off);
+    generate(
+        sys, rowptr64, 2 * h + 1,
+        [&](Shard& s, void* rp, int rp64) {
+          launch_banded_count(b, s.row0, s.n, rp, rp64, s.stream);
+        },
+        [&](Shard& s, void* rp, int rp64, int32_t* col, double* val) {
+          launch_banded_fill(b, s.row0, s.n, rp, rp64, col, val, s.stream);
+        });
+  });
+}
+
+int kr_system_finalize(kr_system* sys) {
+  return guarded([&] {
+    KR_REQUIRE(sys, "NULL system");
+    sys->finalize();
+  });
+}
+
+int kr_system_shard_info(kr_system* sys, int shard, int64_t* n_local, int64_t* halo_lo,
+                         int64_t* halo_hi, int64_t* nnz) {
+  return guarded([&] {
+    KR_REQUIRE(sys && shard >= 0 && shard < (int)sys->shards.size(), "bad shard");
+    const Shard& s = sys->shards[shard];
+    if (n_local) *n_local = s.n;
+    if (halo_lo) *halo_lo = s.halo_lo;
+    if (halo_hi) *halo_hi = s.halo_hi;
+    if (nnz) *nnz = s.nnz;
+  });
+}
+
+int kr_fill_rhs(kr_system* sys, int shard, uint64_t seed, double* b) {
+  return guarded([&] {
+    KR_REQUIRE(sys && shard >= 0 && shard < (int)sys->shards.size(), "bad shard");
+    Shard& s = sys->shards[shard];
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    launch_fill_rhs(seed, s.row0, s.n, b, s.stream);
+    KR_HIP_CHECK(hipStreamSynchronize(s.stream));
+  });
+}
+
+int kr_system_spmv(kr_system* sys, const double* const* x, double* const* y) {
+  return guarded([&] {
+    KR_REQUIRE(sys && sys->finalized, "system not finalized");
+    KR_REQUIRE(x && y, "NULL operand");
+    sys->session.reset();
+    sys->alloc_vectors(2);
+    for (size_t li = 0; li < sys->shards.size(); ++li) {
+      Shard& s = sys->shards[li];
+      KR_HIP_CHECK(hipSetDevice(s.dev));
+      KR_HIP_CHECK(hipMemcpyAsync(s.own(0), x[li], 8 * (size_t)s.n, hipMemcpyDeviceToDevice,
+                                  s.stream));
+    }
+    sys->spmv(EPI_NONE, 0, -1, 1, -1, -1, -1, 0);
+    for (size_t li = 0; li < sys->shards.size(); ++li) {
+      Shard& s = sys->shards[li];
+      KR_HIP_CHECK(hipSetDevice(s.dev));
+      KR_HIP_CHECK(hipMemcpyAsync(y[li], s.own(1), 8 * (size_t)s.n, hipMemcpyDeviceToDevice,
+                                  s.stream));
+    }
+    for (auto& s : sys->shards) {
+      KR_HIP_CHECK(hipSetDevice(s.dev));
+      KR_HIP_CHECK(hipStreamSynchronize(s.stream));
+    }
+  });
+}
+
+// ----------------------------------------------------------------- solver
+int kr_solve_begin(kr_system* sys, const kr_solve_params* params, const double* const* b,
+                   const double* const* x0) {
+  return guarded([&] {
+    KR_REQUIRE(sys && params, "NULL argument");
+    if (!sys->finalized) throw Failure(KR_ERR_STATE, "kr_system_finalize was not called");
+    sys->session.reset();
+    for (auto& s : sys->shards) s.stats.clear();
+    sys->profile = params->profile != 0;
+    sys->session = make_session(sys, *params);
+    sys->session->begin(b, x0);
+  });
+}
+
+int kr_solve_step(kr_system* sys, int64_t max_outer, int* done) {
+  return guarded([&] {
+    KR_REQUIRE(sys, "NULL system");
+    if (!sys->session) throw Failure(KR_ERR_STATE, "kr_solve_begin was not called");
+    Session& ss = *sys->session;
+    for (int64_t c = 0; c < max_outer && !ss.done; ++c) ss.step_once();
+    if (done) *done = ss.done ? 1 : 0;
+  });
+}
+
+int kr_solve_end(kr_system* sys, double* const* x, kr_solve_result* res) {
+  return guarded([&] {
+    KR_REQUIRE(sys, "NULL system");
+    if (!sys->session) throw Failure(KR_ERR_STATE, "kr_solve_begin was not called");
+    Session& ss = *sys->session;
+    for (auto& s : sys->shards) {
+      KR_HIP_CHECK(hipSetDevice(s.dev));
+      KR_HIP_CHECK(hipStreamSynchronize(s.stream));
+    }
+    ss.t_end = now_seconds();
+    sys->harvest_profile();
+    if (res) {
+      res->time_s = ss.t_end - ss.t_start;
+      res->iterations = ss.i;
+      res->entries = ss.entries();
+      res->converged = ss.converged ? 1 : 0;
+      res->final_k = ss.k;
+      res->final_residual = ss.residual.empty() ? 0.0 : ss.residual[ss.index];
+    }
+    if (x) {
+      const int id = ss.result_x();
+      for (size_t li = 0; li < sys->shards.size(); ++li) {
+        Shard& s = sys->shards[li];
+        if (!x[li]) continue;
+        KR_HIP_CHECK(hipSetDevice(s.dev));
+        KR_HIP_CHECK(hipMemcpyAsync(x[li], s.own(id), 8 * (size_t)s.n, hipMemcpyDeviceToDevice,
+                                    s.stream));
+        KR_HIP_CHECK(hipStreamSynchronize(s.stream));
+      }
+    }
+  });
+}
+
+int kr_solve_history(kr_system* sys, double* residual, int64_t* nosl, int64_t* khistory,
+                     int64_t capacity) {
+  return guarded([&] {
+    KR_REQUIRE(sys && sys->session, "no session");
+    Session& ss = *sys->session;
+    const int64_t n = std::min<int64_t>(capacity, ss.entries());
+    for (int64_t q = 0; q < n; ++q) {
+      if (residual) residual[q] = q < (int64_t)ss.residual.size() ? ss.residual[q] : 0.0;
+      if (nosl) nosl[q] = q < (int64_t)ss.nosl.size() ? ss.nosl[q] : 0;
+      if (khistory) khistory[q] = q < (int64_t)ss.khist.size() ? ss.khist[q] : 0;
+    }
+  });
+}
+
+int kr_solve_kernel_stats(kr_system* sys, kr_kernel_stat* stats, int cap, int* count) {
+  return guarded([&] {
+    KR_REQUIRE(sys && count, "NULL argument");
+    int c = 0;
+    if (!sys->shards.empty()) {
+      for (auto& kv : sys->shards[0].stats) {
+        if (c < cap && stats) {
+          std::memset(&stats[c], 0, sizeof(kr_kernel_stat));
+          std::strncpy(stats[c].name, kv.first.c_str(), sizeof(stats[c].name) - 1);
+          stats[c].launches = kv.second.launches;
+          stats[c].total_ms = kv.second.total_ms;
+          stats[c].bytes_per_launch = kv.second.bytes;
+        }
+        ++c;
+      }
+    }
+    *count = c;
+  });
+}
+
+int kr_solve_kernel_stats_reset(kr_system* sys) {
+  return guarded([&] {
+    KR_REQUIRE(sys, "NULL system");
+    sys->harvest_profile();
+    for (auto& s : sys->shards) s.stats.clear();
+  });
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ helpers
+namespace kr {
+
+uint64_t splitmix64(uint64_t x);
+
+void banded_offsets(int h, int64_t width, uint64_t seed, int64_t* out_sorted) {
+  // Partial Fisher-Yates over [1, width] driven by the counter hash; the
+  // numpy oracle (oracle/matrices.py) restates it integer for integer.
+  std::vector<int64_t> pool(width);
+  for (int64_t t = 0; t < width; ++t) pool[t] = t + 1;
+  for (int t = 0; t < h; ++t) {
+    const uint64_t r = splitmix64(seed * 0x2545F4914F6CDD1Dull + (uint64_t)t);
+    const int64_t j = t + (int64_t)(r % (uint64_t)(width - t));
+    std::swap(pool[t], pool[j]);
+  }
+  std::vector<int64_t> pick(pool.begin(), pool.begin() + h);
+  std::sort(pick.begin(), pick.end());
+  for (int t = 0; t < h; ++t) out_sorted[t] = pick[t];
+}
+
+uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+}  // namespace kr

@@ -1,0 +1,786 @@
+// Host engine: sharded system + solver sessions.
+//
+// The reference keeps vectors replicated and moves whole vectors per SpMV
+// (v3/gpu/common.py:113-126: full-x peer broadcast + gather; the MPI family
+// adds comm.Allgather, v3/gpu/mpi/common.py:163). Here A and EVERY vector are
+// row-partitioned; a SpMV input is exchanged only over the halo rows its
+// columns reach, and the Gram/dot scalars are reduced once per sync point.
+#include "kr_engine.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+
+namespace kr {
+
+double now_seconds() {
+  using clk = std::chrono::steady_clock;
+  return std::chrono::duration<double>(clk::now().time_since_epoch()).count();
+}
+
+namespace {
+
+int g_grid_cap = 0;
+
+int grid_cap() {
+  if (g_grid_cap == 0) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        cus > 0)
+      g_grid_cap = cus * 8;
+    else
+      g_grid_cap = 2048;
+  }
+  return g_grid_cap;
+}
+
+int ew_vectors(EwOp op) {
+  switch (op) {
+    case EW_DOT: return 2;
+    case EW_MRR_FIRST: return 7;
+    case EW_MRR: return 9;
+    case EW_CG: return 6;
+    case EW_CG_P: return 3;
+    case EW_KCG: return 7;
+    case EW_MRR_S: return 3;
+    case EW_COPY: return 2;
+  }
+  return 0;
+}
+
+const char* epi_name(SpmvEpi e) {
+  switch (e) {
+    case EPI_NONE: return "spmv";
+    case EPI_BMINUS: return "spmv_bminus";
+    case EPI_XY: return "spmv_xy";
+    case EPI_HEAD_MRR: return "spmv_head_mrr";
+    case EPI_HEAD_KCG: return "spmv_head_kcg";
+    case EPI_MRR_LOOP: return "spmv_mrr_loop";
+    case EPI_DUAL_NONE: return "spmv2";
+    case EPI_DUAL_MRR: return "spmv2_gram_mrr";
+    case EPI_DUAL_KCG: return "spmv2_gram_kcg";
+  }
+  return "spmv?";
+}
+
+const char* ew_name(EwOp op) {
+  switch (op) {
+    case EW_DOT: return "dot";
+    case EW_MRR_FIRST: return "update_mrr_first";
+    case EW_MRR: return "update_mrr";
+    case EW_CG: return "update_cg";
+    case EW_CG_P: return "update_cg_p";
+    case EW_KCG: return "update_kcg";
+    case EW_MRR_S: return "mrr_s";
+    case EW_COPY: return "copy";
+  }
+  return "ew?";
+}
+
+}  // namespace
+
+int default_grid(int64_t n) {
+  const int64_t need = std::max<int64_t>(1, (n + kBlock - 1) / kBlock);
+  return (int)std::min<int64_t>(need, grid_cap());
+}
+
+void plan_halo(int P, const int64_t* part, const int64_t* need_lo, const int64_t* need_hi,
+               int me, std::vector<HaloPiece>& recv, std::vector<HaloPiece>& send) {
+  recv.clear();
+  send.clear();
+  const int64_t r0 = part[me], r1 = part[me + 1];
+  for (int t = 0; t < P; ++t) {
+    if (t == me) continue;
+    const int64_t t0 = part[t], t1 = part[t + 1];
+    // rows I need that t owns: my needed range minus my own rows, cut by t's rows
+    auto add = [](std::vector<HaloPiece>& out, int peer, int64_t a, int64_t b, int64_t c0,
+                  int64_t c1) {
+      const int64_t x0 = std::max(a, c0), x1 = std::min(b, c1);
+      if (x1 > x0) out.push_back({peer, x0, x1 - x0});
+    };
+    add(recv, t, need_lo[me], r0, t0, t1);
+    add(recv, t, r1, need_hi[me] + 1, t0, t1);
+    // rows t needs that I own (the matching sends)
+    add(send, t, need_lo[t], t0, r0, r1);
+    add(send, t, t1, need_hi[t] + 1, r0, r1);
+  }
+}
+
+System::~System() {
+  session.reset();
+  for (auto& s : shards) {
+    (void)hipSetDevice(s.dev);
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
+    for (double* v : s.vec) (void)hipFree(v);
+    for (void* p : s.owned) (void)hipFree(p);
+    if (s.partials) (void)hipFree(s.partials);
+    if (s.slots) (void)hipFree(s.slots);
+    if (s.gather) (void)hipFree(s.gather);
+    if (s.host) (void)hipHostFree(s.host);
+    for (auto& p : s.pending) {
+      (void)hipEventDestroy(p.t0);
+      (void)hipEventDestroy(p.t1);
+    }
+    for (auto e : s.event_pool) (void)hipEventDestroy(e);
+    if (s.ev_a) (void)hipEventDestroy(s.ev_a);
+    if (s.ev_b) (void)hipEventDestroy(s.ev_b);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+  }
+}
+
+void System::finalize() {
+  KR_REQUIRE(!finalized, "system already finalized");
+  const int P = nglobal_shards();
+  const int nranks = comm ? comm->nranks : 1;
+  // 1. column range of every local block
+  for (auto& s : shards) {
+    KR_REQUIRE(s.rowptr && s.col && s.val, "matrix of a shard is not set");
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    int64_t* d = nullptr;
+    KR_HIP_CHECK(hipMalloc(&d, 2 * sizeof(int64_t)));
+    launch_col_minmax(s.rowptr, s.rowptr64, s.n, s.col, d, s.stream);
+    int64_t h[2];
+    KR_HIP_CHECK(hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, s.stream));
+    KR_HIP_CHECK(hipStreamSynchronize(s.stream));
+    KR_HIP_CHECK(hipFree(d));
+    if (s.n == 0 || h[0] == INT64_MAX) {
+      s.col_lo = s.row0;
+      s.col_hi = s.row0 + s.n - 1;
+    } else {
+      s.col_lo = std::min(h[0], s.row0);
+      s.col_hi = std::max(h[1], s.row0 + s.n - 1);
+    }
+    KR_REQUIRE(s.col_lo >= 0 && s.col_hi < n_global, "column index out of range");
+    // nnz
+    if (s.rowptr64) {
+      int64_t e[2];
+      KR_HIP_CHECK(hipMemcpy(&e[0], s.rowptr, 8, hipMemcpyDeviceToHost));
+      KR_HIP_CHECK(hipMemcpy(&e[1], (const int64_t*)s.rowptr + s.n, 8, hipMemcpyDeviceToHost));
+      s.nnz = e[1] - e[0];
+    } else {
+      int32_t e[2];
+      KR_HIP_CHECK(hipMemcpy(&e[0], s.rowptr, 4, hipMemcpyDeviceToHost));
+      KR_HIP_CHECK(hipMemcpy(&e[1], (const int32_t*)s.rowptr + s.n, 4, hipMemcpyDeviceToHost));
+      s.nnz = (int64_t)e[1] - e[0];
+    }
+  }
+  // 2. everybody's needed range [lo, hi]
+  std::vector<int64_t> lo(P), hi(P);
+  if (comm) {
+    Shard& s = shards[0];
+    int64_t* d = nullptr;
+    KR_HIP_CHECK(hipMalloc(&d, (size_t)(2 + 2 * P) * sizeof(int64_t)));
+    int64_t mine[2] = {s.col_lo, s.col_hi};
+    KR_HIP_CHECK(hipMemcpy(d, mine, sizeof(mine), hipMemcpyHostToDevice));
+    KR_NCCL_CHECK(ncclAllGather(d, d + 2, 2, ncclInt64, comm->nccl, s.stream));
+    std::vector<int64_t> all(2 * P);
+    KR_HIP_CHECK(hipMemcpyAsync(all.data(), d + 2, all.size() * 8, hipMemcpyDeviceToHost,
+                                s.stream));
+    KR_HIP_CHECK(hipStreamSynchronize(s.stream));
+    KR_HIP_CHECK(hipFree(d));
+    for (int t = 0; t < P; ++t) {
+      lo[t] = all[2 * t];
+      hi[t] = all[2 * t + 1];
+    }
+  } else {
+    for (int t = 0; t < P; ++t) {
+      lo[t] = shards[t].col_lo;
+      hi[t] = shards[t].col_hi;
+    }
+  }
+  // 3. halo geometry and exchange plan
+  for (size_t li = 0; li < shards.size(); ++li) {
+    Shard& s = shards[li];
+    const int me = first_global + (int)li;
+    s.halo_lo = s.row0 - s.col_lo;
+    s.halo_hi = s.col_hi - (s.row0 + s.n - 1);
+    s.pad = (s.halo_lo + 7) / 8 * 8;
+    s.ld = s.pad + s.n + s.halo_hi;
+    s.ld = (s.ld + 7) / 8 * 8;
+    KR_REQUIRE(s.ld < (int64_t)INT32_MAX, "shard too large for 32-bit local columns");
+    plan_halo(P, part.data(), lo.data(), hi.data(), me, s.recv, s.send);
+    if (!comm) {
+      for (auto& p : s.recv) p.peer -= first_global;
+      s.send.clear();
+    }
+    // 4. rewrite columns to local numbering: local = global - row0 + pad
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    launch_col_shift(s.rowptr, s.rowptr64, s.n, s.col, s.pad - s.row0, s.stream);
+    // 5. reduction buffers
+    s.grid = default_grid(s.n);
+    KR_HIP_CHECK(hipMalloc(&s.partials, sizeof(double) * (size_t)kMaxSlots * s.grid));
+    KR_HIP_CHECK(hipMemsetAsync(s.partials, 0, sizeof(double) * (size_t)kMaxSlots * s.grid,
+                                s.stream));
+    KR_HIP_CHECK(hipMalloc(&s.slots, sizeof(double) * kMaxSlots));
+    KR_HIP_CHECK(hipMalloc(&s.gather, sizeof(double) * kMaxSlots * nranks));
+    KR_HIP_CHECK(hipHostMalloc(&s.host, sizeof(double) * kMaxSlots * nranks, 0));
+    if (!s.ev_a) KR_HIP_CHECK(hipEventCreateWithFlags(&s.ev_a, hipEventDisableTiming));
+    if (!s.ev_b) KR_HIP_CHECK(hipEventCreateWithFlags(&s.ev_b, hipEventDisableTiming));
+    KR_HIP_CHECK(hipStreamSynchronize(s.stream));
+  }
+  finalized = true;
+}
+
+void System::alloc_vectors(int count) {
+  for (auto& s : shards) {
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    KR_HIP_CHECK(hipStreamSynchronize(s.stream));
+    for (double* v : s.vec) KR_HIP_CHECK(hipFree(v));
+    s.vec.assign(count, nullptr);
+    for (int i = 0; i < count; ++i) {
+      if (hipMalloc(&s.vec[i], sizeof(double) * (size_t)s.ld) != hipSuccess)
+        throw Failure(KR_ERR_NOMEM, "vector allocation failed");
+      KR_HIP_CHECK(hipMemsetAsync(s.vec[i], 0, sizeof(double) * (size_t)s.ld, s.stream));
+    }
+    KR_HIP_CHECK(hipStreamSynchronize(s.stream));
+  }
+}
+
+void System::prof_begin(Shard& s, const char* name, hipEvent_t& t0) {
+  (void)name;
+  if (!profile) return;
+  if (s.event_pool.empty()) {
+    hipEvent_t e;
+    KR_HIP_CHECK(hipEventCreate(&e));
+    s.event_pool.push_back(e);
+  }
+  t0 = s.event_pool.back();
+  s.event_pool.pop_back();
+  KR_HIP_CHECK(hipEventRecord(t0, s.stream));
+}
+
+void System::prof_end(Shard& s, const char* name, hipEvent_t t0, double bytes) {
+  if (!profile) return;
+  if (s.event_pool.empty()) {
+    hipEvent_t e;
+    KR_HIP_CHECK(hipEventCreate(&e));
+    s.event_pool.push_back(e);
+  }
+  hipEvent_t t1 = s.event_pool.back();
+  s.event_pool.pop_back();
+  KR_HIP_CHECK(hipEventRecord(t1, s.stream));
+  s.pending.push_back({name, t0, t1});
+  s.stats[name].bytes = bytes;
+}
+
+void System::harvest_profile() {
+  if (!profile) return;
+  for (auto& s : shards) {
+    for (auto& p : s.pending) {
+      float ms = 0;
+      KR_HIP_CHECK(hipEventSynchronize(p.t1));
+      KR_HIP_CHECK(hipEventElapsedTime(&ms, p.t0, p.t1));
+      auto& st = s.stats[p.name];
+      st.launches += 1;
+      st.total_ms += ms;
+      s.event_pool.push_back(p.t0);
+      s.event_pool.push_back(p.t1);
+    }
+    s.pending.clear();
+  }
+}
+
+void System::halo(int id1, int id2) {
+  if (comm) {
+    Shard& s = shards[0];
+    if (s.recv.empty() && s.send.empty()) return;
+    hipEvent_t t0 = nullptr;
+    prof_begin(s, "halo", t0);
+    double bytes = 0;
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    KR_NCCL_CHECK(ncclGroupStart());
+    for (int id : {id1, id2}) {
+      if (id < 0) continue;
+      for (auto& p : s.send) {
+        KR_NCCL_CHECK(ncclSend(s.vec[id] + s.local_index(p.g0), (size_t)p.count, ncclFloat64,
+                               p.peer, comm->nccl, s.stream));
+        bytes += 8.0 * p.count;
+      }
+      for (auto& p : s.recv) {
+        KR_NCCL_CHECK(ncclRecv(s.vec[id] + s.local_index(p.g0), (size_t)p.count, ncclFloat64,
+                               p.peer, comm->nccl, s.stream));
+        bytes += 8.0 * p.count;
+      }
+    }
+    KR_NCCL_CHECK(ncclGroupEnd());
+    prof_end(s, "halo", t0, bytes);
+    return;
+  }
+  if (shards.size() < 2) return;
+  for (auto& s : shards) {
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    KR_HIP_CHECK(hipEventRecord(s.ev_a, s.stream));
+  }
+  for (auto& s : shards) {
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    for (auto& p : s.recv) {
+      Shard& t = shards[p.peer];
+      KR_HIP_CHECK(hipStreamWaitEvent(s.stream, t.ev_a, 0));
+      for (int id : {id1, id2}) {
+        if (id < 0) continue;
+        double* dst = s.vec[id] + s.local_index(p.g0);
+        const double* src = t.vec[id] + t.local_index(p.g0);
+        if (s.dev == t.dev)
+          KR_HIP_CHECK(hipMemcpyAsync(dst, src, 8 * (size_t)p.count, hipMemcpyDeviceToDevice,
+                                      s.stream));
+        else
+          KR_HIP_CHECK(hipMemcpyPeerAsync(dst, s.dev, src, t.dev, 8 * (size_t)p.count, s.stream));
+      }
+    }
+    KR_HIP_CHECK(hipEventRecord(s.ev_b, s.stream));
+  }
+  // Nobody overwrites a vector before every reader has copied its halo.
+  for (auto& t : shards) {
+    KR_HIP_CHECK(hipSetDevice(t.dev));
+    for (auto& s : shards)
+      if (&s != &t) KR_HIP_CHECK(hipStreamWaitEvent(t.stream, s.ev_b, 0));
+  }
+}
+
+void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int b,
+                  int slot0) {
+  const bool dual = (epi == EPI_DUAL_NONE || epi == EPI_DUAL_MRR || epi == EPI_DUAL_KCG);
+  KR_REQUIRE(slot0 + spmv_products(epi) <= kMaxSlots, "reduction slots exhausted");
+  halo(in1, dual ? in2 : -1);
+  for (auto& s : shards) {
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    SpmvArgs a;
+    a.rowptr = s.rowptr;
+    a.rowptr64 = s.rowptr64;
+    a.col = s.col;
+    a.val = s.val;
+    a.n = s.n;
+    a.x1 = s.vec[in1];
+    a.x2 = dual ? s.vec[in2] : nullptr;
+    a.xoff = s.pad;
+    a.y1 = s.own(out1);
+    a.y2 = dual ? s.own(out2) : nullptr;
+    a.b = b >= 0 ? s.own(b) : nullptr;
+    a.e = e >= 0 ? s.own(e) : nullptr;
+    a.partials = s.partials + (size_t)slot0 * s.grid;
+    a.grid = s.grid;
+    hipEvent_t t0 = nullptr;
+    const char* nm = epi_name(epi);
+    prof_begin(s, nm, t0);
+    launch_spmv(epi, a, s.stream);
+    if (profile) {
+      const double nv = dual ? 2.0 : 1.0;
+      const double extra = (b >= 0 || e >= 0) ? 8.0 * s.n : 0.0;
+      const double bytes = 12.0 * s.nnz + (s.rowptr64 ? 8.0 : 4.0) * (s.n + 1) +
+                           nv * 16.0 * s.n + extra;
+      prof_end(s, nm, t0, bytes);
+    }
+  }
+}
+
+void System::ew(EwOp op, double c0, double c1, std::array<int, 6> ids, int slot0) {
+  KR_REQUIRE(slot0 + ew_products(op) <= kMaxSlots, "reduction slots exhausted");
+  for (auto& s : shards) {
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    EwArgs a;
+    a.c0 = c0;
+    a.c1 = c1;
+    for (int q = 0; q < 6; ++q) a.p[q] = ids[q] >= 0 ? s.own(ids[q]) : nullptr;
+    a.n = s.n;
+    a.partials = s.partials + (size_t)slot0 * s.grid;
+    a.grid = s.grid;
+    hipEvent_t t0 = nullptr;
+    const char* nm = ew_name(op);
+    prof_begin(s, nm, t0);
+    launch_ew(op, a, s.stream);
+    prof_end(s, nm, t0, 8.0 * ew_vectors(op) * s.n);
+  }
+}
+
+void System::copy_own(int dst, int src) {
+  for (auto& s : shards) {
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    KR_HIP_CHECK(hipMemcpyAsync(s.own(dst), s.own(src), 8 * (size_t)s.n,
+                                hipMemcpyDeviceToDevice, s.stream));
+  }
+}
+
+std::vector<double> System::reduce(int nslots) {
+  std::vector<double> tot(nslots, 0.0);
+  if (nslots <= 0) return tot;
+  KR_REQUIRE(nslots <= kMaxSlots, "too many slots");
+  for (auto& s : shards) {
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    hipEvent_t t0 = nullptr;
+    prof_begin(s, "reduce", t0);
+    launch_finalize(s.partials, s.grid, nslots, s.slots, s.stream);
+    if (comm) {
+      KR_NCCL_CHECK(ncclAllGather(s.slots, s.gather, (size_t)nslots, ncclFloat64, comm->nccl,
+                                  s.stream));
+      KR_HIP_CHECK(hipMemcpyAsync(s.host, s.gather, sizeof(double) * nslots * comm->nranks,
+                                  hipMemcpyDeviceToHost, s.stream));
+    } else {
+      KR_HIP_CHECK(hipMemcpyAsync(s.host, s.slots, sizeof(double) * nslots,
+                                  hipMemcpyDeviceToHost, s.stream));
+    }
+    prof_end(s, "reduce", t0, 8.0 * nslots * s.grid);
+  }
+  for (auto& s : shards) {
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    KR_HIP_CHECK(hipStreamSynchronize(s.stream));
+  }
+  // Fixed order: global shard 0, 1, ... (identical for in-process and RCCL).
+  if (comm) {
+    const double* h = shards[0].host;
+    for (int r = 0; r < comm->nranks; ++r)
+      for (int q = 0; q < nslots; ++q) tot[q] = tot[q] + h[r * nslots + q];
+  } else {
+    for (auto& s : shards)
+      for (int q = 0; q < nslots; ++q) tot[q] = tot[q] + s.host[q];
+  }
+  harvest_profile();
+  return tot;
+}
+
+// ===========================================================================
+// Solver sessions
+// ===========================================================================
+namespace {
+
+class Base : public Session {
+ protected:
+  // Shared start-up: b, x0 into their vectors and ||b||.
+  void load_bx(int B, int X, const double* const* b, const double* const* x0) {
+    for (size_t li = 0; li < sys->shards.size(); ++li) {
+      Shard& s = sys->shards[li];
+      KR_HIP_CHECK(hipSetDevice(s.dev));
+      KR_REQUIRE(b && b[li], "b is required");
+      KR_HIP_CHECK(hipMemcpyAsync(s.own(B), b[li], 8 * (size_t)s.n, hipMemcpyDeviceToDevice,
+                                  s.stream));
+      if (x0 && x0[li])
+        KR_HIP_CHECK(hipMemcpyAsync(s.own(X), x0[li], 8 * (size_t)s.n,
+                                    hipMemcpyDeviceToDevice, s.stream));
+    }
+    sys->ew(EW_DOT, 0, 0, {B, B, -1, -1, -1, -1}, 0);
+    bnorm = std::sqrt(sys->reduce(1)[0]);
+  }
+  double rel(double sq) const { return std::sqrt(sq) / bnorm; }
+  void start_timer() { t_start = now_seconds(); }
+};
+
+// --------------------------------------------------------------------- CG
+// v3/gpu/cg.py:8-51 (oracle v3/cpu/cg.py:7-48)
+class CgSession : public Base {
+  enum { X, B, R, P, V, NV };
+  double gamma = 0;
+
+ public:
+  void begin(const double* const* b, const double* const* x0) override {
+    sys->alloc_vectors(NV);
+    load_bx(B, X, b, x0);
+    sys->spmv(EPI_BMINUS, X, -1, R, -1, -1, B, 0);  // r = b - A x
+    gamma = sys->reduce(1)[0];                      // gamma = <r,r>
+    sys->copy_own(P, R);                            // p = r.copy()
+    i = 0;
+    index = 0;
+    set_nosl(0, 0);
+    start_timer();
+  }
+  bool step_once() override {
+    if (i >= prm.maxiter) {  // while-else branch
+      set_entry(i, rel(gamma));
+      index = i;
+      return done = true;
+    }
+    set_entry(i, rel(gamma));
+    index = i;
+    if (residual[i] < prm.tol) {
+      converged = true;
+      return done = true;
+    }
+    sys->spmv(EPI_XY, P, -1, V, -1, -1, -1, 0);  // v = A p ; sigma = <p,v>
+    const double sigma = sys->reduce(3)[1];
+    const double alpha = gamma / sigma;
+    sys->ew(EW_CG, alpha, 0, {X, P, R, V, -1, -1}, 0);  // x += a p ; r -= a v
+    const double gnew = sys->reduce(1)[0];
+    const double beta = gnew / gamma;
+    gamma = gnew;
+    sys->ew(EW_CG_P, beta, 0, {P, R, -1, -1, -1, -1}, 0);  // p = r + b p
+    i += 1;
+    set_nosl(i, i);
+    index = i;
+    set_entry(i, 0.0);
+    return false;
+  }
+  int result_x() const override { return X; }
+};
+
+// --------------------------------------------------------------------- MrR
+// v3/gpu/mrr.py:8-65 (oracle v3/cpu/mrr.py:7-61)
+class MrrSession : public Base {
+  enum { X, B, R, Y, Z, AR, NV };
+
+ public:
+  void begin(const double* const* b, const double* const* x0) override {
+    sys->alloc_vectors(NV);
+    load_bx(B, X, b, x0);
+    sys->spmv(EPI_BMINUS, X, -1, R, -1, -1, B, 0);
+    set_entry(0, rel(sys->reduce(1)[0]));
+    set_nosl(0, 0);
+    start_timer();
+    sys->spmv(EPI_XY, R, -1, AR, -1, -1, -1, 0);  // Ar = A r
+    const auto g = sys->reduce(3);
+    const double zeta = g[1] / g[2];  // <r,Ar>/<Ar,Ar>
+    sys->ew(EW_MRR_FIRST, 0, zeta, {Y, AR, Z, R, X, X}, 0);
+    set_nosl(1, 1);
+    i = 1;
+    index = 1;
+    set_entry(1, 0.0);
+  }
+  bool step_once() override {
+    if (i >= prm.maxiter) {
+      sys->ew(EW_DOT, 0, 0, {R, R, -1, -1, -1, -1}, 0);
+      set_entry(i, rel(sys->reduce(1)[0]));
+      index = i;
+      return done = true;
+    }
+    sys->spmv(EPI_MRR_LOOP, R, -1, AR, -1, Y, -1, 0);  // Ar = A r ; <r,r> mu nu
+    const auto g = sys->reduce(3);
+    set_entry(i, rel(g[0]));
+    index = i;
+    if (residual[i] < prm.tol) {
+      converged = true;
+      return done = true;
+    }
+    const double gamma = g[2] / g[1];  // nu / mu
+    sys->ew(EW_MRR_S, gamma, 0, {AR, Y, R, -1, -1, -1}, 0);
+    const auto h = sys->reduce(2);
+    const double zeta = h[0] / h[1];
+    const double eta = (-zeta) * gamma;
+    sys->ew(EW_MRR, eta, zeta, {Y, AR, Z, R, X, X}, 0);
+    i += 1;
+    set_nosl(i, i);
+    index = i;
+    set_entry(i, 0.0);
+    return false;
+  }
+  int result_x() const override { return X; }
+};
+
+// ------------------------------------------------------------ k-skip MrR
+// v3/gpu/kskipmrr.py:9-110 (oracle v3/cpu/kskipmrr.py:8-108) and, with
+// adaptive = true, v3/cpu/adaptivekskipmrr.py:8-141 semantics.
+class KskipMrrSession : public Base {
+  // vector ids: fixed ones, then Ar[0..k0+1], Ay[0..k0]
+  enum { XA, XB, B, Z, FIXED };
+  int k0 = 0;
+  bool adaptive = false;
+  int cur = XA, pre = XB;  // current x buffer / adaptive snapshot buffer
+  int xsrc = XA;           // source of the next x update
+  double pre_residual = 0;
+  int AR(int j) const { return FIXED + j; }
+  int AY(int j) const { return FIXED + (k0 + 2) + j; }
+  static constexpr int kHead = 5;
+  int gram_slots(int kk) const { return kHead + 7 * kk; }
+
+  void head() { sys->spmv(EPI_HEAD_MRR, AR(0), -1, AR(1), -1, AY(0), -1, 0); }
+  void chain(int kk) {
+    for (int m = 0; m < kk; ++m)
+      sys->spmv(EPI_DUAL_MRR, AR(m + 1), AY(m), AR(m + 2), AY(m + 1), -1, -1, kHead + 7 * m);
+  }
+  // Initial / restart MrR step (v3/cpu/kskipmrr.py:26-31).
+  void mrr_first(int x_from) {
+    sys->spmv(EPI_XY, AR(0), -1, AR(1), -1, -1, -1, 0);
+    const auto g = sys->reduce(3);
+    const double zeta = g[1] / g[2];
+    sys->ew(EW_MRR_FIRST, 0, zeta, {AY(0), AR(1), Z, AR(0), x_from, cur}, 0);
+    xsrc = cur;
+  }
+
+ public:
+  explicit KskipMrrSession(bool adapt) : adaptive(adapt) {}
+
+  void begin(const double* const* b, const double* const* x0) override {
+    k = prm.k;
+    k0 = k;
+    KR_REQUIRE(k >= 0 && gram_slots(k) <= kMaxSlots, "k out of range");
+    sys->alloc_vectors(FIXED + (k0 + 2) + (k0 + 1));
+    load_bx(B, XA, b, x0);
+    if (adaptive) sys->copy_own(XB, XA);  // pre_x guard = x0
+    sys->spmv(EPI_BMINUS, XA, -1, AR(0), -1, -1, B, 0);
+    set_entry(0, rel(sys->reduce(1)[0]));
+    pre_residual = residual[0];
+    set_nosl(0, 0);
+    track_k = adaptive;
+    if (adaptive) set_k(0, k);
+    start_timer();
+    mrr_first(XA);
+    set_nosl(1, 1);
+    if (adaptive) set_k(1, k);
+    i = 1;
+    index = 1;
+    set_entry(1, 0.0);
+    head();
+  }
+
+  bool step_once() override {
+    if (i >= prm.maxiter) {
+      set_entry(index, rel(sys->reduce(kHead)[0]));
+      return done = true;
+    }
+    chain(k);  // speculative: launched before the convergence test
+    std::vector<double> g = sys->reduce(gram_slots(k));
+    set_entry(index, rel(g[0]));
+    if (adaptive) {
+      if (residual[index] > pre_residual) {
+        // roll back to the snapshot and restart (v3/cpu/adaptivekskipmrr.py:45-66)
+        sys->spmv(EPI_BMINUS, pre, -1, AR(0), -1, -1, B, 0);
+        mrr_first(pre);
+        i += 1;
+        index += 1;
+        head();
+        const int knew = k > 1 ? k - 1 : k;
+        chain(knew);
+        g = sys->reduce(gram_slots(knew));
+        set_entry(index, rel(g[0]));
+        set_nosl(index, i);
+        k = knew;
+        set_k(index, k);
+      } else {
+        pre_residual = residual[index];
+        std::swap(cur, pre);  // pre_x = x.copy(): the next update writes the other buffer
+        xsrc = pre;
+      }
+    }
+    if (residual[index] < prm.tol) {
+      converged = true;
+      return done = true;
+    }
+    // Gram -> (alpha, beta, delta) as the reference lays them out.
+    std::vector<double> alpha(2 * k + 3, 0.0), beta(2 * k + 2, 0.0), delta(2 * k + 1, 0.0);
+    alpha[0] = g[0];
+    alpha[1] = g[1];
+    alpha[2] = g[2];
+    beta[1] = g[3];
+    delta[0] = g[4];
+    for (int m = 0; m < k; ++m) {
+      const double* d = &g[kHead + 7 * m];
+      alpha[2 * m + 3] = d[0];
+      alpha[2 * m + 4] = d[1];
+      delta[2 * m + 2] = d[2];
+      delta[2 * m + 1] = d[3];
+      beta[2 * m + 3] = d[4];
+      if (m > 0) beta[2 * m + 1] = d[5];  // same bits as the previous step's d[4]
+      beta[2 * m + 2] = d[6];
+    }
+    std::vector<double> zeta(k + 1), eta(k + 1);
+    kskipmrr_recurrence(k, alpha.data(), beta.data(), delta.data(), zeta.data(), eta.data());
+    for (int j = 0; j <= k; ++j) {
+      sys->ew(EW_MRR, eta[j], zeta[j], {AY(0), AR(1), Z, AR(0), xsrc, cur}, 0);
+      xsrc = cur;
+      if (j < k)
+        sys->spmv(EPI_NONE, AR(0), -1, AR(1), -1, -1, -1, 0);
+      else
+        head();
+    }
+    i += k + 1;
+    index += 1;
+    set_nosl(index, i);
+    if (adaptive) set_k(index, k);
+    set_entry(index, 0.0);
+    return false;
+  }
+  int result_x() const override { return xsrc; }
+};
+
+// ------------------------------------------------------------- k-skip CG
+// v3/gpu/kskipcg.py:9-92 (oracle v3/cpu/kskipcg.py:8-87)
+class KskipCgSession : public Base {
+  enum { X, B, FIXED };
+  int AR(int j) const { return FIXED + j; }
+  int AP(int j) const { return FIXED + (k + 2) + j; }
+  static constexpr int kHead = 6;
+  int gram_slots() const { return kHead + 7 * k; }
+  void head() { sys->spmv(EPI_HEAD_KCG, AP(0), -1, AP(1), -1, AR(0), -1, 0); }
+
+ public:
+  void begin(const double* const* b, const double* const* x0) override {
+    k = prm.k;
+    KR_REQUIRE(k >= 0 && gram_slots() <= kMaxSlots, "k out of range");
+    sys->alloc_vectors(FIXED + (k + 2) + (k + 3));
+    load_bx(B, X, b, x0);
+    sys->spmv(EPI_BMINUS, X, -1, AR(0), -1, -1, B, 0);  // Ar[0] = b - A x
+    sys->reduce(1);
+    sys->copy_own(AP(0), AR(0));  // Ap[0] = Ar[0]
+    i = 0;
+    index = 0;
+    set_nosl(0, 0);
+    set_entry(0, 0.0);
+    start_timer();
+    head();
+  }
+  bool step_once() override {
+    if (i >= prm.maxiter) {
+      set_entry(index, rel(sys->reduce(kHead)[0]));
+      return done = true;
+    }
+    for (int j = 1; j <= k; ++j)
+      sys->spmv(EPI_DUAL_KCG, AR(j - 1), AP(j), AR(j), AP(j + 1), -1, -1, kHead + 7 * (j - 1));
+    const std::vector<double> g = sys->reduce(gram_slots());
+    set_entry(index, rel(g[0]));
+    if (residual[index] < prm.tol) {
+      converged = true;
+      return done = true;
+    }
+    std::vector<double> a(2 * k + 2, 0.0), f(2 * k + 4, 0.0), c(2 * k + 2, 0.0);
+    a[0] = g[0];
+    f[0] = g[1];
+    f[1] = g[2];
+    f[2] = g[3];
+    c[0] = g[4];
+    c[1] = g[5];
+    for (int j = 1; j <= k; ++j) {
+      const double* d = &g[kHead + 7 * (j - 1)];
+      a[2 * j - 1] = d[0];
+      a[2 * j] = d[1];
+      f[2 * j + 1] = d[2];
+      f[2 * j + 2] = d[3];
+      c[2 * j - 1] = d[4];
+      c[2 * j] = d[5];
+      c[2 * j + 1] = d[6];
+    }
+    // f[2k+3] = <Ap[k+1], Ap[k+2]> with Ap[k+2] never computed: 0.
+    std::vector<double> al(k + 1), be(k + 1);
+    kskipcg_recurrence(k, a.data(), f.data(), c.data(), al.data(), be.data());
+    for (int j = 0; j <= k; ++j) {
+      sys->ew(EW_KCG, al[j], be[j], {X, AP(0), AR(0), AP(1), -1, -1}, 0);
+      if (j < k)
+        sys->spmv(EPI_NONE, AP(0), -1, AP(1), -1, -1, -1, 0);
+      else
+        head();
+    }
+    i += k + 1;
+    index += 1;
+    set_nosl(index, i);
+    set_entry(index, 0.0);
+    return false;
+  }
+  int result_x() const override { return X; }
+};
+
+}  // namespace
+
+std::unique_ptr<Session> make_session(System* sys, const kr_solve_params& p) {
+  std::unique_ptr<Session> s;
+  switch (p.method) {
+    case KR_METHOD_CG: s.reset(new CgSession()); break;
+    case KR_METHOD_MRR: s.reset(new MrrSession()); break;
+    case KR_METHOD_KSKIPCG: s.reset(new KskipCgSession()); break;
+    case KR_METHOD_KSKIPMRR: s.reset(new KskipMrrSession(false)); break;
+    case KR_METHOD_ADAPTIVE_KSKIPMRR: s.reset(new KskipMrrSession(true)); break;
+    default: throw Failure(KR_ERR_INVALID, "unknown method");
+  }
+  s->sys = sys;
+  s->prm = p;
+  if (s->prm.maxiter <= 0) s->prm.maxiter = sys->n_global;
+  return s;
+}
+
+}  // namespace kr

@@ -1,0 +1,164 @@
+// Host engine: sharded system, halo exchange, deterministic reductions and
+// the solver sessions. One host thread drives every shard the process owns.
+#pragma once
+
+#include <rccl/rccl.h>
+
+#include <array>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "kr_internal.h"
+
+namespace kr {
+
+void kskipmrr_recurrence(int k, double* alpha, double* beta, double* delta, double* zeta_out,
+                         double* eta_out);
+void kskipcg_recurrence(int k, double* a, double* f, double* c, double* alpha_out,
+                        double* beta_out);
+
+// RCCL communicator, one rank per GPU.
+struct Comm {
+  ncclComm_t nccl = nullptr;
+  int rank = 0, nranks = 1, device = 0;
+};
+
+#define KR_NCCL_CHECK(expr)                                                              \
+  do {                                                                                   \
+    ncclResult_t kr_r_ = (expr);                                                         \
+    if (kr_r_ != ncclSuccess)                                                            \
+      throw ::kr::Failure(KR_ERR_RCCL, std::string(#expr) + " -> " +                     \
+                                           ncclGetErrorString(kr_r_));                   \
+  } while (0)
+
+// Slots of fused reduction products per shard (enough for k <= 16).
+constexpr int kMaxSlots = 6 + 7 * 16 + 8;
+
+// A contiguous range of global rows exchanged with one peer shard/rank.
+struct HaloPiece {
+  int peer;        // local shard index (in-process) or rank (RCCL)
+  int64_t g0;      // first global row
+  int64_t count;   // rows
+};
+
+struct KernelStat {
+  int64_t launches = 0;
+  double total_ms = 0;
+  double bytes = 0;
+};
+
+struct Shard {
+  int dev = 0;
+  hipStream_t stream = nullptr;
+  int64_t row0 = 0, n = 0;
+  // CSR block (global columns until finalize, local afterwards)
+  const void* rowptr = nullptr;
+  int rowptr64 = 0;
+  int32_t* col = nullptr;
+  const double* val = nullptr;
+  int64_t nnz = 0;
+  std::vector<void*> owned;
+  // halo geometry: vector = [pad | n own rows | halo_hi]; halo_lo rows sit
+  // just below the own rows (pad >= halo_lo, pad multiple of 8).
+  int64_t col_lo = 0, col_hi = -1;
+  int64_t halo_lo = 0, halo_hi = 0, pad = 0, ld = 0;
+  std::vector<HaloPiece> recv, send;
+  int grid = 1;
+  // reductions
+  double* partials = nullptr;   // [kMaxSlots][grid]
+  double* slots = nullptr;      // [kMaxSlots]
+  double* gather = nullptr;     // [nranks][kMaxSlots] (RCCL)
+  double* host = nullptr;       // pinned [nranks][kMaxSlots]
+  // vectors, each ld doubles, zero-initialised
+  std::vector<double*> vec;
+  hipEvent_t ev_a = nullptr, ev_b = nullptr;
+  // profiling (event pairs pending until the next sync)
+  struct Pending {
+    std::string name;
+    hipEvent_t t0, t1;
+  };
+  std::vector<Pending> pending;
+  std::vector<hipEvent_t> event_pool;
+  std::map<std::string, KernelStat> stats;
+
+  double* own(int id) const { return vec[id] + pad; }
+  int64_t local_index(int64_t g) const { return g - row0 + pad; }
+};
+
+class Session;
+
+// Exchange plan of global shard `me`: the rows it receives from / sends to
+// every other shard, as contiguous global ranges (pure host arithmetic).
+void plan_halo(int P, const int64_t* part, const int64_t* need_lo, const int64_t* need_hi,
+               int me, std::vector<HaloPiece>& recv, std::vector<HaloPiece>& send);
+
+struct System {
+  int64_t n_global = 0;
+  std::vector<Shard> shards;
+  Comm* comm = nullptr;             // null: single process
+  std::vector<int64_t> part;        // global partition, size P+1
+  int first_global = 0;             // global index of shards[0]
+  bool finalized = false;
+  bool profile = false;
+  std::unique_ptr<Session> session;
+
+  ~System();
+  int nglobal_shards() const { return (int)part.size() - 1; }
+
+  void finalize();
+  void alloc_vectors(int count);
+  // Halo exchange of up to two vectors (ids), all shards.
+  void halo(int id1, int id2 = -1);
+  void spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int b, int slot0);
+  void ew(EwOp op, double c0, double c1, std::array<int, 6> ids, int slot0);
+  // Device->host of the summed slots [0, nslots): the one host sync point.
+  std::vector<double> reduce(int nslots);
+  void copy_own(int dst, int src);
+  void harvest_profile();
+
+  // profiling helpers
+  void prof_begin(Shard& s, const char* name, hipEvent_t& t0);
+  void prof_end(Shard& s, const char* name, hipEvent_t t0, double bytes);
+};
+
+// Solver session interface (one per kr_solve_begin).
+class Session {
+ public:
+  virtual ~Session() = default;
+  virtual void begin(const double* const* b, const double* const* x0) = 0;
+  // Returns true when done.
+  virtual bool step_once() = 0;
+  virtual int result_x() const = 0;  // vector id holding the solution
+
+  System* sys = nullptr;
+  kr_solve_params prm{};
+  int k = 0;
+  double bnorm = 0;
+  int64_t i = 0, index = 0;
+  bool done = false, converged = false;
+  std::vector<double> residual;
+  std::vector<int64_t> nosl, khist;
+  bool track_k = false;
+  double t_start = 0, t_end = 0;
+
+  void set_entry(int64_t idx, double res) {
+    if ((int64_t)residual.size() <= idx) residual.resize(idx + 1, 0.0);
+    residual[idx] = res;
+  }
+  void set_nosl(int64_t idx, int64_t v) {
+    if ((int64_t)nosl.size() <= idx) nosl.resize(idx + 1, 0);
+    nosl[idx] = v;
+  }
+  void set_k(int64_t idx, int64_t v) {
+    if ((int64_t)khist.size() <= idx) khist.resize(idx + 1, 0);
+    khist[idx] = v;
+  }
+  int64_t entries() const { return index + 1; }
+};
+
+std::unique_ptr<Session> make_session(System* sys, const kr_solve_params& p);
+double now_seconds();
+
+}  // namespace kr

@@ -1,0 +1,157 @@
+// Internal declarations shared by the HIP kernels and the host engine.
+// Nothing in here crosses the C ABI (include/krylov_amd.h is the boundary).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+#include "../../include/krylov_amd.h"
+
+namespace kr {
+
+// Rows per row-block == threads per block: one lane owns one row so every
+// row is summed sequentially in stored order (scipy csr_matvec order).
+constexpr int kBlock = 256;
+// Matrix entries staged in LDS per window (vals 16 KiB + cols 8 KiB).
+constexpr int kWindow = 2048;
+// Upper bound on fused reduction products in one kernel.
+constexpr int kMaxProducts = 8;
+
+struct Failure : std::runtime_error {
+  int code;
+  Failure(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define KR_HIP_CHECK(expr)                                                        \
+  do {                                                                            \
+    hipError_t kr_e_ = (expr);                                                    \
+    if (kr_e_ != hipSuccess)                                                      \
+      throw ::kr::Failure(KR_ERR_HIP, std::string(#expr) + " -> " +               \
+                                          hipGetErrorString(kr_e_) + " at " +     \
+                                          __FILE__ ":" + std::to_string(__LINE__)); \
+  } while (0)
+
+#define KR_REQUIRE(cond, msg)                                        \
+  do {                                                               \
+    if (!(cond)) throw ::kr::Failure(KR_ERR_INVALID, std::string(msg)); \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// SpMV with fused epilogue reductions.
+// Operand names used by the product tables (per own row r):
+//   X1, X2 : the SpMV inputs at row r      Y1, Y2 : the SpMV results at row r
+//   E      : an extra vector at row r (own-row indexing)
+// ---------------------------------------------------------------------------
+enum SpmvEpi : int {
+  EPI_NONE = 0,   // y = A x
+  EPI_BMINUS,     // y = b - A x ; <y,y>
+  EPI_XY,         // <x,x> <x,y> <y,y>
+  EPI_HEAD_MRR,   // <x,x> <x,y> <y,y> <e,y> <e,e>       (x=Ar0 y=Ar1 e=Ay0)
+  EPI_HEAD_KCG,   // <e,e> <x,x> <x,y> <y,y> <e,x> <e,y> (x=Ap0 y=Ap1 e=Ar0)
+  EPI_MRR_LOOP,   // <x,x> <e,e> <e,y>                   (x=r  y=Ar  e=y)
+  EPI_DUAL_NONE,  // y1 = A x1, y2 = A x2
+  EPI_DUAL_MRR,   // 7 products, see kernels
+  EPI_DUAL_KCG,   // 7 products, see kernels
+};
+int spmv_products(SpmvEpi epi);
+
+struct SpmvArgs {
+  const void* rowptr = nullptr;
+  int rowptr64 = 0;
+  const int32_t* col = nullptr;
+  const double* val = nullptr;
+  int64_t n = 0;               // rows
+  const double* x1 = nullptr;  // indexed by col (halo-extended vector base)
+  const double* x2 = nullptr;
+  int64_t xoff = 0;            // own row 0 sits at x[xoff]
+  double* y1 = nullptr;        // own rows
+  double* y2 = nullptr;
+  const double* b = nullptr;   // own rows (EPI_BMINUS)
+  const double* e = nullptr;   // own rows (extra operand)
+  double* partials = nullptr;  // products: partials[p * grid + block]
+  int grid = 0;
+};
+void launch_spmv(SpmvEpi epi, const SpmvArgs& a, hipStream_t s);
+
+// ---------------------------------------------------------------------------
+// Elementwise vector steps with fused reductions (all own-row pointers).
+// ---------------------------------------------------------------------------
+enum EwOp : int {
+  EW_DOT = 0,     // <u,v>                                   (p0 = u, p1 = v)
+  EW_MRR_FIRST,   // y = zeta*ar1; z = (-zeta)*r; r -= y; xd = xs - z
+  EW_MRR,         // y = eta*y + zeta*ar1; z = eta*z - zeta*r; r -= y; xd = xs - z
+  EW_CG,          // x += alpha*p; r -= alpha*v; <r,r>
+  EW_CG_P,        // p = r + beta*p
+  EW_KCG,         // x += alpha*ap0; r -= alpha*ap1; ap0 = r + beta*ap0
+  EW_MRR_S,       // s = ar - gamma*y; <r,s> <s,s>   (s not stored)
+  EW_COPY,        // p0 <- p1
+};
+int ew_products(EwOp op);
+
+struct EwArgs {
+  double c0 = 0, c1 = 0;           // scalars (eta/alpha/gamma, zeta/beta)
+  double* p[6] = {};               // operand pointers, meaning per op
+  int64_t n = 0;
+  double* partials = nullptr;
+  int grid = 0;
+};
+void launch_ew(EwOp op, const EwArgs& a, hipStream_t s);
+
+// Sum partials[slot*grid .. +grid) for slots [0, nslots) into out[slot],
+// in a fixed order (deterministic).
+void launch_finalize(const double* partials, int grid, int nslots, double* out,
+                     hipStream_t s);
+
+// Many independent dot products in one pass (count <= 64).
+struct MultiDotArgs {
+  const double* u[64];
+  const double* v[64];
+  int count;
+  int64_t n;
+  double* partials;
+  int grid;
+};
+void launch_multidot(const MultiDotArgs& a, hipStream_t s);
+
+// ---------------------------------------------------------------------------
+// Synthetic generators (rows [row0, row0+n) of the global matrix).
+// ---------------------------------------------------------------------------
+// Poisson: counts (rowptr[i+1] = nnz of row i) then fill after the scan.
+void launch_poisson_count(int dim, int64_t side, int64_t row0, int64_t n, void* rowptr,
+                          int rowptr64, hipStream_t s);
+void launch_poisson_fill(int dim, int64_t side, int64_t row0, int64_t n,
+                         const void* rowptr, int rowptr64, int32_t* col, double* val,
+                         hipStream_t s);
+struct BandSpec {
+  int h;
+  int64_t off[64];  // sorted ascending, distinct, >= 1
+  uint64_t seed;
+  int64_t n_global;
+};
+void launch_banded_count(const BandSpec& b, int64_t row0, int64_t n, void* rowptr,
+                         int rowptr64, hipStream_t s);
+void launch_banded_fill(const BandSpec& b, int64_t row0, int64_t n, const void* rowptr,
+                        int rowptr64, int32_t* col, double* val, hipStream_t s);
+// In-place inclusive scan of rowptr[1..n] (rowptr[0] = 0 set by the caller).
+void rowptr_scan(void* rowptr, int rowptr64, int64_t n, hipStream_t s);
+void launch_fill_rhs(uint64_t seed, int64_t row0, int64_t n, double* b, hipStream_t s);
+// Column statistics of a CSR block: min and max column (global numbering).
+void launch_col_minmax(const void* rowptr, int rowptr64, int64_t n, const int32_t* col,
+                       int64_t* out2 /* device: {min, max} */, hipStream_t s);
+// col[j] += delta for all stored entries of the block.
+void launch_col_shift(const void* rowptr, int rowptr64, int64_t n, int32_t* col,
+                      int64_t delta, hipStream_t s);
+
+// Host-side helpers shared with the oracle definition.
+uint64_t splitmix64(uint64_t x);
+void banded_offsets(int h, int64_t width, uint64_t seed, int64_t* out_sorted);
+
+// Scratch for the primitive entry points (grown on demand, per device).
+double* primitive_scratch(size_t doubles);
+
+int default_grid(int64_t n);
+
+}  // namespace kr

@@ -1,0 +1,776 @@
+// CDNA4 (gfx950) kernels for the Krylov inner loop.
+//
+// Numerics contract: this file is compiled with
+// -ffp-contract=off, so every `a*b + c` below rounds the product and the sum
+// separately, exactly like the numpy statements of the reference
+// (v3/cpu/*.py, v3/gpu/*.py). SpMV rows are summed by one lane, sequentially,
+// in stored order, starting from 0.0 -- the order of scipy's csr_matvec -- so
+// y = A x is bitwise equal to scipy. Dot products use a fixed two-stage tree
+// (per-block partials, then kr::launch_finalize), so they are deterministic
+// run to run, but they are not OpenBLAS's order.
+#include <hipcub/hipcub.hpp>
+
+#include "kr_hash.h"
+#include "kr_internal.h"
+
+namespace kr {
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Block-level deterministic reduction of NP per-thread accumulators into
+// partials[p * grid + blockIdx.x].
+// ---------------------------------------------------------------------------
+template <int NP>
+__device__ __forceinline__ void block_reduce_store(double (&acc)[NP > 0 ? NP : 1],
+                                                   double* partials, int grid,
+                                                   double* s_red /* NP*4 */) {
+  if constexpr (NP > 0) {
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      double v = acc[p];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+      if (lane == 0) s_red[p * 4 + wave] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < NP) {
+      const double* r = s_red + threadIdx.x * 4;
+      double t = r[0];
+      t = t + r[1];
+      t = t + r[2];
+      t = t + r[3];
+      partials[(int64_t)threadIdx.x * grid + blockIdx.x] = t;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// SpMV epilogue product tables.
+// ---------------------------------------------------------------------------
+template <int EPI>
+struct EpiTraits;
+template <>
+struct EpiTraits<EPI_NONE> {
+  static constexpr int NP = 0, NV = 1;
+  static constexpr bool kX = false, kX2 = false, kE = false;
+};
+template <>
+struct EpiTraits<EPI_BMINUS> {
+  static constexpr int NP = 1, NV = 1;
+  static constexpr bool kX = false, kX2 = false, kE = false;
+};
+template <>
+struct EpiTraits<EPI_XY> {
+  static constexpr int NP = 3, NV = 1;
+  static constexpr bool kX = true, kX2 = false, kE = false;
+};
+template <>
+struct EpiTraits<EPI_HEAD_MRR> {
+  static constexpr int NP = 5, NV = 1;
+  static constexpr bool kX = true, kX2 = false, kE = true;
+};
+template <>
+struct EpiTraits<EPI_HEAD_KCG> {
+  static constexpr int NP = 6, NV = 1;
+  static constexpr bool kX = true, kX2 = false, kE = true;
+};
+template <>
+struct EpiTraits<EPI_MRR_LOOP> {
+  static constexpr int NP = 3, NV = 1;
+  static constexpr bool kX = true, kX2 = false, kE = true;
+};
+template <>
+struct EpiTraits<EPI_DUAL_NONE> {
+  static constexpr int NP = 0, NV = 2;
+  static constexpr bool kX = false, kX2 = false, kE = false;
+};
+template <>
+struct EpiTraits<EPI_DUAL_MRR> {
+  static constexpr int NP = 7, NV = 2;
+  static constexpr bool kX = true, kX2 = true, kE = false;
+};
+template <>
+struct EpiTraits<EPI_DUAL_KCG> {
+  static constexpr int NP = 7, NV = 2;
+  static constexpr bool kX = true, kX2 = true, kE = false;
+};
+
+// Products of one row. x/x2: inputs at the row, y/y2: results, e: extra.
+template <int EPI>
+__device__ __forceinline__ void epi_products(double x, double x2, double y, double y2,
+                                             double e,
+                                             double (&acc)[EpiTraits<EPI>::NP > 0
+                                                               ? EpiTraits<EPI>::NP
+                                                               : 1]) {
+  if constexpr (EPI == EPI_BMINUS) {
+    acc[0] += y * y;
+  } else if constexpr (EPI == EPI_XY) {
+    acc[0] += x * x;
+    acc[1] += x * y;
+    acc[2] += y * y;
+  } else if constexpr (EPI == EPI_HEAD_MRR) {  // x=Ar0 y=Ar1 e=Ay0
+    acc[0] += x * x;                           // alpha[0]
+    acc[1] += x * y;                           // alpha[1]
+    acc[2] += y * y;                           // alpha[2]
+    acc[3] += e * y;                           // beta[1]
+    acc[4] += e * e;                           // delta[0]
+  } else if constexpr (EPI == EPI_HEAD_KCG) {  // x=Ap0 y=Ap1 e=Ar0
+    acc[0] += e * e;                           // a[0]
+    acc[1] += x * x;                           // f[0]
+    acc[2] += x * y;                           // f[1]
+    acc[3] += y * y;                           // f[2]
+    acc[4] += e * x;                           // c[0]
+    acc[5] += e * y;                           // c[1]
+  } else if constexpr (EPI == EPI_MRR_LOOP) {  // x=r y=Ar e=y
+    acc[0] += x * x;                           // <r,r>
+    acc[1] += e * e;                           // mu
+    acc[2] += e * y;                           // nu
+  } else if constexpr (EPI == EPI_DUAL_MRR) {  // x=Ar[m+1] x2=Ay[m] y=Ar[m+2] y2=Ay[m+1]
+    acc[0] += x * y;                           // alpha[2m+3]
+    acc[1] += y * y;                           // alpha[2m+4]
+    acc[2] += y2 * y2;                         // delta[2m+2]
+    acc[3] += x2 * y2;                         // delta[2m+1]
+    acc[4] += y2 * y;                          // beta[2m+3]
+    acc[5] += x2 * x;                          // beta[2m+1]
+    acc[6] += y2 * x;                          // beta[2m+2]
+  } else if constexpr (EPI == EPI_DUAL_KCG) {  // x=Ar[j-1] x2=Ap[j] y=Ar[j] y2=Ap[j+1]
+    acc[0] += x * y;                           // a[2j-1]
+    acc[1] += y * y;                           // a[2j]
+    acc[2] += x2 * y2;                         // f[2j+1]
+    acc[3] += y2 * y2;                         // f[2j+2]
+    acc[4] += x * x2;                          // c[2j-1]
+    acc[5] += y * x2;                          // c[2j]
+    acc[6] += y * y2;                          // c[2j+1]
+  }
+}
+
+// ---------------------------------------------------------------------------
+// CSR SpMV, one lane per row, matrix entries staged through LDS.
+//   Row block = kBlock consecutive rows; its nnz range is copied into LDS in
+//   windows of kWindow entries with coalesced loads, then each lane walks its
+//   own row inside the window in stored order and gathers x[col].
+//   Grid-stride over row blocks; reductions accumulate per lane across row
+//   blocks and are reduced once per workgroup at the end.
+// ---------------------------------------------------------------------------
+template <typename RP, int EPI>
+__global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
+  using T = EpiTraits<EPI>;
+  constexpr int NP = T::NP;
+  constexpr int NV = T::NV;
+  __shared__ double s_val[kWindow];
+  __shared__ int32_t s_col[kWindow];
+  __shared__ int64_t s_rp[kBlock + 1];
+  __shared__ double s_red[(NP > 0 ? NP : 1) * 4];
+
+  const RP* __restrict__ rowptr = static_cast<const RP*>(a.rowptr);
+  const double* __restrict__ val = a.val;
+  const int32_t* __restrict__ col = a.col;
+  const double* __restrict__ x1 = a.x1;
+  const double* __restrict__ x2 = a.x2;
+  const int tid = threadIdx.x;
+
+  double acc[NP > 0 ? NP : 1];
+#pragma unroll
+  for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;
+
+  const int64_t nrb = (a.n + kBlock - 1) / kBlock;
+  for (int64_t rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
+    const int64_t r0 = rb * kBlock;
+    const int nr = (int)min((int64_t)kBlock, a.n - r0);
+    if (tid < nr) s_rp[tid] = (int64_t)rowptr[r0 + tid];
+    if (tid == 0) s_rp[nr] = (int64_t)rowptr[r0 + nr];
+    __syncthreads();
+    const int64_t bs = s_rp[0], be = s_rp[nr];
+    const bool active = tid < nr;
+    const int64_t rs = active ? s_rp[tid] : 0;
+    const int64_t re = active ? s_rp[tid + 1] : 0;
+    double sum1 = 0.0, sum2 = 0.0;
+    for (int64_t ws = bs; ws < be; ws += kWindow) {
+      const int wn = (int)min((int64_t)kWindow, be - ws);
+      for (int j = tid; j < wn; j += kBlock) {
+        s_val[j] = __builtin_nontemporal_load(val + ws + j);
+        s_col[j] = __builtin_nontemporal_load(col + ws + j);
+      }
+      __syncthreads();
+      if (active) {
+        const int js = (int)max(rs - ws, (int64_t)0);
+        const int je = (int)min(re - ws, (int64_t)wn);
+        for (int j = js; j < je; ++j) {
+          const double v = s_val[j];
+          const int c = s_col[j];
+          sum1 = sum1 + v * x1[c];
+          if constexpr (NV == 2) sum2 = sum2 + v * x2[c];
+        }
+      }
+      __syncthreads();
+    }
+    if (active) {
+      const int64_t row = r0 + tid;
+      double y1 = sum1;
+      if constexpr (EPI == EPI_BMINUS) y1 = a.b[row] - sum1;
+      a.y1[row] = y1;
+      if constexpr (NV == 2) a.y2[row] = sum2;
+      if constexpr (NP > 0) {
+        const double xv = T::kX ? x1[a.xoff + row] : 0.0;
+        const double x2v = T::kX2 ? x2[a.xoff + row] : 0.0;
+        const double ev = T::kE ? a.e[row] : 0.0;
+        epi_products<EPI>(xv, x2v, y1, sum2, ev, acc);
+      }
+    }
+    __syncthreads();  // s_rp is rewritten by the next row block
+  }
+  block_reduce_store<NP>(acc, a.partials, a.grid, s_red);
+}
+
+template <typename RP>
+void spmv_dispatch(SpmvEpi epi, const SpmvArgs& a, hipStream_t s) {
+  const dim3 grid(a.grid), block(kBlock);
+  switch (epi) {
+#define KR_CASE(E) \
+  case E:          \
+    spmv_kernel<RP, E><<<grid, block, 0, s>>>(a); \
+    break;
+    KR_CASE(EPI_NONE)
+    KR_CASE(EPI_BMINUS)
+    KR_CASE(EPI_XY)
+    KR_CASE(EPI_HEAD_MRR)
+    KR_CASE(EPI_HEAD_KCG)
+    KR_CASE(EPI_MRR_LOOP)
+    KR_CASE(EPI_DUAL_NONE)
+    KR_CASE(EPI_DUAL_MRR)
+    KR_CASE(EPI_DUAL_KCG)
+#undef KR_CASE
+    default:
+      throw Failure(KR_ERR_INVALID, "unknown SpMV epilogue");
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Elementwise vector steps. Operand slots p[0..5]; READ/WRITE masks say which
+// slots are loaded and stored. Pairs of doubles move as one 16-byte access.
+// ---------------------------------------------------------------------------
+template <int OP>
+struct EwTraits;
+template <>
+struct EwTraits<EW_DOT> {
+  static constexpr int NP = 1, R = 0b000011, W = 0;
+};
+template <>
+struct EwTraits<EW_MRR_FIRST> {  // p: y ar1 z r xs xd
+  static constexpr int NP = 0, R = 0b011010, W = 0b101101;
+};
+template <>
+struct EwTraits<EW_MRR> {
+  static constexpr int NP = 0, R = 0b011111, W = 0b101101;
+};
+template <>
+struct EwTraits<EW_CG> {  // p: x p r v
+  static constexpr int NP = 1, R = 0b001111, W = 0b000101;
+};
+template <>
+struct EwTraits<EW_CG_P> {  // p: p r
+  static constexpr int NP = 0, R = 0b000011, W = 0b000001;
+};
+template <>
+struct EwTraits<EW_KCG> {  // p: x ap0 r ap1
+  static constexpr int NP = 0, R = 0b001111, W = 0b000111;
+};
+template <>
+struct EwTraits<EW_MRR_S> {  // p: ar y r
+  static constexpr int NP = 2, R = 0b000111, W = 0;
+};
+template <>
+struct EwTraits<EW_COPY> {  // p: dst src
+  static constexpr int NP = 0, R = 0b000010, W = 0b000001;
+};
+
+template <int OP>
+__device__ __forceinline__ void ew_elem(double c0, double c1, double (&v)[6],
+                                        double (&acc)[EwTraits<OP>::NP > 0
+                                                          ? EwTraits<OP>::NP
+                                                          : 1]) {
+  if constexpr (OP == EW_DOT) {
+    acc[0] += v[0] * v[1];
+  } else if constexpr (OP == EW_MRR_FIRST) {  // c1 = zeta
+    const double y = c1 * v[1];
+    const double z = (-c1) * v[3];
+    v[0] = y;
+    v[2] = z;
+    v[3] = v[3] - y;
+    v[5] = v[4] - z;
+  } else if constexpr (OP == EW_MRR) {  // c0 = eta, c1 = zeta
+    const double t1 = c0 * v[0];
+    const double t2 = c1 * v[1];
+    const double y = t1 + t2;
+    const double t3 = c0 * v[2];
+    const double t4 = c1 * v[3];
+    const double z = t3 - t4;
+    v[0] = y;
+    v[2] = z;
+    v[3] = v[3] - y;
+    v[5] = v[4] - z;
+  } else if constexpr (OP == EW_CG) {  // c0 = alpha
+    const double ap = c0 * v[1];
+    const double av = c0 * v[3];
+    v[0] = v[0] + ap;
+    v[2] = v[2] - av;
+    acc[0] += v[2] * v[2];
+  } else if constexpr (OP == EW_CG_P) {  // c0 = beta
+    const double bp = c0 * v[0];
+    v[0] = v[1] + bp;
+  } else if constexpr (OP == EW_KCG) {  // c0 = alpha, c1 = beta
+    const double a0 = c0 * v[1];
+    const double a1 = c0 * v[3];
+    v[0] = v[0] + a0;
+    v[2] = v[2] - a1;
+    const double bp = c1 * v[1];
+    v[1] = v[2] + bp;
+  } else if constexpr (OP == EW_MRR_S) {  // c0 = gamma
+    const double gy = c0 * v[1];
+    const double s = v[0] - gy;
+    acc[0] += v[2] * s;
+    acc[1] += s * s;
+  } else if constexpr (OP == EW_COPY) {
+    v[0] = v[1];
+  }
+}
+
+template <int OP, bool VEC>
+__global__ __launch_bounds__(kBlock) void ew_kernel(EwArgs a) {
+  using T = EwTraits<OP>;
+  constexpr int NP = T::NP;
+  __shared__ double s_red[(NP > 0 ? NP : 1) * 4];
+  double acc[NP > 0 ? NP : 1];
+#pragma unroll
+  for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  const int64_t t0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if constexpr (VEC) {
+    const int64_t npairs = a.n >> 1;
+    for (int64_t q = t0; q < npairs; q += stride) {
+      double va[6], vb[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        if (T::R & (1 << k)) {
+          const double2 d = reinterpret_cast<const double2*>(a.p[k])[q];
+          va[k] = d.x;
+          vb[k] = d.y;
+        } else {
+          va[k] = vb[k] = 0.0;
+        }
+      }
+      ew_elem<OP>(a.c0, a.c1, va, acc);
+      ew_elem<OP>(a.c0, a.c1, vb, acc);
+#pragma unroll
+      for (int k = 0; k < 6; ++k)
+        if (T::W & (1 << k)) reinterpret_cast<double2*>(a.p[k])[q] = make_double2(va[k], vb[k]);
+    }
+    if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+      const int64_t i = a.n - 1;
+      double v[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) v[k] = (T::R & (1 << k)) ? a.p[k][i] : 0.0;
+      ew_elem<OP>(a.c0, a.c1, v, acc);
+#pragma unroll
+      for (int k = 0; k < 6; ++k)
+        if (T::W & (1 << k)) a.p[k][i] = v[k];
+    }
+  } else {
+    for (int64_t i = t0; i < a.n; i += stride) {
+      double v[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) v[k] = (T::R & (1 << k)) ? a.p[k][i] : 0.0;
+      ew_elem<OP>(a.c0, a.c1, v, acc);
+#pragma unroll
+      for (int k = 0; k < 6; ++k)
+        if (T::W & (1 << k)) a.p[k][i] = v[k];
+    }
+  }
+  block_reduce_store<NP>(acc, a.partials, a.grid, s_red);
+}
+
+template <int OP>
+void ew_dispatch_op(const EwArgs& a, hipStream_t s) {
+  bool aligned = true;
+  for (int k = 0; k < 6; ++k)
+    if (((EwTraits<OP>::R | EwTraits<OP>::W) & (1 << k)) &&
+        (reinterpret_cast<uintptr_t>(a.p[k]) & 15))
+      aligned = false;
+  if (aligned)
+    ew_kernel<OP, true><<<a.grid, kBlock, 0, s>>>(a);
+  else
+    ew_kernel<OP, false><<<a.grid, kBlock, 0, s>>>(a);
+}
+
+// ---------------------------------------------------------------------------
+// Fixed-order final reduction: one workgroup per slot.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void finalize_kernel(const double* __restrict__ part,
+                                                          int grid, double* __restrict__ out) {
+  __shared__ double s_red[4];
+  const int slot = blockIdx.x;
+  double t = 0.0;
+  for (int i = threadIdx.x; i < grid; i += kBlock) t += part[(int64_t)slot * grid + i];
+  for (int off = 32; off > 0; off >>= 1) t += __shfl_down(t, off, 64);
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double r = s_red[0];
+    r = r + s_red[1];
+    r = r + s_red[2];
+    r = r + s_red[3];
+    out[slot] = r;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Multi-dot (test/composition primitive), up to 16 products per launch.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void multidot_kernel(MultiDotArgs a, int base) {
+  constexpr int NP = 16;
+  __shared__ double s_red[NP * 4];
+  double acc[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) acc[p] = 0.0;
+  const int cnt = min(NP, a.count - base);
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < a.n; i += stride) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+      if (p < cnt) acc[p] += a.u[base + p][i] * a.v[base + p][i];
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    double v = acc[p];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    if (lane == 0) s_red[p * 4 + wave] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < cnt) {
+    const double* r = s_red + threadIdx.x * 4;
+    double t = r[0];
+    t = t + r[1];
+    t = t + r[2];
+    t = t + r[3];
+    a.partials[(int64_t)(base + threadIdx.x) * a.grid + blockIdx.x] = t;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Generators.
+// ---------------------------------------------------------------------------
+template <typename RP>
+__global__ void poisson_count_kernel(int dim, int64_t side, int64_t row0, int64_t n,
+                                     RP* rowptr) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int64_t g = row0 + i;
+  int cnt = 1;
+  for (int d = 0; d < dim; ++d) {
+    const int64_t c = g % side;
+    g /= side;
+    cnt += (c > 0) + (c < side - 1);
+  }
+  rowptr[i + 1] = (RP)cnt;
+}
+
+template <typename RP>
+__global__ void poisson_fill_kernel(int dim, int64_t side, int64_t row0, int64_t n,
+                                    const RP* rowptr, int32_t* col, double* val) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t g = row0 + i;
+  int64_t coord[3] = {0, 0, 0};
+  int64_t stride[3] = {1, side, side * side};
+  int64_t t = g;
+  for (int d = 0; d < dim; ++d) {
+    coord[d] = t % side;
+    t /= side;
+  }
+  int64_t j = (int64_t)rowptr[i];
+  // Sorted column order: outermost lower neighbours first.
+  for (int d = dim - 1; d >= 0; --d)
+    if (coord[d] > 0) {
+      col[j] = (int32_t)(g - stride[d]);
+      val[j] = -1.0;
+      ++j;
+    }
+  col[j] = (int32_t)g;
+  val[j] = 2.0 * dim;
+  ++j;
+  for (int d = 0; d < dim; ++d)
+    if (coord[d] < side - 1) {
+      col[j] = (int32_t)(g + stride[d]);
+      val[j] = -1.0;
+      ++j;
+    }
+}
+
+template <typename RP>
+__global__ void banded_count_kernel(BandSpec b, int64_t row0, int64_t n, RP* rowptr) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t g = row0 + i;
+  int cnt = 1;
+  for (int t = 0; t < b.h; ++t) cnt += (g - b.off[t] >= 0) + (g + b.off[t] < b.n_global);
+  rowptr[i + 1] = (RP)cnt;
+}
+
+template <typename RP>
+__global__ void banded_fill_kernel(BandSpec b, int64_t row0, int64_t n, const RP* rowptr,
+                                   int32_t* col, double* val) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t g = row0 + i;
+  // Diagonal = (sum of |off| in column order) + 1.
+  double s = 0.0;
+  for (int t = b.h - 1; t >= 0; --t)
+    if (g - b.off[t] >= 0) s = s + fabs(band_value(b.seed, g - b.off[t], b.off[t]));
+  for (int t = 0; t < b.h; ++t)
+    if (g + b.off[t] < b.n_global) s = s + fabs(band_value(b.seed, g, b.off[t]));
+  int64_t j = (int64_t)rowptr[i];
+  for (int t = b.h - 1; t >= 0; --t)
+    if (g - b.off[t] >= 0) {
+      col[j] = (int32_t)(g - b.off[t]);
+      val[j] = band_value(b.seed, g - b.off[t], b.off[t]);
+      ++j;
+    }
+  col[j] = (int32_t)g;
+  val[j] = s + 1.0;
+  ++j;
+  for (int t = 0; t < b.h; ++t)
+    if (g + b.off[t] < b.n_global) {
+      col[j] = (int32_t)(g + b.off[t]);
+      val[j] = band_value(b.seed, g, b.off[t]);
+      ++j;
+    }
+}
+
+__global__ void fill_rhs_kernel(uint64_t seed, int64_t row0, int64_t n, double* b) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) b[i] = rhs_value(seed, (uint64_t)(row0 + i));
+}
+
+template <typename RP>
+__global__ void col_minmax_kernel(const RP* rowptr, int64_t n, const int32_t* col,
+                                  unsigned long long* out) {
+  __shared__ int64_t s_min[kBlock], s_max[kBlock];
+  const int64_t base = (int64_t)rowptr[0];
+  const int64_t nnz = (int64_t)rowptr[n] - base;
+  int64_t mn = INT64_MAX, mx = -1;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nnz;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = col[base + j];
+    mn = c < mn ? c : mn;
+    mx = c > mx ? c : mx;
+  }
+  s_min[threadIdx.x] = mn;
+  s_max[threadIdx.x] = mx;
+  __syncthreads();
+  for (int off = kBlock / 2; off > 0; off >>= 1) {
+    if (threadIdx.x < off) {
+      s_min[threadIdx.x] = min(s_min[threadIdx.x], s_min[threadIdx.x + off]);
+      s_max[threadIdx.x] = max(s_max[threadIdx.x], s_max[threadIdx.x + off]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    atomicMin(&out[0], (unsigned long long)s_min[0]);
+    if (s_max[0] >= 0) atomicMax(&out[1], (unsigned long long)s_max[0]);
+  }
+}
+
+template <typename RP>
+__global__ void col_shift_kernel(const RP* rowptr, int64_t n, int32_t* col, int64_t delta) {
+  const int64_t base = (int64_t)rowptr[0];
+  const int64_t nnz = (int64_t)rowptr[n] - base;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nnz;
+       j += (int64_t)gridDim.x * blockDim.x)
+    col[base + j] = (int32_t)((int64_t)col[base + j] + delta);
+}
+
+inline unsigned blocks_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Launchers
+// ---------------------------------------------------------------------------
+int spmv_products(SpmvEpi epi) {
+  switch (epi) {
+    case EPI_NONE: return EpiTraits<EPI_NONE>::NP;
+    case EPI_BMINUS: return EpiTraits<EPI_BMINUS>::NP;
+    case EPI_XY: return EpiTraits<EPI_XY>::NP;
+    case EPI_HEAD_MRR: return EpiTraits<EPI_HEAD_MRR>::NP;
+    case EPI_HEAD_KCG: return EpiTraits<EPI_HEAD_KCG>::NP;
+    case EPI_MRR_LOOP: return EpiTraits<EPI_MRR_LOOP>::NP;
+    case EPI_DUAL_NONE: return EpiTraits<EPI_DUAL_NONE>::NP;
+    case EPI_DUAL_MRR: return EpiTraits<EPI_DUAL_MRR>::NP;
+    case EPI_DUAL_KCG: return EpiTraits<EPI_DUAL_KCG>::NP;
+  }
+  return 0;
+}
+
+void launch_spmv(SpmvEpi epi, const SpmvArgs& a, hipStream_t s) {
+  KR_REQUIRE(a.grid > 0, "spmv: grid must be positive");
+  if (a.rowptr64)
+    spmv_dispatch<int64_t>(epi, a, s);
+  else
+    spmv_dispatch<int32_t>(epi, a, s);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
+int ew_products(EwOp op) {
+  switch (op) {
+    case EW_DOT: return EwTraits<EW_DOT>::NP;
+    case EW_MRR_FIRST: return EwTraits<EW_MRR_FIRST>::NP;
+    case EW_MRR: return EwTraits<EW_MRR>::NP;
+    case EW_CG: return EwTraits<EW_CG>::NP;
+    case EW_CG_P: return EwTraits<EW_CG_P>::NP;
+    case EW_KCG: return EwTraits<EW_KCG>::NP;
+    case EW_MRR_S: return EwTraits<EW_MRR_S>::NP;
+    case EW_COPY: return EwTraits<EW_COPY>::NP;
+  }
+  return 0;
+}
+
+void launch_ew(EwOp op, const EwArgs& a, hipStream_t s) {
+  KR_REQUIRE(a.grid > 0, "elementwise: grid must be positive");
+  switch (op) {
+    case EW_DOT: ew_dispatch_op<EW_DOT>(a, s); break;
+    case EW_MRR_FIRST: ew_dispatch_op<EW_MRR_FIRST>(a, s); break;
+    case EW_MRR: ew_dispatch_op<EW_MRR>(a, s); break;
+    case EW_CG: ew_dispatch_op<EW_CG>(a, s); break;
+    case EW_CG_P: ew_dispatch_op<EW_CG_P>(a, s); break;
+    case EW_KCG: ew_dispatch_op<EW_KCG>(a, s); break;
+    case EW_MRR_S: ew_dispatch_op<EW_MRR_S>(a, s); break;
+    case EW_COPY: ew_dispatch_op<EW_COPY>(a, s); break;
+    default: throw Failure(KR_ERR_INVALID, "unknown elementwise op");
+  }
+  KR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_finalize(const double* partials, int grid, int nslots, double* out,
+                     hipStream_t s) {
+  if (nslots <= 0) return;
+  finalize_kernel<<<nslots, kBlock, 0, s>>>(partials, grid, out);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_multidot(const MultiDotArgs& a, hipStream_t s) {
+  KR_REQUIRE(a.count >= 0 && a.count <= 64, "multidot: count must be in [0, 64]");
+  for (int base = 0; base < a.count; base += 16) {
+    multidot_kernel<<<a.grid, kBlock, 0, s>>>(a, base);
+    KR_HIP_CHECK(hipGetLastError());
+  }
+}
+
+void launch_poisson_count(int dim, int64_t side, int64_t row0, int64_t n, void* rowptr,
+                          int rowptr64, hipStream_t s) {
+  if (n <= 0) return;
+  if (rowptr64)
+    poisson_count_kernel<int64_t><<<blocks_for(n, 256), 256, 0, s>>>(
+        dim, side, row0, n, static_cast<int64_t*>(rowptr));
+  else
+    poisson_count_kernel<int32_t><<<blocks_for(n, 256), 256, 0, s>>>(
+        dim, side, row0, n, static_cast<int32_t*>(rowptr));
+  KR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_poisson_fill(int dim, int64_t side, int64_t row0, int64_t n,
+                         const void* rowptr, int rowptr64, int32_t* col, double* val,
+                         hipStream_t s) {
+  if (n <= 0) return;
+  if (rowptr64)
+    poisson_fill_kernel<int64_t><<<blocks_for(n, 256), 256, 0, s>>>(
+        dim, side, row0, n, static_cast<const int64_t*>(rowptr), col, val);
+  else
+    poisson_fill_kernel<int32_t><<<blocks_for(n, 256), 256, 0, s>>>(
+        dim, side, row0, n, static_cast<const int32_t*>(rowptr), col, val);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_banded_count(const BandSpec& b, int64_t row0, int64_t n, void* rowptr,
+                         int rowptr64, hipStream_t s) {
+  if (n <= 0) return;
+  if (rowptr64)
+    banded_count_kernel<int64_t><<<blocks_for(n, 256), 256, 0, s>>>(
+        b, row0, n, static_cast<int64_t*>(rowptr));
+  else
+    banded_count_kernel<int32_t><<<blocks_for(n, 256), 256, 0, s>>>(
+        b, row0, n, static_cast<int32_t*>(rowptr));
+  KR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_banded_fill(const BandSpec& b, int64_t row0, int64_t n, const void* rowptr,
+                        int rowptr64, int32_t* col, double* val, hipStream_t s) {
+  if (n <= 0) return;
+  if (rowptr64)
+    banded_fill_kernel<int64_t><<<blocks_for(n, 256), 256, 0, s>>>(
+        b, row0, n, static_cast<const int64_t*>(rowptr), col, val);
+  else
+    banded_fill_kernel<int32_t><<<blocks_for(n, 256), 256, 0, s>>>(
+        b, row0, n, static_cast<const int32_t*>(rowptr), col, val);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
+void rowptr_scan(void* rowptr, int rowptr64, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  size_t tmp_bytes = 0;
+  if (rowptr64) {
+    int64_t* p = static_cast<int64_t*>(rowptr) + 1;
+    KR_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, tmp_bytes, p, p, n, s));
+    void* tmp = nullptr;
+    KR_HIP_CHECK(hipMalloc(&tmp, tmp_bytes));
+    KR_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(tmp, tmp_bytes, p, p, n, s));
+    KR_HIP_CHECK(hipStreamSynchronize(s));
+    KR_HIP_CHECK(hipFree(tmp));
+  } else {
+    int32_t* p = static_cast<int32_t*>(rowptr) + 1;
+    KR_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, tmp_bytes, p, p, (int)n, s));
+    void* tmp = nullptr;
+    KR_HIP_CHECK(hipMalloc(&tmp, tmp_bytes));
+    KR_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(tmp, tmp_bytes, p, p, (int)n, s));
+    KR_HIP_CHECK(hipStreamSynchronize(s));
+    KR_HIP_CHECK(hipFree(tmp));
+  }
+}
+
+void launch_fill_rhs(uint64_t seed, int64_t row0, int64_t n, double* b, hipStream_t s) {
+  if (n <= 0) return;
+  fill_rhs_kernel<<<blocks_for(n, 256), 256, 0, s>>>(seed, row0, n, b);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_col_minmax(const void* rowptr, int rowptr64, int64_t n, const int32_t* col,
+                       int64_t* out2, hipStream_t s) {
+  const unsigned long long init[2] = {(unsigned long long)INT64_MAX, 0ull};
+  KR_HIP_CHECK(hipMemcpyAsync(out2, init, sizeof(init), hipMemcpyHostToDevice, s));
+  if (n <= 0) return;
+  auto* o = reinterpret_cast<unsigned long long*>(out2);
+  if (rowptr64)
+    col_minmax_kernel<int64_t><<<1024, kBlock, 0, s>>>(static_cast<const int64_t*>(rowptr),
+                                                        n, col, o);
+  else
+    col_minmax_kernel<int32_t><<<1024, kBlock, 0, s>>>(static_cast<const int32_t*>(rowptr),
+                                                        n, col, o);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_col_shift(const void* rowptr, int rowptr64, int64_t n, int32_t* col,
+                      int64_t delta, hipStream_t s) {
+  if (n <= 0 || delta == 0) return;
+  if (rowptr64)
+    col_shift_kernel<int64_t><<<2048, kBlock, 0, s>>>(static_cast<const int64_t*>(rowptr),
+                                                       n, col, delta);
+  else
+    col_shift_kernel<int32_t><<<2048, kBlock, 0, s>>>(static_cast<const int32_t*>(rowptr),
+                                                       n, col, delta);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace kr

@@ -1,0 +1,360 @@
+"""Host-side mirror of the reference's multi-GPU runtime (``MultiGpu``).
+
+``KrylovSystem`` owns a row-partitioned SPD system on one or more devices and
+runs the solver loops natively (``kr_solve_*`` in libkrylov_amd.so). It is the
+MI355X replacement for ``MultiGpu.init/alloc/dot`` of the reference
+(v3/gpu/common.py:43-126, v3/gpu/mpi/common.py:46-171):
+
+* the reference splits A by rows but REPLICATES every vector and moves full
+  vectors per SpMV (peer broadcast + gather, then ``comm.Allgather``);
+* here A and every vector stay row-partitioned; a SpMV moves only the halo
+  rows its columns reach, and the dot products are reduced once per sync.
+
+Two ways to hold shards, matching the two reference families:
+* single process, ``devices`` = list of HIP devices (v3/gpu: all visible GPUs);
+  several shards may share one device (used by the tests);
+* one process per GPU with a ``Communicator`` (v3/gpu/mpi), RCCL over xGMI.
+
+Device memory is held in torch tensors (PyTorch-ROCm is the allocator and the
+bootstrap; no torch op runs on the solver path).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from ._lib import call, library, ptr_array
+
+METHODS = tuple(_lib.KR_METHOD)
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def balanced_partition(n: int, parts: int) -> list:
+    """Contiguous row blocks whose sizes differ by at most one row.
+
+    (The reference uses ``N // G`` rows per GPU and silently drops the
+    remainder, v3/gpu/common.py:86; here every row is owned.)"""
+    q, r = divmod(n, parts)
+    out = [0]
+    for p in range(parts):
+        out.append(out[-1] + q + (1 if p < r else 0))
+    return out
+
+
+def visible_devices() -> list:
+    """Shard -> device map for the single-process family.
+
+    ``KRYLOV_AMD_SHARDS="0,0,1"`` overrides (several shards may share a
+    device); otherwise one shard per visible device, like MultiGpu.init
+    (v3/gpu/common.py:62-66)."""
+    env = os.environ.get("KRYLOV_AMD_SHARDS")
+    if env:
+        return [int(t) for t in env.split(",") if t.strip() != ""]
+    n = _lib.device_count()
+    if n <= 0:
+        raise RuntimeError("no HIP device visible: the parallel_krylov_amd solvers need an "
+                           "MI355X (gfx950) GPU; there is no CPU fallback")
+    return list(range(n))
+
+
+class Communicator:
+    """RCCL communicator, one rank per GPU (replaces mpi4py on the hot path).
+
+    Bootstrapped by broadcasting the RCCL unique id over ``bcast`` (a
+    torch.distributed group or an mpi4py-like ``comm.bcast``)."""
+
+    def __init__(self, rank: int, size: int, device: int, bcast):
+        self.rank, self.size, self.device = rank, size, device
+        uid = (ctypes.c_uint8 * 128)()
+        if rank == 0:
+            call("kr_comm_unique_id", uid)
+        payload = bcast(bytes(uid))
+        uid = (ctypes.c_uint8 * 128).from_buffer_copy(payload)
+        self.handle = ctypes.c_void_p()
+        call("kr_comm_init", ctypes.byref(self.handle), uid, size, rank, device)
+
+    @classmethod
+    def from_torch(cls, group=None, device=None):
+        import torch.distributed as dist
+        rank, size = dist.get_rank(group), dist.get_world_size(group)
+        if device is None:
+            device = local_device(rank)
+
+        def bcast(data):
+            obj = [data]
+            dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0)
+                                       if group is not None else 0, group=group)
+            return obj[0]
+        return cls(rank, size, device, bcast)
+
+    @classmethod
+    def from_mpi(cls, comm, device=None):
+        rank, size = comm.Get_rank(), comm.Get_size()
+        if device is None:
+            device = local_device(rank)
+        return cls(rank, size, device, lambda data: comm.bcast(data, root=0))
+
+    def close(self):
+        if getattr(self, "handle", None):
+            library().kr_comm_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def local_device(rank: int) -> int:
+    """Device of this rank: LOCAL_RANK, else the first of GPU_IDS
+    (v3/gpu/mpi/common.py:77-83), else rank modulo the device count."""
+    if "LOCAL_RANK" in os.environ:
+        return int(os.environ["LOCAL_RANK"])
+    if os.environ.get("GPU_IDS"):
+        return int(os.environ["GPU_IDS"].split(",")[0])
+    n = _lib.device_count()
+    return rank % max(n, 1)
+
+
+@dataclass
+class SolveOutput:
+    x: list                      # per local shard: torch float64 tensor of own rows
+    info: dict                   # reference info dict (time, nosl, residual[, khistory])
+    converged: bool
+    iterations: int
+    final_k: int
+    final_residual: float
+    kernel_stats: list = field(default_factory=list)
+
+
+class KrylovSystem:
+    """A row-partitioned SPD system resident on HIP devices."""
+
+    def __init__(self, n_global: int, row_begin, devices, comm: Communicator | None = None):
+        torch = _torch()
+        self.n_global = int(n_global)
+        self.row_begin = [int(r) for r in row_begin]
+        self.devices = [int(d) for d in devices]
+        self.comm = comm
+        if len(self.row_begin) != len(self.devices) + 1:
+            raise ValueError("row_begin needs one more entry than devices")
+        self._keep = []
+        self._finalized = False
+        self.handle = ctypes.c_void_p()
+        for d in set(self.devices):
+            torch.cuda.set_device(d)  # initialise the context before the library uses it
+        devs = (ctypes.c_int * len(self.devices))(*self.devices)
+        rb = (ctypes.c_int64 * len(self.row_begin))(*self.row_begin)
+        call("kr_system_create", ctypes.byref(self.handle), self.n_global, len(self.devices),
+             devs, rb, comm.handle if comm is not None else None)
+
+    # ------------------------------------------------------------- building
+    @property
+    def nshards(self) -> int:
+        return len(self.devices)
+
+    def shard_rows(self, s: int):
+        return self.row_begin[s], self.row_begin[s + 1]
+
+    def device(self, s: int):
+        return _torch().device("cuda", self.devices[s])
+
+    def adopt_csr(self, s: int, block) -> None:
+        """Upload the CSR block of shard s (its rows, GLOBAL column indices).
+
+        ``block`` is a scipy sparse matrix/array (any format) or a
+        (indptr, indices, data) triple. Column indices are uploaded as int32
+        and rewritten on the device to the shard's halo-local numbering."""
+        torch = _torch()
+        if isinstance(block, tuple):
+            indptr, indices, data = block
+        else:
+            import scipy.sparse as sp
+            csr = sp.csr_matrix(block) if not sp.isspmatrix_csr(block) else block
+            indptr, indices, data = csr.indptr, csr.indices, csr.data
+        indptr = np.asarray(indptr)
+        nnz = int(indptr[-1] - indptr[0])
+        rp64 = nnz >= 2 ** 31 - 1 or indptr.dtype == np.int64 and int(indptr[-1]) >= 2 ** 31 - 1
+        dev = self.device(s)
+        t_rp = torch.from_numpy(np.ascontiguousarray(indptr, dtype=np.int64 if rp64 else np.int32)).to(dev)
+        t_col = torch.from_numpy(np.ascontiguousarray(indices, dtype=np.int32)).to(dev)
+        t_val = torch.from_numpy(np.ascontiguousarray(data, dtype=np.float64)).to(dev)
+        torch.cuda.synchronize(dev)
+        self._keep += [t_rp, t_col, t_val]
+        call("kr_system_adopt_csr", self.handle, s, t_rp.data_ptr(), int(rp64),
+             t_col.data_ptr(), t_val.data_ptr())
+
+    def set_matrix(self, A) -> None:
+        """Distribute a whole matrix (scipy sparse or dense ndarray) over the
+        local shards (in-process family)."""
+        import scipy.sparse as sp
+        A = sp.csr_matrix(A) if not sp.isspmatrix_csr(A) else A
+        for s in range(self.nshards):
+            r0, r1 = self.shard_rows(s)
+            self.adopt_csr(s, A[r0:r1])
+
+    def gen_poisson(self, n_side: int, dim: int) -> None:
+        call("kr_system_gen_poisson", self.handle, dim, n_side)
+
+    def gen_banded(self, h: int, width: int, seed: int, rowptr64: bool = False) -> None:
+        call("kr_system_gen_banded", self.handle, h, width, seed, int(rowptr64))
+
+    def finalize(self) -> None:
+        call("kr_system_finalize", self.handle)
+        self._finalized = True
+
+    def shard_info(self, s: int) -> dict:
+        v = [ctypes.c_int64() for _ in range(4)]
+        call("kr_system_shard_info", self.handle, s, *[ctypes.byref(t) for t in v])
+        return dict(zip(("n_local", "halo_lo", "halo_hi", "nnz"), [t.value for t in v]))
+
+    # ------------------------------------------------------------- vectors
+    def split(self, v) -> list:
+        """Own-row device tensors of a full-length host/device vector."""
+        torch = _torch()
+        out = []
+        for s in range(self.nshards):
+            r0, r1 = self.shard_rows(s)
+            seg = v[r0:r1]
+            if isinstance(seg, np.ndarray):
+                seg = torch.from_numpy(np.ascontiguousarray(seg, dtype=np.float64))
+            out.append(seg.to(device=self.device(s), dtype=torch.float64).contiguous())
+        return out
+
+    def rhs(self, seed: int) -> list:
+        """Synthetic b (2u-1, counter hash) generated on the device per shard."""
+        torch = _torch()
+        out = []
+        for s in range(self.nshards):
+            r0, r1 = self.shard_rows(s)
+            t = torch.empty(r1 - r0, dtype=torch.float64, device=self.device(s))
+            call("kr_fill_rhs", self.handle, s, seed, t.data_ptr())
+            out.append(t)
+        return out
+
+    def gather(self, parts) -> "object":
+        torch = _torch()
+        if len(parts) == 1:
+            return parts[0]
+        d0 = self.device(0)
+        return torch.cat([p.to(d0) for p in parts])
+
+    # ------------------------------------------------------------- compute
+    def spmv(self, x_parts) -> list:
+        """Distributed y = A x through the halo exchange (own rows in/out)."""
+        torch = _torch()
+        ys = [torch.empty_like(x) for x in x_parts]
+        for s in range(self.nshards):
+            torch.cuda.synchronize(self.device(s))
+        call("kr_system_spmv", self.handle, ptr_array([x.data_ptr() for x in x_parts]),
+             ptr_array([y.data_ptr() for y in ys]))
+        return ys
+
+    def solve(self, method: str, b_parts, x0_parts=None, tol=1e-5, maxiter=None, k=0,
+              profile=False, max_outer=None) -> SolveOutput:
+        """Run one solver to completion (or for ``max_outer`` outer steps)."""
+        torch = _torch()
+        if not self._finalized:
+            self.finalize()
+        if method not in _lib.KR_METHOD:
+            raise ValueError(f"unknown method {method!r}")
+        prm = _lib.SolveParams(method=_lib.KR_METHOD[method], k=int(k or 0), tol=float(tol),
+                               maxiter=-1 if maxiter is None else int(maxiter),
+                               profile=1 if profile else 0)
+        for s in range(self.nshards):
+            torch.cuda.synchronize(self.device(s))
+        b_arr = ptr_array([t.data_ptr() for t in b_parts])
+        x0_arr = ptr_array([t.data_ptr() for t in x0_parts]) if x0_parts is not None else None
+        call("kr_solve_begin", self.handle, ctypes.byref(prm), b_arr, x0_arr)
+        done = ctypes.c_int(0)
+        call("kr_solve_step", self.handle, (1 << 62) if max_outer is None else int(max_outer),
+             ctypes.byref(done))
+        return self.finish(method)
+
+    def begin(self, method, b_parts, x0_parts=None, tol=1e-5, maxiter=None, k=0,
+              profile=False) -> None:
+        torch = _torch()
+        if not self._finalized:
+            self.finalize()
+        prm = _lib.SolveParams(method=_lib.KR_METHOD[method], k=int(k or 0), tol=float(tol),
+                               maxiter=-1 if maxiter is None else int(maxiter),
+                               profile=1 if profile else 0)
+        for s in range(self.nshards):
+            torch.cuda.synchronize(self.device(s))
+        b_arr = ptr_array([t.data_ptr() for t in b_parts])
+        x0_arr = ptr_array([t.data_ptr() for t in x0_parts]) if x0_parts is not None else None
+        call("kr_solve_begin", self.handle, ctypes.byref(prm), b_arr, x0_arr)
+
+    def step(self, n_outer: int) -> bool:
+        done = ctypes.c_int(0)
+        call("kr_solve_step", self.handle, int(n_outer), ctypes.byref(done))
+        return bool(done.value)
+
+    def finish(self, method: str) -> SolveOutput:
+        torch = _torch()
+        xs = [torch.empty(self.row_begin[s + 1] - self.row_begin[s], dtype=torch.float64,
+                          device=self.device(s)) for s in range(self.nshards)]
+        res = _lib.SolveResult()
+        call("kr_solve_end", self.handle, ptr_array([x.data_ptr() for x in xs]),
+             ctypes.byref(res))
+        n = int(res.entries)
+        residual = np.zeros(n, np.float64)
+        nosl = np.zeros(n, np.int64)
+        khist = np.zeros(n, np.int64)
+        call("kr_solve_history", self.handle,
+             residual.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+             nosl.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+             khist.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), n)
+        info = {"time": float(res.time_s), "nosl": nosl, "residual": residual}
+        if method == "adaptivekskipmrr":
+            info["khistory"] = khist
+        return SolveOutput(x=xs, info=info, converged=bool(res.converged),
+                           iterations=int(res.iterations), final_k=int(res.final_k),
+                           final_residual=float(res.final_residual),
+                           kernel_stats=self.kernel_stats())
+
+    def reset_kernel_stats(self) -> None:
+        call("kr_solve_kernel_stats_reset", self.handle)
+
+    def kernel_stats(self) -> list:
+        cap = 64
+        arr = (_lib.KernelStat * cap)()
+        cnt = ctypes.c_int(0)
+        call("kr_solve_kernel_stats", self.handle, arr, cap, ctypes.byref(cnt))
+        return [dict(name=arr[i].name.decode(), launches=int(arr[i].launches),
+                     total_ms=float(arr[i].total_ms),
+                     bytes_per_launch=float(arr[i].bytes_per_launch))
+                for i in range(min(cnt.value, cap))]
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            library().kr_system_destroy(self.handle)
+            self.handle = None
+            self._keep = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def system_from_matrix(A, devices=None) -> KrylovSystem:
+    """Single-process system over ``devices`` (default: all visible GPUs)."""
+    import scipy.sparse as sp
+    devices = visible_devices() if devices is None else list(devices)
+    A = sp.csr_matrix(A) if not sp.isspmatrix_csr(A) else A
+    n = A.shape[0]
+    sysm = KrylovSystem(n, balanced_partition(n, len(devices)), devices)
+    sysm.set_matrix(A)
+    sysm.finalize()
+    return sysm

@@ -1,0 +1,11 @@
+"""MrR, one rank per GPU (drop-in for reference v3/gpu/mpi/mrr.py:10).
+
+Each rank holds its row block; halos move by RCCL send/recv and the partial
+dot products by one RCCL all-gather per sync point (see common.py).
+"""
+from .common import run
+
+
+def mrr(comm, local_A, b, x=None, tol=1e-05, maxiter=None, M=None, callback=None, atol=None,
+        exit_nonroot=False) -> tuple:
+    return run("mrr", "MrR + GPU + MPI", comm, local_A, b, x, tol, maxiter, None, exit_nonroot)

@@ -1,0 +1,223 @@
+"""HIP kernels through the C ABI vs the oracle (MI355X only).
+
+Bitwise where the arithmetic is fixed-order: SpMV rows (scipy csr_matvec
+order), the fused vector updates (numpy statement rounding) and the synthetic
+generators. Dot products are deterministic but use a tree order, so they are
+compared with a rounding bound instead.
+"""
+import ctypes
+import math
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from conftest import golden_matrix
+from oracle import matrices
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return torch.device("cuda", 0)
+
+
+def _lib():
+    import parallel_krylov_amd._lib as L
+    return L.library()
+
+
+def _t(a, dev, dtype=None):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a if dtype is None else a.astype(dtype))).to(dev)
+
+
+def _sync():
+    import torch
+    torch.cuda.synchronize()
+
+
+def _irregular(n, seed):
+    """Random sparse matrix with empty rows, a very long row and ragged rows."""
+    rng = np.random.default_rng(seed)
+    rows, cols = [], []
+    for i in range(n):
+        if i % 97 == 5:
+            continue  # empty row
+        cnt = 6000 if i == n // 2 else int(rng.integers(1, 40))
+        c = np.unique(rng.integers(0, n, size=cnt))
+        rows.append(np.full(c.size, i))
+        cols.append(c)
+    r = np.concatenate(rows)
+    c = np.concatenate(cols)
+    v = rng.standard_normal(r.size)
+    A = sp.csr_matrix((v, (r, c)), shape=(n, n))
+    A.sort_indices()
+    return A
+
+
+MATRICES = {
+    "poisson2d_33": lambda: golden_matrix(["poisson", 33, 2]),
+    "poisson3d_17": lambda: golden_matrix(["poisson", 17, 3]),
+    "banded_3001": lambda: golden_matrix(["banded", 3001, 13, 64, 0]),
+    "banded63_2000": lambda: golden_matrix(["banded", 2000, 31, 256, 0]),
+    "irregular_5000": lambda: _irregular(5000, 1),
+    "single_row": lambda: sp.csr_matrix(np.array([[4.0]])),
+}
+
+
+@pytest.mark.parametrize("name", list(MATRICES))
+@pytest.mark.parametrize("rp64", [0, 1])
+def test_spmv_bitwise_vs_scipy(torch_dev, name, rp64):
+    A = MATRICES[name]()
+    n = A.shape[0]
+    rng = np.random.default_rng(7)
+    x = rng.standard_normal(n)
+    x2 = rng.standard_normal(n)
+    rp = _t(A.indptr, torch_dev, np.int64 if rp64 else np.int32)
+    col = _t(A.indices, torch_dev, np.int32)
+    val = _t(A.data, torch_dev, np.float64)
+    xt, x2t = _t(x, torch_dev), _t(x2, torch_dev)
+    import torch
+    y = torch.full((n,), np.nan, dtype=torch.float64, device=torch_dev)
+    y2 = torch.full((n,), np.nan, dtype=torch.float64, device=torch_dev)
+    y3 = torch.full((n,), np.nan, dtype=torch.float64, device=torch_dev)
+    _sync()
+    lib = _lib()
+    assert lib.kr_spmv_csr_f64(rp.data_ptr(), rp64, col.data_ptr(), val.data_ptr(), n,
+                               xt.data_ptr(), y.data_ptr(), None) == 0
+    assert lib.kr_spmv2_csr_f64(rp.data_ptr(), rp64, col.data_ptr(), val.data_ptr(), n,
+                                xt.data_ptr(), x2t.data_ptr(), y2.data_ptr(), y3.data_ptr(),
+                                None) == 0
+    _sync()
+    ref = A.dot(x)
+    np.testing.assert_array_equal(y.cpu().numpy(), ref)
+    np.testing.assert_array_equal(y2.cpu().numpy(), ref)
+    np.testing.assert_array_equal(y3.cpu().numpy(), A.dot(x2))
+
+
+def test_spmv_empty_and_errors(torch_dev):
+    lib = _lib()
+    assert lib.kr_spmv_csr_f64(None, 0, None, None, 0, None, None, None) == 0  # n = 0
+    assert lib.kr_spmv_csr_f64(None, 0, None, None, 5, None, None, None) < 0
+    assert b"NULL" in lib.kr_last_error()
+
+
+@pytest.mark.parametrize("n", [1, 2, 255, 256, 257, 100003, 3 * 2 ** 20 + 1])
+def test_dot_deterministic_and_accurate(torch_dev, n):
+    import torch
+    rng = np.random.default_rng(n)
+    u = rng.standard_normal(n)
+    v = rng.standard_normal(n)
+    ut, vt = _t(u, torch_dev), _t(v, torch_dev)
+    out = torch.zeros(2, dtype=torch.float64, device=torch_dev)
+    _sync()
+    lib = _lib()
+    for i in range(2):
+        assert lib.kr_dot_f64(ut.data_ptr(), vt.data_ptr(), n, out[i:].data_ptr(), None) == 0
+    _sync()
+    o = out.cpu().numpy()
+    assert o[0] == o[1]  # deterministic
+    exact = math.fsum(u * v)
+    bound = 2 * n * np.finfo(float).eps * float(np.abs(u * v).sum()) + 1e-300
+    assert abs(o[0] - exact) <= bound
+
+
+def test_multidot_matches_dot(torch_dev):
+    import torch
+    n = 50001
+    rng = np.random.default_rng(0)
+    V = [_t(rng.standard_normal(n), torch_dev) for _ in range(5)]
+    pairs = [(i, j) for i in range(5) for j in range(i, 5)][:13]
+    us = (ctypes.c_void_p * len(pairs))(*[V[i].data_ptr() for i, _ in pairs])
+    vs = (ctypes.c_void_p * len(pairs))(*[V[j].data_ptr() for _, j in pairs])
+    out = torch.zeros(len(pairs), dtype=torch.float64, device=torch_dev)
+    _sync()
+    assert _lib().kr_multidot_f64(us, vs, len(pairs), n, out.data_ptr(), None) == 0
+    _sync()
+    Vh = [t.cpu().numpy() for t in V]
+    for q, (i, j) in enumerate(pairs):
+        exact = math.fsum(Vh[i] * Vh[j])
+        assert abs(out[q].item() - exact) <= 1e-12 * np.abs(Vh[i] * Vh[j]).sum()
+
+
+@pytest.mark.parametrize("n,offset", [(1, 0), (4097, 0), (4097, 1), (300000, 0)])
+@pytest.mark.parametrize("first", [0, 1])
+def test_update_mrr_bitwise(torch_dev, n, offset, first):
+    import torch
+    rng = np.random.default_rng(n + first)
+    y, ar1, z, r, x = [rng.standard_normal(n + offset) for _ in range(5)]
+    eta, zeta = -0.3141592653589793, 1.2345678901234567
+    T = [_t(a, torch_dev) for a in (y, ar1, z, r, x)]
+    P = [t[offset:].data_ptr() for t in T]  # offset 1: unaligned, scalar path
+    _sync()
+    assert _lib().kr_update_mrr_f64(eta, zeta, first, P[0], P[1], P[2], P[3], P[4], n,
+                                    None) == 0
+    _sync()
+    y, ar1, z, r, x = [a[offset:] for a in (y, ar1, z, r, x)]
+    if first:
+        y_ref = zeta * ar1
+        z_ref = -zeta * r
+    else:
+        y_ref = eta * y + zeta * ar1
+        z_ref = eta * z - zeta * r
+    r_ref = r - y_ref
+    x_ref = x - z_ref
+    for t, ref in zip((T[0], T[2], T[3], T[4]), (y_ref, z_ref, r_ref, x_ref)):
+        np.testing.assert_array_equal(t[offset:].cpu().numpy(), ref)
+
+
+def test_update_cg_bitwise(torch_dev):
+    n = 12345
+    rng = np.random.default_rng(5)
+    x, p, r, v = [rng.standard_normal(n) for _ in range(4)]
+    alpha = 0.7071067811865476
+    T = [_t(a, torch_dev) for a in (x, p, r, v)]
+    _sync()
+    assert _lib().kr_update_cg_f64(alpha, *[t.data_ptr() for t in T], n, None) == 0
+    _sync()
+    np.testing.assert_array_equal(T[0].cpu().numpy(), x + alpha * p)
+    np.testing.assert_array_equal(T[2].cpu().numpy(), r - alpha * v)
+
+
+@pytest.mark.parametrize("spec,shards", [
+    (("poisson", 19, 2), 1), (("poisson", 13, 3), 1), (("poisson", 13, 3), 3),
+    (("banded", 4099, 13, 64, 0), 1), (("banded", 4099, 13, 64, 0), 4),
+    (("banded", 3000, 31, 256, 5), 2),
+])
+def test_device_generators_and_sharded_spmv_bitwise(torch_dev, spec, shards):
+    from parallel_krylov_amd.system import KrylovSystem, balanced_partition
+    A = golden_matrix(list(spec))
+    n = A.shape[0]
+    sysm = KrylovSystem(n, balanced_partition(n, shards), [0] * shards)
+    if spec[0] == "poisson":
+        sysm.gen_poisson(spec[1], spec[2])
+    else:
+        sysm.gen_banded(spec[2], spec[3], spec[4])
+    sysm.finalize()
+    for s in range(shards):
+        r0, r1 = sysm.shard_rows(s)
+        assert sysm.shard_info(s)["nnz"] == A[r0:r1].nnz
+    x = np.random.default_rng(3).standard_normal(n)
+    y = sysm.gather(sysm.spmv(sysm.split(x))).cpu().numpy()
+    np.testing.assert_array_equal(y, A.dot(x))
+    b = sysm.gather(sysm.rhs(11)).cpu().numpy()
+    np.testing.assert_array_equal(b, matrices.rhs(n, 11))
+    sysm.close()
+
+
+def test_adopted_csr_sharded_spmv_bitwise(torch_dev):
+    from parallel_krylov_amd.system import KrylovSystem, balanced_partition
+    A = _irregular(3000, 2)
+    n = A.shape[0]
+    for shards in (1, 2, 5):
+        sysm = KrylovSystem(n, balanced_partition(n, shards), [0] * shards)
+        sysm.set_matrix(A)
+        sysm.finalize()
+        x = np.random.default_rng(shards).standard_normal(n)
+        y = sysm.gather(sysm.spmv(sysm.split(x))).cpu().numpy()
+        np.testing.assert_array_equal(y, A.dot(x))
+        sysm.close()

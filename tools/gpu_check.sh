@@ -1,0 +1,15 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, a short bench. Stops at the first
+# crash/timeout (exit codes other than pytest's "tests failed" = 1).
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 ${PYTEST_TIMEOUT:-900} python -m pytest tests -m gpu -q -p no:cacheprovider ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+timeout -k 10 600 python bench.py ${BENCH_ARGS:---steps 10 --warmup 2} > gpurun_out/bench.log 2>&1
+rc=$?; echo "bench rc=$rc"; tail -c 3000 gpurun_out/bench.log
+exit $rc
