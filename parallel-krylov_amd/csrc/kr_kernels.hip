@@ -149,20 +149,30 @@ __device__ __forceinline__ void epi_products(double x, double x2, double y, doub
 
 // ---------------------------------------------------------------------------
 // CSR SpMV, one lane per row, matrix entries staged through LDS.
-//   Row block = kBlock consecutive rows; its nnz range is copied into LDS in
-//   windows of kWindow entries with coalesced loads, then each lane walks its
-//   own row inside the window in stored order and gathers x[col].
+//   Row block = kBlock consecutive rows. Its nnz range is staged into LDS in
+//   windows of kWindow entries: every lane first issues all of its 16-byte
+//   loads (4 entries per slot, kSlots slots: vals as 2 x 16 B, cols as 16 B),
+//   then writes them to LDS, so a wave has 3*kSlots loads in flight instead of
+//   a load/wait/store chain. Each lane then walks its own row inside the
+//   window in stored order, issuing up to kGather x-gathers before it adds
+//   them -- in order -- to its running sum (bitwise scipy csr_matvec).
 //   Grid-stride over row blocks; reductions accumulate per lane across row
 //   blocks and are reduced once per workgroup at the end.
 // ---------------------------------------------------------------------------
-template <typename RP, int EPI>
+typedef double dbl2v __attribute__((ext_vector_type(2)));
+typedef int int4v __attribute__((ext_vector_type(4)));
+constexpr int kSlots = kWindow / (4 * kBlock);
+constexpr int kGather = 8;
+static_assert(kSlots * 4 * kBlock == kWindow, "window must be a multiple of 4*kBlock");
+
+template <typename RP, int EPI, bool VEC>
 __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
   using T = EpiTraits<EPI>;
   constexpr int NP = T::NP;
   constexpr int NV = T::NV;
-  __shared__ double s_val[kWindow];
-  __shared__ int32_t s_col[kWindow];
-  __shared__ int64_t s_rp[kBlock + 1];
+  __shared__ __attribute__((aligned(16))) double s_val[kWindow];
+  __shared__ __attribute__((aligned(16))) int32_t s_col[kWindow];
+  __shared__ int32_t s_rp[kBlock + 1];  // row pointers relative to the block start
   __shared__ double s_red[(NP > 0 ? NP : 1) * 4];
 
   const RP* __restrict__ rowptr = static_cast<const RP*>(a.rowptr);
@@ -180,29 +190,73 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
   for (int64_t rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
     const int64_t r0 = rb * kBlock;
     const int nr = (int)min((int64_t)kBlock, a.n - r0);
-    if (tid < nr) s_rp[tid] = (int64_t)rowptr[r0 + tid];
-    if (tid == 0) s_rp[nr] = (int64_t)rowptr[r0 + nr];
+    const int64_t bs = (int64_t)rowptr[r0];
+    const int64_t be = (int64_t)rowptr[r0 + nr];
+    if (tid < nr) s_rp[tid + 1] = (int32_t)((int64_t)rowptr[r0 + tid + 1] - bs);
+    if (tid == 0) s_rp[0] = 0;
     __syncthreads();
-    const int64_t bs = s_rp[0], be = s_rp[nr];
     const bool active = tid < nr;
-    const int64_t rs = active ? s_rp[tid] : 0;
-    const int64_t re = active ? s_rp[tid + 1] : 0;
+    const int rs = active ? s_rp[tid] : 0;
+    const int re = active ? s_rp[tid + 1] : 0;
     double sum1 = 0.0, sum2 = 0.0;
-    for (int64_t ws = bs; ws < be; ws += kWindow) {
-      const int wn = (int)min((int64_t)kWindow, be - ws);
-      for (int j = tid; j < wn; j += kBlock) {
-        s_val[j] = __builtin_nontemporal_load(val + ws + j);
-        s_col[j] = __builtin_nontemporal_load(col + ws + j);
+    // windows start 4-aligned so every slot is one 16-byte access
+    const int64_t w0 = VEC ? (bs & ~(int64_t)3) : bs;
+    for (int64_t ws = w0; ws < be; ws += kWindow) {
+      dbl2v v_lo[kSlots], v_hi[kSlots];
+      int4v c4[kSlots];
+#pragma unroll
+      for (int q = 0; q < kSlots; ++q) {
+        const int e0 = (tid + q * kBlock) * 4;
+        const int64_t g0 = ws + e0;
+        if (VEC && g0 >= bs && g0 + 4 <= be) {
+          v_lo[q] = __builtin_nontemporal_load(reinterpret_cast<const dbl2v*>(val + g0));
+          v_hi[q] = __builtin_nontemporal_load(reinterpret_cast<const dbl2v*>(val + g0 + 2));
+          c4[q] = __builtin_nontemporal_load(reinterpret_cast<const int4v*>(col + g0));
+        } else {
+          double tv[4];
+          int tc[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int64_t g = g0 + u;
+            const bool ok = g >= bs && g < be;
+            tv[u] = ok ? val[g] : 0.0;
+            tc[u] = ok ? col[g] : 0;
+          }
+          v_lo[q] = dbl2v{tv[0], tv[1]};
+          v_hi[q] = dbl2v{tv[2], tv[3]};
+          c4[q] = int4v{tc[0], tc[1], tc[2], tc[3]};
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < kSlots; ++q) {
+        const int e0 = (tid + q * kBlock) * 4;
+        *reinterpret_cast<dbl2v*>(&s_val[e0]) = v_lo[q];
+        *reinterpret_cast<dbl2v*>(&s_val[e0 + 2]) = v_hi[q];
+        *reinterpret_cast<int4v*>(&s_col[e0]) = c4[q];
       }
       __syncthreads();
       if (active) {
-        const int js = (int)max(rs - ws, (int64_t)0);
-        const int je = (int)min(re - ws, (int64_t)wn);
-        for (int j = js; j < je; ++j) {
-          const double v = s_val[j];
-          const int c = s_col[j];
-          sum1 = sum1 + v * x1[c];
-          if constexpr (NV == 2) sum2 = sum2 + v * x2[c];
+        // this lane's entries inside the window, as window offsets
+        const int64_t off = bs - ws;  // window offset of the block's entry 0
+        const int js = (int)max((int64_t)rs + off, (int64_t)0);
+        const int je = (int)min((int64_t)re + off, (int64_t)kWindow);
+        for (int j = js; j < je; j += kGather) {
+          double v[kGather], p1[kGather], p2[kGather];
+#pragma unroll
+          for (int u = 0; u < kGather; ++u) {
+            const int jj = (j + u < je) ? j + u : js;
+            v[u] = s_val[jj];
+            const int c = s_col[jj];
+            p1[u] = x1[c];
+            if constexpr (NV == 2) p2[u] = x2[c];
+          }
+#pragma unroll
+          for (int u = 0; u < kGather; ++u) {
+            if (j + u < je) {
+              sum1 = sum1 + v[u] * p1[u];
+              if constexpr (NV == 2) sum2 = sum2 + v[u] * p2[u];
+            }
+          }
         }
       }
       __syncthreads();
@@ -225,13 +279,13 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
   block_reduce_store<NP>(acc, a.partials, a.grid, s_red);
 }
 
-template <typename RP>
+template <typename RP, bool VEC>
 void spmv_dispatch(SpmvEpi epi, const SpmvArgs& a, hipStream_t s) {
   const dim3 grid(a.grid), block(kBlock);
   switch (epi) {
 #define KR_CASE(E) \
   case E:          \
-    spmv_kernel<RP, E><<<grid, block, 0, s>>>(a); \
+    spmv_kernel<RP, E, VEC><<<grid, block, 0, s>>>(a); \
     break;
     KR_CASE(EPI_NONE)
     KR_CASE(EPI_BMINUS)
@@ -617,10 +671,20 @@ int spmv_products(SpmvEpi epi) {
 
 void launch_spmv(SpmvEpi epi, const SpmvArgs& a, hipStream_t s) {
   KR_REQUIRE(a.grid > 0, "spmv: grid must be positive");
-  if (a.rowptr64)
-    spmv_dispatch<int64_t>(epi, a, s);
-  else
-    spmv_dispatch<int32_t>(epi, a, s);
+  // 16-byte staging needs 16-byte aligned val/col bases
+  const bool vec = ((reinterpret_cast<uintptr_t>(a.val) | reinterpret_cast<uintptr_t>(a.col)) &
+                    15) == 0;
+  if (a.rowptr64) {
+    if (vec)
+      spmv_dispatch<int64_t, true>(epi, a, s);
+    else
+      spmv_dispatch<int64_t, false>(epi, a, s);
+  } else {
+    if (vec)
+      spmv_dispatch<int32_t, true>(epi, a, s);
+    else
+      spmv_dispatch<int32_t, false>(epi, a, s);
+  }
   KR_HIP_CHECK(hipGetLastError());
 }
 

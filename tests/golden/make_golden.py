@@ -16,9 +16,10 @@ Two harness shims are needed, and only here:
 Each case file stores the inputs (matrix spec + sha256 of its CSR arrays, b,
 x0, parameters) and the reference's outputs (x, residual, nosl, khistory), plus
 an ``envelope``: the per-entry relative change of the residual history when
-the oracle's dot products are summed in a different order (blocked partial
-sums, as a GPU does). It is the measured rounding sensitivity of each entry
- and scales the tolerance of the GPU parity tests.
+the oracle's dot products are summed in other orders (max over blocked partial
+sums as a GPU does, the exactly rounded sum, and six shuffled pairwise sums).
+It is the measured rounding sensitivity of each entry and
+scales the tolerance of the GPU parity tests.
 """
 from __future__ import annotations
 
@@ -107,12 +108,30 @@ def blocked_dot(u, v, block=256):
     return np.float64(total)
 
 
-def run_perturbed(method, A, b, kwargs):
+def exact_dot(u, v):
+    return np.float64(math.fsum(np.asarray(u, dtype=np.float64) * np.asarray(v, dtype=np.float64)))
+
+
+def permuted_dot(seed):
+    def dot(u, v):
+        p = np.asarray(u, dtype=np.float64) * np.asarray(v, dtype=np.float64)
+        perm = np.random.default_rng(seed + p.size).permutation(p.size)
+        return np.float64(np.sum(p[perm]))
+    return dot
+
+
+# Summation orders a GPU reduction could plausibly use: blocked partial sums,
+# exactly rounded, and pairwise sums of shuffled products.
+PERTURBATIONS = [blocked_dot, exact_dot] + [permuted_dot(s) for s in range(6)]
+
+
+def run_perturbed(method, A, b, kwargs, dot):
     saved = (v3cpu._dot, v3cpu._norm)
-    v3cpu._dot = blocked_dot
-    v3cpu._norm = lambda v: np.float64(math.sqrt(blocked_dot(v, v)))
+    v3cpu._dot = dot
+    v3cpu._norm = lambda v: np.float64(math.sqrt(dot(v, v)))
     try:
-        return v3cpu.METHODS[method](A, b, **kwargs)
+        with np.errstate(all="ignore"):
+            return v3cpu.METHODS[method](A, b, **kwargs)
     finally:
         v3cpu._dot, v3cpu._norm = saved
 
@@ -130,17 +149,24 @@ def main():
             kwargs["k"] = c["k"]
         with contextlib.redirect_stdout(io.StringIO()):
             x, info = ref[c["method"]](A, b, x=None if x0 is None else x0.copy(), **kwargs)
-        xp, infop = run_perturbed(c["method"], A, b, dict(kwargs, x=x0))
         res = np.asarray(info["residual"], dtype=np.float64)
-        resp = np.asarray(infop["residual"], dtype=np.float64)
-        m = min(res.size, resp.size)
-        env = np.full(res.size, np.inf)
-        env[:m] = np.abs(resp[:m] - res[:m]) / np.maximum(np.abs(res[:m]), 1e-300)
+        env = np.zeros(res.size)
+        x_env = 0.0
+        same_length = True
+        for dot in PERTURBATIONS:
+            xp, infop = run_perturbed(c["method"], A, b, dict(kwargs, x=x0), dot)
+            resp = np.asarray(infop["residual"], dtype=np.float64)
+            m = min(res.size, resp.size)
+            d = np.full(res.size, np.inf)
+            d[:m] = np.abs(resp[:m] - res[:m]) / np.maximum(np.abs(res[:m]), 1e-300)
+            env = np.maximum(env, d)
+            same_length &= resp.size == res.size and np.array_equal(infop["nosl"], info["nosl"])
+            x_env = max(x_env, float(np.linalg.norm(xp - x) / np.linalg.norm(x)))
         out = dict(
             b=b, x=np.asarray(x, dtype=np.float64), residual=res,
             nosl=np.asarray(info["nosl"], dtype=np.int64), envelope=env,
-            x_envelope=np.float64(np.linalg.norm(xp - x) / np.linalg.norm(x)),
-            same_length=np.bool_(res.size == resp.size),
+            x_envelope=np.float64(x_env),
+            same_length=np.bool_(same_length),
         )
         if x0 is not None:
             out["x0"] = x0

@@ -47,11 +47,15 @@ def check_parity(c, g, x, info):
     x = x.cpu().numpy() if hasattr(x, "cpu") else np.asarray(x)
     res, gres = info["residual"], g["residual"]
     if _chaotic(g):
+        # The reference itself is not reproducible under a change of summation
+        # order here: check the entries that are stable, then structure.
         assert res[-1] < c["tol"] or (c["maxiter"] is not None)
-        n_early = int(np.argmax(gres < 1e-6)) if (gres < 1e-6).any() else gres.size
-        n_early = min(n_early, res.size)
-        np.testing.assert_allclose(res[:n_early], gres[:n_early], rtol=1e-8)
-        assert abs(int(info["nosl"][-1]) - int(g["nosl"][-1])) <= 0.25 * g["nosl"][-1]
+        env = g["envelope"]
+        stable = np.nonzero(np.cumprod(np.isfinite(env) & (env < 1e-7)))[0]
+        m = min(stable.size, res.size)
+        rel = np.abs(res[:m] - gres[:m]) / np.abs(gres[:m])
+        assert np.all(rel <= np.maximum(1e-12, 10 * env[:m])), rel
+        assert abs(int(info["nosl"][-1]) - int(g["nosl"][-1])) <= 0.5 * g["nosl"][-1]
         if "khistory" in g:
             kh = info["khistory"]
             assert np.all(np.diff(kh) <= 0) and kh[0] == g["khistory"][0]
