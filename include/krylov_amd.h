@@ -148,6 +148,10 @@ int kr_system_gen_banded(kr_system* sys, int h, int64_t width, uint64_t seed,
 /* Column remap, halo plan, row blocks and workspaces. Call once after the
  * matrix of every shard is set. */
 int kr_system_finalize(kr_system* sys);
+/* Device CSR arrays of shard s (after finalize: LOCAL column numbering, own
+ * row r of the halo-extended vector sits at index pad + r; see shard_info). */
+int kr_system_csr(kr_system* sys, int shard, const void** rowptr_dev, int* rowptr64,
+                  const int32_t** col_dev, const double** val_dev, int64_t* pad);
 /* Info: n_local, halo_lo, halo_hi, nnz of shard s. */
 int kr_system_shard_info(kr_system* sys, int shard, int64_t* n_local, int64_t* halo_lo,
                          int64_t* halo_hi, int64_t* nnz);

@@ -81,6 +81,7 @@ _SIGNATURES = {
     "kr_system_finalize": [_P],
     "kr_system_shard_info": [_P, _I, _PI64, _PI64, _PI64, _PI64],
     "kr_fill_rhs": [_P, _I, _U64, _P],
+    "kr_system_csr": [_P, _I, _PP, _PI, _PP, _PP, _PI64],
     "kr_system_spmv": [_PP, _PP, _PP],
     "kr_solve_begin": [_P, ctypes.POINTER(SolveParams), _PP, _PP],
     "kr_solve_step": [_P, _I64, _PI],

@@ -458,6 +458,19 @@ int kr_system_shard_info(kr_system* sys, int shard, int64_t* n_local, int64_t* h
   });
 }
 
+int kr_system_csr(kr_system* sys, int shard, const void** rowptr, int* rowptr64,
+                  const int32_t** col, const double** val, int64_t* pad) {
+  return guarded([&] {
+    KR_REQUIRE(sys && shard >= 0 && shard < (int)sys->shards.size(), "bad shard");
+    const Shard& s = sys->shards[shard];
+    if (rowptr) *rowptr = s.rowptr;
+    if (rowptr64) *rowptr64 = s.rowptr64;
+    if (col) *col = s.col;
+    if (val) *val = s.val;
+    if (pad) *pad = s.pad;
+  });
+}
+
 int kr_fill_rhs(kr_system* sys, int shard, uint64_t seed, double* b) {
   return guarded([&] {
     KR_REQUIRE(sys && shard >= 0 && shard < (int)sys->shards.size(), "bad shard");

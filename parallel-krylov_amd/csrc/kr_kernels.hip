@@ -10,6 +10,8 @@
 // run to run, but they are not OpenBLAS's order.
 #include <hipcub/hipcub.hpp>
 
+#include <cstdlib>
+
 #include "kr_hash.h"
 #include "kr_internal.h"
 
@@ -165,8 +167,209 @@ constexpr int kSlots = kWindow / (4 * kBlock);
 constexpr int kGather = 8;
 static_assert(kSlots * 4 * kBlock == kWindow, "window must be a multiple of 4*kBlock");
 
+// Registers holding one staged window. Values move as one 16-byte double2 per
+// lane per slot and columns as one 16-byte int4, so consecutive lanes touch
+// consecutive 16-byte LDS slots (bank-conflict-free ds_write_b128) and every
+// wave-instruction reads 1 KiB of contiguous HBM.
+constexpr int kVSlots = kWindow / (2 * kBlock);
+constexpr int kCSlots = kWindow / (4 * kBlock);
+struct Stage {
+  dbl2v v[kVSlots];
+  int4v c[kCSlots];
+};
+
+template <bool VEC>
+__device__ __forceinline__ void stage_load(Stage& st, const double* __restrict__ val,
+                                           const int32_t* __restrict__ col, int64_t ws,
+                                           int64_t bs, int64_t be, int tid) {
+#pragma unroll
+  for (int q = 0; q < kVSlots; ++q) {
+    const int64_t g0 = ws + (int64_t)(tid + q * kBlock) * 2;
+    if (VEC && g0 >= bs && g0 + 2 <= be) {
+      st.v[q] = *reinterpret_cast<const dbl2v*>(val + g0);
+    } else {
+      const bool ok0 = g0 >= bs && g0 < be, ok1 = g0 + 1 >= bs && g0 + 1 < be;
+      st.v[q] = dbl2v{ok0 ? val[g0] : 0.0, ok1 ? val[g0 + 1] : 0.0};
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < kCSlots; ++q) {
+    const int64_t g0 = ws + (int64_t)(tid + q * kBlock) * 4;
+    if (VEC && g0 >= bs && g0 + 4 <= be) {
+      st.c[q] = *reinterpret_cast<const int4v*>(col + g0);
+    } else {
+      int tc[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t g = g0 + u;
+        tc[u] = (g >= bs && g < be) ? col[g] : 0;
+      }
+      st.c[q] = int4v{tc[0], tc[1], tc[2], tc[3]};
+    }
+  }
+}
+
+__device__ __forceinline__ void stage_commit(const Stage& st, double* s_val, int32_t* s_col,
+                                             int tid) {
+#pragma unroll
+  for (int q = 0; q < kVSlots; ++q) reinterpret_cast<dbl2v*>(s_val)[tid + q * kBlock] = st.v[q];
+#pragma unroll
+  for (int q = 0; q < kCSlots; ++q) reinterpret_cast<int4v*>(s_col)[tid + q * kBlock] = st.c[q];
+}
+
+// One lane's entries [js, je) of the staged window, in stored order.
+template <int NV>
+__device__ __forceinline__ void row_window(const double* s_val, const int32_t* s_col,
+                                           const double* __restrict__ x1,
+                                           const double* __restrict__ x2, int js, int je,
+                                           double& sum1, double& sum2) {
+  for (int j = js; j < je; j += kGather) {
+    double v[kGather], p1[kGather], p2[kGather];
+#pragma unroll
+    for (int u = 0; u < kGather; ++u) {
+      const int jj = (j + u < je) ? j + u : js;
+      v[u] = s_val[jj];
+      const int c = s_col[jj];
+      p1[u] = x1[c];
+      if constexpr (NV == 2) p2[u] = x2[c];
+    }
+#pragma unroll
+    for (int u = 0; u < kGather; ++u) {
+      if (j + u < je) {
+        sum1 = sum1 + v[u] * p1[u];
+        if constexpr (NV == 2) sum2 = sum2 + v[u] * p2[u];
+      }
+    }
+  }
+}
+
+// Software pipeline over row blocks: while a row block is multiplied out of
+// LDS, the row pointers and the first staged window of the NEXT row block of
+// this workgroup are already in flight (registers), so the load latency of
+// block b+1 hides under the gathers of block b.
 template <typename RP, int EPI, bool VEC>
 __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
+  using T = EpiTraits<EPI>;
+  constexpr int NP = T::NP;
+  constexpr int NV = T::NV;
+  __shared__ __attribute__((aligned(16))) double s_val[kWindow];
+  __shared__ __attribute__((aligned(16))) int32_t s_col[kWindow];
+  __shared__ int32_t s_rp[kBlock + 1];  // row pointers relative to the block start
+  __shared__ double s_red[(NP > 0 ? NP : 1) * 4];
+
+  const RP* __restrict__ rowptr = static_cast<const RP*>(a.rowptr);
+  const double* __restrict__ val = a.val;
+  const int32_t* __restrict__ col = a.col;
+  const double* __restrict__ x1 = a.x1;
+  const double* __restrict__ x2 = a.x2;
+  const int tid = threadIdx.x;
+
+  double acc[NP > 0 ? NP : 1];
+#pragma unroll
+  for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;
+
+  const int64_t nrb = (a.n + kBlock - 1) / kBlock;
+  int64_t rb = blockIdx.x;
+  if (rb >= nrb) {
+    block_reduce_store<NP>(acc, a.partials, a.grid, s_red);
+    return;
+  }
+  // prologue: row block rb in flight, and the nnz range of the next one
+  // (scalar loads) requested, so that no iteration waits on a row-pointer
+  // load before it can issue the next block's staging.
+  auto block_rows = [&](int64_t b) { return (int)min((int64_t)kBlock, a.n - b * kBlock); };
+  Stage st;
+  int64_t r0 = rb * kBlock;
+  int nr = block_rows(rb);
+  int64_t bs = (int64_t)rowptr[r0];
+  int64_t be = (int64_t)rowptr[r0 + nr];
+  int64_t my_end = tid < nr ? (int64_t)rowptr[r0 + tid + 1] : 0;
+  stage_load<VEC>(st, val, col, VEC ? (bs & ~(int64_t)3) : bs, bs, be, tid);
+  int64_t bsn = 0, ben = 0;
+  if (rb + gridDim.x < nrb) {
+    const int64_t r0n = (rb + gridDim.x) * kBlock;
+    bsn = (int64_t)rowptr[r0n];
+    ben = (int64_t)rowptr[r0n + block_rows(rb + gridDim.x)];
+  }
+
+  for (;;) {
+    const int64_t ws0 = VEC ? (bs & ~(int64_t)3) : bs;
+    if (tid < nr) s_rp[tid + 1] = (int32_t)(my_end - bs);
+    if (tid == 0) s_rp[0] = 0;
+    stage_commit(st, s_val, s_col, tid);
+    __syncthreads();
+    const bool active = tid < nr;
+    const int rs = active ? s_rp[tid] : 0;
+    const int re = active ? s_rp[tid + 1] : 0;
+
+    // issue the next row block's loads before computing this one; its nnz
+    // range (bsn, ben) was requested one iteration ago, the one after it now
+    const int64_t rb_next = rb + gridDim.x;
+    const bool has_next = rb_next < nrb;
+    int64_t r0n = 0, my_end_n = 0, bsnn = 0, benn = 0;
+    int nrn = 0;
+    if (has_next) {
+      r0n = rb_next * kBlock;
+      nrn = block_rows(rb_next);
+      my_end_n = tid < nrn ? (int64_t)rowptr[r0n + tid + 1] : 0;
+      stage_load<VEC>(st, val, col, VEC ? (bsn & ~(int64_t)3) : bsn, bsn, ben, tid);
+      const int64_t rb_nn = rb_next + gridDim.x;
+      if (rb_nn < nrb) {
+        const int64_t r0nn = rb_nn * kBlock;
+        bsnn = (int64_t)rowptr[r0nn];
+        benn = (int64_t)rowptr[r0nn + block_rows(rb_nn)];
+      }
+    }
+
+    double sum1 = 0.0, sum2 = 0.0;
+    const int64_t off0 = bs - ws0;  // window offset of this block's entry 0
+    if (active)
+      row_window<NV>(s_val, s_col, x1, x2, (int)max((int64_t)rs + off0, (int64_t)0),
+                     (int)min((int64_t)re + off0, (int64_t)kWindow), sum1, sum2);
+    // rare: row blocks whose entries span more than one window
+    for (int64_t ws = ws0 + kWindow; ws < be; ws += kWindow) {
+      __syncthreads();
+      Stage extra;
+      stage_load<VEC>(extra, val, col, ws, bs, be, tid);
+      stage_commit(extra, s_val, s_col, tid);
+      __syncthreads();
+      const int64_t off = bs - ws;
+      if (active)
+        row_window<NV>(s_val, s_col, x1, x2, (int)max((int64_t)rs + off, (int64_t)0),
+                       (int)min((int64_t)re + off, (int64_t)kWindow), sum1, sum2);
+    }
+    if (active) {
+      const int64_t row = r0 + tid;
+      double y1 = sum1;
+      if constexpr (EPI == EPI_BMINUS) y1 = a.b[row] - sum1;
+      a.y1[row] = y1;
+      if constexpr (NV == 2) a.y2[row] = sum2;
+      if constexpr (NP > 0) {
+        const double xv = T::kX ? x1[a.xoff + row] : 0.0;
+        const double x2v = T::kX2 ? x2[a.xoff + row] : 0.0;
+        const double ev = T::kE ? a.e[row] : 0.0;
+        epi_products<EPI>(xv, x2v, y1, sum2, ev, acc);
+      }
+    }
+    if (!has_next) break;
+    __syncthreads();  // LDS and s_rp are rewritten by the next row block
+    rb = rb_next;
+    r0 = r0n;
+    nr = nrn;
+    bs = bsn;
+    be = ben;
+    bsn = bsnn;
+    ben = benn;
+    my_end = my_end_n;
+  }
+  __syncthreads();
+  block_reduce_store<NP>(acc, a.partials, a.grid, s_red);
+}
+
+// Variant 1: no cross-row-block prefetch (lower VGPR count, higher occupancy).
+// DBG (timing diagnostics only, results are wrong): 1 = no x gather.
+template <typename RP, int EPI, bool VEC, int DBG = 0>
+__global__ __launch_bounds__(kBlock) void spmv_kernel_simple(SpmvArgs a) {
   using T = EpiTraits<EPI>;
   constexpr int NP = T::NP;
   constexpr int NV = T::NV;
@@ -202,37 +405,10 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
     // windows start 4-aligned so every slot is one 16-byte access
     const int64_t w0 = VEC ? (bs & ~(int64_t)3) : bs;
     for (int64_t ws = w0; ws < be; ws += kWindow) {
-      dbl2v v_lo[kSlots], v_hi[kSlots];
-      int4v c4[kSlots];
-#pragma unroll
-      for (int q = 0; q < kSlots; ++q) {
-        const int e0 = (tid + q * kBlock) * 4;
-        const int64_t g0 = ws + e0;
-        if (VEC && g0 >= bs && g0 + 4 <= be) {
-          v_lo[q] = __builtin_nontemporal_load(reinterpret_cast<const dbl2v*>(val + g0));
-          v_hi[q] = __builtin_nontemporal_load(reinterpret_cast<const dbl2v*>(val + g0 + 2));
-          c4[q] = __builtin_nontemporal_load(reinterpret_cast<const int4v*>(col + g0));
-        } else {
-          double tv[4];
-          int tc[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int64_t g = g0 + u;
-            const bool ok = g >= bs && g < be;
-            tv[u] = ok ? val[g] : 0.0;
-            tc[u] = ok ? col[g] : 0;
-          }
-          v_lo[q] = dbl2v{tv[0], tv[1]};
-          v_hi[q] = dbl2v{tv[2], tv[3]};
-          c4[q] = int4v{tc[0], tc[1], tc[2], tc[3]};
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < kSlots; ++q) {
-        const int e0 = (tid + q * kBlock) * 4;
-        *reinterpret_cast<dbl2v*>(&s_val[e0]) = v_lo[q];
-        *reinterpret_cast<dbl2v*>(&s_val[e0 + 2]) = v_hi[q];
-        *reinterpret_cast<int4v*>(&s_col[e0]) = c4[q];
+      {
+        Stage st;
+        stage_load<VEC>(st, val, col, ws, bs, be, tid);
+        stage_commit(st, s_val, s_col, tid);
       }
       __syncthreads();
       if (active) {
@@ -279,13 +455,137 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
   block_reduce_store<NP>(acc, a.partials, a.grid, s_red);
 }
 
+// Variant 2: wave-independent. Each wave owns 64-row blocks and a private
+// LDS window; staging and the row walk need only wave-local ordering (an
+// s_waitcnt on the LDS counter), never a workgroup barrier, so the four waves
+// of a workgroup stream independently.
+constexpr int kWaveRows = 64;
+constexpr int kWaveWindow = 512;  // entries per wave window (2 slots of 4 per lane)
+constexpr int kWaveSlots = kWaveWindow / (4 * kWaveRows);
+static_assert(kWaveSlots * 4 * kWaveRows == kWaveWindow, "wave window layout");
+
+__device__ __forceinline__ void lds_fence() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+template <typename RP, int EPI, bool VEC>
+__global__ __launch_bounds__(kBlock) void spmv_kernel_wave(SpmvArgs a) {
+  using T = EpiTraits<EPI>;
+  constexpr int NP = T::NP;
+  constexpr int NV = T::NV;
+  constexpr int kWaves = kBlock / 64;
+  __shared__ __attribute__((aligned(16))) double s_val_all[kWaves][kWaveWindow];
+  __shared__ __attribute__((aligned(16))) int32_t s_col_all[kWaves][kWaveWindow];
+  __shared__ double s_red[(NP > 0 ? NP : 1) * 4];
+
+  const RP* __restrict__ rowptr = static_cast<const RP*>(a.rowptr);
+  const double* __restrict__ val = a.val;
+  const int32_t* __restrict__ col = a.col;
+  const double* __restrict__ x1 = a.x1;
+  const double* __restrict__ x2 = a.x2;
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  double* s_val = s_val_all[w];
+  int32_t* s_col = s_col_all[w];
+
+  double acc[NP > 0 ? NP : 1];
+#pragma unroll
+  for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;
+
+  const int64_t nwb = (a.n + kWaveRows - 1) / kWaveRows;
+  const int64_t gw = (int64_t)blockIdx.x * kWaves + w;
+  const int64_t nwaves = (int64_t)gridDim.x * kWaves;
+  for (int64_t wb = gw; wb < nwb; wb += nwaves) {
+    const int64_t r0 = wb * kWaveRows;
+    const int nr = (int)min((int64_t)kWaveRows, a.n - r0);
+    const int64_t bs = (int64_t)rowptr[r0];
+    const int64_t be = (int64_t)rowptr[r0 + nr];
+    const bool active = lane < nr;
+    const int64_t my_end = active ? (int64_t)rowptr[r0 + lane + 1] : be;
+    // row start = previous lane's end (lane 0: block start)
+    const int64_t my_beg = !active ? be : lane == 0 ? bs : (int64_t)rowptr[r0 + lane];
+    const int rs = (int)(my_beg - bs), re = (int)(my_end - bs);
+    double sum1 = 0.0, sum2 = 0.0;
+    const int64_t w0 = VEC ? (bs & ~(int64_t)3) : bs;
+    for (int64_t ws = w0; ws < be; ws += kWaveWindow) {
+      dbl2v lo[kWaveSlots], hi[kWaveSlots];
+      int4v c4[kWaveSlots];
+#pragma unroll
+      for (int q = 0; q < kWaveSlots; ++q) {
+        const int64_t g0 = ws + (int64_t)(lane + q * 64) * 4;
+        if (VEC && g0 >= bs && g0 + 4 <= be) {
+          lo[q] = *reinterpret_cast<const dbl2v*>(val + g0);
+          hi[q] = *reinterpret_cast<const dbl2v*>(val + g0 + 2);
+          c4[q] = *reinterpret_cast<const int4v*>(col + g0);
+        } else {
+          double tv[4];
+          int tc[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int64_t g = g0 + u;
+            const bool ok = g >= bs && g < be;
+            tv[u] = ok ? val[g] : 0.0;
+            tc[u] = ok ? col[g] : 0;
+          }
+          lo[q] = dbl2v{tv[0], tv[1]};
+          hi[q] = dbl2v{tv[2], tv[3]};
+          c4[q] = int4v{tc[0], tc[1], tc[2], tc[3]};
+        }
+      }
+      lds_fence();  // previous window fully read by every lane of the wave
+#pragma unroll
+      for (int q = 0; q < kWaveSlots; ++q) {
+        const int e0 = (lane + q * 64) * 4;
+        *reinterpret_cast<dbl2v*>(&s_val[e0]) = lo[q];
+        *reinterpret_cast<dbl2v*>(&s_val[e0 + 2]) = hi[q];
+        *reinterpret_cast<int4v*>(&s_col[e0]) = c4[q];
+      }
+      lds_fence();  // window visible to every lane of the wave
+      if (active) {
+        const int64_t off = bs - ws;
+        row_window<NV>(s_val, s_col, x1, x2, (int)max((int64_t)rs + off, (int64_t)0),
+                       (int)min((int64_t)re + off, (int64_t)kWaveWindow), sum1, sum2);
+      }
+    }
+    if (active) {
+      const int64_t row = r0 + lane;
+      double y1 = sum1;
+      if constexpr (EPI == EPI_BMINUS) y1 = a.b[row] - sum1;
+      a.y1[row] = y1;
+      if constexpr (NV == 2) a.y2[row] = sum2;
+      if constexpr (NP > 0) {
+        const double xv = T::kX ? x1[a.xoff + row] : 0.0;
+        const double x2v = T::kX2 ? x2[a.xoff + row] : 0.0;
+        const double ev = T::kE ? a.e[row] : 0.0;
+        epi_products<EPI>(xv, x2v, y1, sum2, ev, acc);
+      }
+    }
+  }
+  block_reduce_store<NP>(acc, a.partials, a.grid, s_red);
+}
+
+template <typename RP, int E, bool VEC>
+void spmv_dbg(int dbg, dim3 grid, dim3 block, hipStream_t s, const SpmvArgs& a) {
+  if (dbg == 1) spmv_kernel_simple<RP, E, VEC, 1><<<grid, block, 0, s>>>(a);
+
+}
+
 template <typename RP, bool VEC>
 void spmv_dispatch(SpmvEpi epi, const SpmvArgs& a, hipStream_t s) {
   const dim3 grid(a.grid), block(kBlock);
+  const char* env = getenv("KR_SPMV_VARIANT");  // A/B knob: 0 pipelined (default), 1 simple
+  const int variant = env ? atoi(env) : 0;
   switch (epi) {
-#define KR_CASE(E) \
-  case E:          \
-    spmv_kernel<RP, E, VEC><<<grid, block, 0, s>>>(a); \
+#define KR_CASE(E)                                      \
+  case E:                                               \
+    if (variant == 1)                                   \
+      spmv_kernel_simple<RP, E, VEC><<<grid, block, 0, s>>>(a); \
+    else if (variant == 2)                              \
+      spmv_kernel_wave<RP, E, VEC><<<grid, block, 0, s>>>(a); \
+    else if (variant >= 11 && variant <= 23)            \
+      spmv_dbg<RP, E, VEC>(variant - 10, grid, block, s, a); \
+    else                                                \
+      spmv_kernel<RP, E, VEC><<<grid, block, 0, s>>>(a); \
     break;
     KR_CASE(EPI_NONE)
     KR_CASE(EPI_BMINUS)

@@ -217,6 +217,15 @@ class KrylovSystem:
         call("kr_system_shard_info", self.handle, s, *[ctypes.byref(t) for t in v])
         return dict(zip(("n_local", "halo_lo", "halo_hi", "nnz"), [t.value for t in v]))
 
+    def csr_pointers(self, s: int) -> dict:
+        """Raw device CSR of shard s (local columns after finalize)."""
+        rp, col, val = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        rp64, pad = ctypes.c_int(), ctypes.c_int64()
+        call("kr_system_csr", self.handle, s, ctypes.byref(rp), ctypes.byref(rp64),
+             ctypes.byref(col), ctypes.byref(val), ctypes.byref(pad))
+        return dict(rowptr=rp.value, rowptr64=rp64.value, col=col.value, val=val.value,
+                    pad=pad.value)
+
     # ------------------------------------------------------------- vectors
     def split(self, v) -> list:
         """Own-row device tensors of a full-length host/device vector."""
