@@ -60,23 +60,33 @@ def poisson(n_side: int, dim: int, dtype_index=np.int32) -> sp.csr_matrix:
         raise ValueError("dim must be 2 or 3")
     N = n_side ** dim
     strides = [n_side ** d for d in range(dim)]
-    g = np.arange(N, dtype=np.int64)
-    coords = [(g // s) % n_side for s in strides]
-    # column order: outer lower neighbours first, diagonal, inner upper first
-    cols, vals, masks = [], [], []
-    for d in reversed(range(dim)):
-        cols.append(g - strides[d]); vals.append(-1.0); masks.append(coords[d] > 0)
-    cols.append(g); vals.append(2.0 * dim); masks.append(np.ones(N, bool))
-    for d in range(dim):
-        cols.append(g + strides[d]); vals.append(-1.0); masks.append(coords[d] < n_side - 1)
-    C = np.stack(cols, axis=1)
-    M = np.stack(masks, axis=1)
-    V = np.broadcast_to(np.asarray(vals, dtype=np.float64), C.shape)
-    counts = M.sum(axis=1)
+    offsets = [-strides[d] for d in reversed(range(dim))] + [0] + strides
+    values = np.array([-1.0] * dim + [2.0 * dim] + [-1.0] * dim)
+
+    def stencil(g):
+        """(cols, mask) of rows g, slots in sorted column order."""
+        coords = [(g // s) % n_side for s in strides]
+        masks = [coords[d] > 0 for d in reversed(range(dim))] + [np.ones(g.size, bool)] + \
+                [coords[d] < n_side - 1 for d in range(dim)]
+        return np.stack([g + o for o in offsets], axis=1), np.stack(masks, axis=1)
+
+    chunk = 1 << 22  # rows per chunk: bounded temporaries at 512^3
     indptr = np.zeros(N + 1, dtype=np.int64)
-    np.cumsum(counts, out=indptr[1:])
-    A = sp.csr_matrix((V[M].copy(), C[M].astype(dtype_index), indptr.astype(dtype_index)),
-                      shape=(N, N))
+    for c0 in range(0, N, chunk):
+        g = np.arange(c0, min(N, c0 + chunk), dtype=np.int64)
+        _, M = stencil(g)
+        indptr[c0 + 1:c0 + 1 + g.size] = M.sum(axis=1)
+    np.cumsum(indptr, out=indptr)
+    nnz = int(indptr[-1])
+    indices = np.empty(nnz, dtype=dtype_index)
+    data = np.empty(nnz, dtype=np.float64)
+    for c0 in range(0, N, chunk):
+        g = np.arange(c0, min(N, c0 + chunk), dtype=np.int64)
+        C, M = stencil(g)
+        s0, s1 = indptr[c0], indptr[c0 + g.size]
+        indices[s0:s1] = C[M]
+        data[s0:s1] = np.broadcast_to(values, C.shape)[M]
+    A = sp.csr_matrix((data, indices, indptr.astype(dtype_index)), shape=(N, N))
     A.has_sorted_indices = True
     return A
 

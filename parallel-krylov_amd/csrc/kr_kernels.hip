@@ -218,15 +218,15 @@ __device__ __forceinline__ void stage_commit(const Stage& st, double* s_val, int
 }
 
 // One lane's entries [js, je) of the staged window, in stored order.
-template <int NV>
+template <int NV, int GATHER = kGather>
 __device__ __forceinline__ void row_window(const double* s_val, const int32_t* s_col,
                                            const double* __restrict__ x1,
                                            const double* __restrict__ x2, int js, int je,
                                            double& sum1, double& sum2) {
-  for (int j = js; j < je; j += kGather) {
-    double v[kGather], p1[kGather], p2[kGather];
+  for (int j = js; j < je; j += GATHER) {
+    double v[GATHER], p1[GATHER], p2[GATHER];
 #pragma unroll
-    for (int u = 0; u < kGather; ++u) {
+    for (int u = 0; u < GATHER; ++u) {
       const int jj = (j + u < je) ? j + u : js;
       v[u] = s_val[jj];
       const int c = s_col[jj];
@@ -234,7 +234,7 @@ __device__ __forceinline__ void row_window(const double* s_val, const int32_t* s
       if constexpr (NV == 2) p2[u] = x2[c];
     }
 #pragma unroll
-    for (int u = 0; u < kGather; ++u) {
+    for (int u = 0; u < GATHER; ++u) {
       if (j + u < je) {
         sum1 = sum1 + v[u] * p1[u];
         if constexpr (NV == 2) sum2 = sum2 + v[u] * p2[u];
@@ -247,7 +247,7 @@ __device__ __forceinline__ void row_window(const double* s_val, const int32_t* s
 // LDS, the row pointers and the first staged window of the NEXT row block of
 // this workgroup are already in flight (registers), so the load latency of
 // block b+1 hides under the gathers of block b.
-template <typename RP, int EPI, bool VEC>
+template <typename RP, int EPI, bool VEC, int GATHER = kGather>
 __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
   using T = EpiTraits<EPI>;
   constexpr int NP = T::NP;
@@ -324,7 +324,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
     double sum1 = 0.0, sum2 = 0.0;
     const int64_t off0 = bs - ws0;  // window offset of this block's entry 0
     if (active)
-      row_window<NV>(s_val, s_col, x1, x2, (int)max((int64_t)rs + off0, (int64_t)0),
+      row_window<NV, GATHER>(s_val, s_col, x1, x2, (int)max((int64_t)rs + off0, (int64_t)0),
                      (int)min((int64_t)re + off0, (int64_t)kWindow), sum1, sum2);
     // rare: row blocks whose entries span more than one window
     for (int64_t ws = ws0 + kWindow; ws < be; ws += kWindow) {
@@ -335,7 +335,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
       __syncthreads();
       const int64_t off = bs - ws;
       if (active)
-        row_window<NV>(s_val, s_col, x1, x2, (int)max((int64_t)rs + off, (int64_t)0),
+        row_window<NV, GATHER>(s_val, s_col, x1, x2, (int)max((int64_t)rs + off, (int64_t)0),
                        (int)min((int64_t)re + off, (int64_t)kWindow), sum1, sum2);
     }
     if (active) {
@@ -367,8 +367,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
 }
 
 // Variant 1: no cross-row-block prefetch (lower VGPR count, higher occupancy).
-// DBG (timing diagnostics only, results are wrong): 1 = no x gather.
-template <typename RP, int EPI, bool VEC, int DBG = 0>
+template <typename RP, int EPI, bool VEC>
 __global__ __launch_bounds__(kBlock) void spmv_kernel_simple(SpmvArgs a) {
   using T = EpiTraits<EPI>;
   constexpr int NP = T::NP;
@@ -564,16 +563,12 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_wave(SpmvArgs a) {
   block_reduce_store<NP>(acc, a.partials, a.grid, s_red);
 }
 
-template <typename RP, int E, bool VEC>
-void spmv_dbg(int dbg, dim3 grid, dim3 block, hipStream_t s, const SpmvArgs& a) {
-  if (dbg == 1) spmv_kernel_simple<RP, E, VEC, 1><<<grid, block, 0, s>>>(a);
-
-}
-
 template <typename RP, bool VEC>
 void spmv_dispatch(SpmvEpi epi, const SpmvArgs& a, hipStream_t s) {
   const dim3 grid(a.grid), block(kBlock);
-  const char* env = getenv("KR_SPMV_VARIANT");  // A/B knob: 0 pipelined (default), 1 simple
+  // A/B knob (tools/spmv_micro.py): 0 pipelined (default), 1 no prefetch,
+  // 2 wave-independent, 3 pipelined with 4-deep gathers
+  const char* env = getenv("KR_SPMV_VARIANT");
   const int variant = env ? atoi(env) : 0;
   switch (epi) {
 #define KR_CASE(E)                                      \
@@ -582,8 +577,8 @@ void spmv_dispatch(SpmvEpi epi, const SpmvArgs& a, hipStream_t s) {
       spmv_kernel_simple<RP, E, VEC><<<grid, block, 0, s>>>(a); \
     else if (variant == 2)                              \
       spmv_kernel_wave<RP, E, VEC><<<grid, block, 0, s>>>(a); \
-    else if (variant >= 11 && variant <= 23)            \
-      spmv_dbg<RP, E, VEC>(variant - 10, grid, block, s, a); \
+    else if (variant == 3)                              \
+      spmv_kernel<RP, E, VEC, 4><<<grid, block, 0, s>>>(a); \
     else                                                \
       spmv_kernel<RP, E, VEC><<<grid, block, 0, s>>>(a); \
     break;
