@@ -178,7 +178,7 @@ struct Stage {
   int4v c[kCSlots];
 };
 
-template <bool VEC>
+template <bool VEC, bool NT = false>
 __device__ __forceinline__ void stage_load(Stage& st, const double* __restrict__ val,
                                            const int32_t* __restrict__ col, int64_t ws,
                                            int64_t bs, int64_t be, int tid) {
@@ -186,7 +186,10 @@ __device__ __forceinline__ void stage_load(Stage& st, const double* __restrict__
   for (int q = 0; q < kVSlots; ++q) {
     const int64_t g0 = ws + (int64_t)(tid + q * kBlock) * 2;
     if (VEC && g0 >= bs && g0 + 2 <= be) {
-      st.v[q] = *reinterpret_cast<const dbl2v*>(val + g0);
+      if constexpr (NT)
+        st.v[q] = __builtin_nontemporal_load(reinterpret_cast<const dbl2v*>(val + g0));
+      else
+        st.v[q] = *reinterpret_cast<const dbl2v*>(val + g0);
     } else {
       const bool ok0 = g0 >= bs && g0 < be, ok1 = g0 + 1 >= bs && g0 + 1 < be;
       st.v[q] = dbl2v{ok0 ? val[g0] : 0.0, ok1 ? val[g0 + 1] : 0.0};
@@ -196,7 +199,10 @@ __device__ __forceinline__ void stage_load(Stage& st, const double* __restrict__
   for (int q = 0; q < kCSlots; ++q) {
     const int64_t g0 = ws + (int64_t)(tid + q * kBlock) * 4;
     if (VEC && g0 >= bs && g0 + 4 <= be) {
-      st.c[q] = *reinterpret_cast<const int4v*>(col + g0);
+      if constexpr (NT)
+        st.c[q] = __builtin_nontemporal_load(reinterpret_cast<const int4v*>(col + g0));
+      else
+        st.c[q] = *reinterpret_cast<const int4v*>(col + g0);
     } else {
       int tc[4];
 #pragma unroll
@@ -247,7 +253,7 @@ __device__ __forceinline__ void row_window(const double* s_val, const int32_t* s
 // LDS, the row pointers and the first staged window of the NEXT row block of
 // this workgroup are already in flight (registers), so the load latency of
 // block b+1 hides under the gathers of block b.
-template <typename RP, int EPI, bool VEC, int GATHER = kGather>
+template <typename RP, int EPI, bool VEC, int GATHER = kGather, bool XCD = true, bool NT = false>
 __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
   using T = EpiTraits<EPI>;
   constexpr int NP = T::NP;
@@ -269,8 +275,23 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
   for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;
 
   const int64_t nrb = (a.n + kBlock - 1) / kBlock;
-  int64_t rb = blockIdx.x;
-  if (rb >= nrb) {
+  // Row-block schedule. XCD-aware: workgroups b and b+8 share an XCD (and its
+  // L2) under the observed round-robin dispatch, so the workgroups with equal
+  // b % 8 sweep one contiguous eighth of the rows together and the x rows
+  // that neighbouring row blocks gather (+-1, +-n) stay in one L2. Placement
+  // only changes speed: every row block is still visited exactly once.
+  int64_t rb, step, limit;
+  if (XCD && (gridDim.x & 7) == 0) {
+    const int64_t chunk = (nrb + 7) / 8;
+    rb = (int64_t)(blockIdx.x & 7) * chunk + (blockIdx.x >> 3);
+    step = gridDim.x >> 3;
+    limit = min(nrb, (int64_t)((blockIdx.x & 7) + 1) * chunk);
+  } else {
+    rb = blockIdx.x;
+    step = gridDim.x;
+    limit = nrb;
+  }
+  if (rb >= limit) {
     block_reduce_store<NP>(acc, a.partials, a.grid, s_red);
     return;
   }
@@ -284,12 +305,12 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
   int64_t bs = (int64_t)rowptr[r0];
   int64_t be = (int64_t)rowptr[r0 + nr];
   int64_t my_end = tid < nr ? (int64_t)rowptr[r0 + tid + 1] : 0;
-  stage_load<VEC>(st, val, col, VEC ? (bs & ~(int64_t)3) : bs, bs, be, tid);
+  stage_load<VEC, NT>(st, val, col, VEC ? (bs & ~(int64_t)3) : bs, bs, be, tid);
   int64_t bsn = 0, ben = 0;
-  if (rb + gridDim.x < nrb) {
-    const int64_t r0n = (rb + gridDim.x) * kBlock;
+  if (rb + step < limit) {
+    const int64_t r0n = (rb + step) * kBlock;
     bsn = (int64_t)rowptr[r0n];
-    ben = (int64_t)rowptr[r0n + block_rows(rb + gridDim.x)];
+    ben = (int64_t)rowptr[r0n + block_rows(rb + step)];
   }
 
   for (;;) {
@@ -304,17 +325,17 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
 
     // issue the next row block's loads before computing this one; its nnz
     // range (bsn, ben) was requested one iteration ago, the one after it now
-    const int64_t rb_next = rb + gridDim.x;
-    const bool has_next = rb_next < nrb;
+    const int64_t rb_next = rb + step;
+    const bool has_next = rb_next < limit;
     int64_t r0n = 0, my_end_n = 0, bsnn = 0, benn = 0;
     int nrn = 0;
     if (has_next) {
       r0n = rb_next * kBlock;
       nrn = block_rows(rb_next);
       my_end_n = tid < nrn ? (int64_t)rowptr[r0n + tid + 1] : 0;
-      stage_load<VEC>(st, val, col, VEC ? (bsn & ~(int64_t)3) : bsn, bsn, ben, tid);
-      const int64_t rb_nn = rb_next + gridDim.x;
-      if (rb_nn < nrb) {
+      stage_load<VEC, NT>(st, val, col, VEC ? (bsn & ~(int64_t)3) : bsn, bsn, ben, tid);
+      const int64_t rb_nn = rb_next + step;
+      if (rb_nn < limit) {
         const int64_t r0nn = rb_nn * kBlock;
         bsnn = (int64_t)rowptr[r0nn];
         benn = (int64_t)rowptr[r0nn + block_rows(rb_nn)];
@@ -579,6 +600,10 @@ void spmv_dispatch(SpmvEpi epi, const SpmvArgs& a, hipStream_t s) {
       spmv_kernel_wave<RP, E, VEC><<<grid, block, 0, s>>>(a); \
     else if (variant == 3)                              \
       spmv_kernel<RP, E, VEC, 4><<<grid, block, 0, s>>>(a); \
+    else if (variant == 6)                              \
+      spmv_kernel<RP, E, VEC, kGather, false><<<grid, block, 0, s>>>(a); \
+    else if (variant == 7)                              \
+      spmv_kernel<RP, E, VEC, kGather, true, true><<<grid, block, 0, s>>>(a); \
     else                                                \
       spmv_kernel<RP, E, VEC><<<grid, block, 0, s>>>(a); \
     break;

@@ -1,0 +1,77 @@
+"""Summarise a tools/profile.sh directory: per kernel, average duration
+(rocprofv3 kernel trace) and per-launch HBM-side traffic from the TCC EA
+request counters. Writes <dir>/summary.json and prints a table.
+
+Read bytes = 128*RDREQ_128B + 64*RDREQ_64B + 32*RDREQ_32B, write bytes =
+64*WRREQ_64B + 32*(WRREQ - WRREQ_64B) (request-size counters, so no width
+calibration is needed; FETCH_SIZE is kept for reference: on gfx950 it counts
+128-B requests as 64 B). The sizes are checked against the elementwise kernels
+whose byte counts are exact (see 'calibration')."""
+import collections
+import csv
+import glob
+import json
+import os
+import re
+import sys
+
+EPI = ["spmv", "spmv_bminus", "spmv_xy", "spmv_head_mrr", "spmv_head_kcg", "spmv_mrr_loop",
+       "spmv2", "spmv2_gram_mrr", "spmv2_gram_kcg"]
+EW = ["dot", "update_mrr_first", "update_mrr", "update_cg", "update_cg_p", "update_kcg",
+      "mrr_s", "copy"]
+
+
+def short(name):
+    m = re.search(r"spmv_kernel\w*<(\w+), (\d+), (\w+)", name)
+    if m:
+        return EPI[int(m.group(2))] + ("" if m.group(1) == "int" else "_rp64")
+    m = re.search(r"ew_kernel<(\d+), (\w+)>", name)
+    if m:
+        return EW[int(m.group(1))] + ("" if m.group(2) == "true" else "_scalar")
+    return re.sub(r"\(.*", "", name.replace("void ", ""))[:48]
+
+
+def main(d):
+    durs = collections.defaultdict(list)
+    for row in csv.DictReader(open(os.path.join(d, "trace", "run_kernel_trace.csv"))):
+        durs[short(row["Kernel_Name"])].append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+    cnt = collections.defaultdict(lambda: collections.defaultdict(list))
+    for path in glob.glob(os.path.join(d, "pmc*", "run_counter_collection.csv")):
+        for row in csv.DictReader(open(path)):
+            cnt[short(row["Kernel_Name"])][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    out = {}
+    for k in sorted(set(durs) | set(cnt)):
+        c = {n: sum(v) / len(v) for n, v in cnt[k].items()}
+        rec = {"launches": len(durs.get(k, [])),
+               "avg_ms": (sum(durs[k]) / len(durs[k]) / 1e6) if durs.get(k) else None}
+        if "TCC_EA0_RDREQ_128B_sum" in c and "TCC_EA0_RDREQ_64B_sum" in c:
+            rd = 128 * c["TCC_EA0_RDREQ_128B_sum"] + 64 * c["TCC_EA0_RDREQ_64B_sum"] + \
+                32 * c.get("TCC_EA0_RDREQ_32B_sum", 0.0)
+            rec["read_bytes"] = rd
+        if "TCC_EA0_WRREQ_sum" in c:
+            w64 = c.get("TCC_EA0_WRREQ_64B_sum", 0.0)
+            rec["write_bytes"] = 64 * w64 + 32 * (c["TCC_EA0_WRREQ_sum"] - w64)
+        if "read_bytes" in rec and "write_bytes" in rec:
+            rec["traffic_bytes"] = rec["read_bytes"] + rec["write_bytes"]
+        if "FETCH_SIZE" in c:
+            rec["fetch_size_kb"] = c["FETCH_SIZE"]
+        if "WRITE_SIZE" in c:
+            rec["write_size_kb"] = c["WRITE_SIZE"]
+        if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
+            rec["l2_hit"] = c["TCC_HIT_sum"] / max(1.0, c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
+        rec["counters"] = c
+        out[k] = rec
+    json.dump(out, open(os.path.join(d, "summary.json"), "w"), indent=1)
+    print(f"{'kernel':28s} {'n':>4s} {'avg_ms':>8s} {'read GB':>8s} {'write GB':>8s} {'GB/s':>8s} {'L2hit':>6s}")
+    for k, r in out.items():
+        if r["avg_ms"] is None:
+            continue
+        rd = r.get("read_bytes", float("nan")) / 1e9
+        wr = r.get("write_bytes", float("nan")) / 1e9
+        bw = (r.get("traffic_bytes", float("nan")) / (r["avg_ms"] * 1e6))
+        print(f"{k:28s} {r['launches']:4d} {r['avg_ms']:8.3f} {rd:8.3f} {wr:8.3f} {bw:8.1f} "
+              f"{r.get('l2_hit', float('nan')):6.3f}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

@@ -1,16 +1,20 @@
 #!/bin/bash
-# rocprofv3 passes over a short bench run: kernel trace + stats, then PMC
-# passes (one counter group per pass; never combined with tracing domains).
+# rocprofv3 passes over one short bench run (GPU box):
+#   1. --kernel-trace --stats            (durations; never combined with PMC)
+#   2.. one PMC group per pass            (TCC slots are scarce; separate runs)
+# then tools/pmc_summary.py writes gpurun_out/<tag>/summary.json.
 # Usage: bash tools/profile.sh <tag> [bench args...]
 tag=${1:-prof}; shift
 args=${@:---steps 5 --warmup 1 --no-cpu-baseline}
 out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
-cd $GRAFT_REPO_ROOT 2>/dev/null || true
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $out/trace -o run --output-format csv -- python3 bench.py $args > $out/trace.log 2>&1 || exit $?
-for pmc in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
-  name=$(echo $pmc | tr ' ' '_')
-  timeout -k 10 600 rocprofv3 --pmc $pmc -d $out/pmc_$name -o run --output-format csv -- python3 bench.py $args --no-profile > $out/pmc_$name.log 2>&1 || exit $?
+i=0
+for pmc in "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_128B_sum" "TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_32B_sum" \
+           "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum" "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+  i=$((i+1))
+  timeout -k 10 600 rocprofv3 --pmc $pmc -d $out/pmc$i -o run --output-format csv -- python3 bench.py $args --no-profile > $out/pmc$i.log 2>&1 || exit $?
 done
-echo done
+python3 tools/pmc_summary.py $out > $out/summary.txt 2>&1 || exit $?
+cat $out/summary.txt

@@ -56,13 +56,17 @@ def main():
     dual = lambda: lib.kr_spmv2_csr_f64(c["rowptr"], c["rowptr64"], c["col"], c["val"], n,
                                         x.data_ptr(), x2.data_ptr(), y.data_ptr(),
                                         y2.data_ptr(), None)
+    dual_alias = lambda: lib.kr_spmv2_csr_f64(c["rowptr"], c["rowptr64"], c["col"], c["val"],
+                                              n, x.data_ptr(), x.data_ptr(), y.data_ptr(),
+                                              y2.data_ptr(), None)
     print(f"N={n} nnz={nnz} single={b1/1e9:.2f} GB dual={b2/1e9:.2f} GB per launch")
     for v in args.variants:
         os.environ["KR_SPMV_VARIANT"] = str(v)
         t1 = timeit(single, args.reps)
         t2 = timeit(dual, args.reps)
+        t3 = timeit(dual_alias, args.reps)
         print(f"variant {v:3d}: single {t1:7.3f} ms {b1/t1/1e6:7.1f} GB/s | "
-              f"dual {t2:7.3f} ms {b2/t2/1e6:7.1f} GB/s", flush=True)
+              f"dual {t2:7.3f} ms {b2/t2/1e6:7.1f} GB/s | dual x2=x1 {t3:7.3f} ms", flush=True)
     os.environ["KR_SPMV_VARIANT"] = "0"
     out = torch.empty(1, dtype=torch.float64, device=dev)
     big = torch.empty(12 * nnz // 8, dtype=torch.float64, device=dev).fill_(1.0)
