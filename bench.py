@@ -26,15 +26,31 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
+# BASELINE.json configs. C4 is the headline (metric) and the default; the others
+# are available as --config for parity/perf runs.
+CONFIGS = {
+    "C1": dict(method="cg", matrix=("poisson", 256, 2), k=0,
+               label="CG on 2D 5-point Poisson 256^2"),
+    "C2": dict(method="cg", matrix=("poisson", 256, 3), k=0,
+               label="CG on 3D 7-point Poisson 256^3"),
+    "C3": dict(method="mrr", matrix=("banded", 10_000_000, 13, 64, 0), k=0,
+               label="MrR on random banded CSR N=10M, 27 nnz/row"),
+    "C4": dict(method="kskipmrr", matrix=("poisson", 512, 3), k=4,
+               label="k-skip MrR k=4 on 3D 7-point Poisson 512^3"),
+    "C5": dict(method="adaptivekskipmrr", matrix=("banded", 50_000_000, 31, 256, 0), k=4,
+               label="Adaptive k-skip MrR on banded CSR N=50M, 63 nnz/row"),
+}
+
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--n-side", type=int, default=512)
-    p.add_argument("--k", type=int, default=4)
-    p.add_argument("--method", default="kskipmrr")
+    p.add_argument("--config", default="C4", choices=sorted(CONFIGS))
+    p.add_argument("--n-side", type=int, default=None, help="override the Poisson grid side")
+    p.add_argument("--k", type=int, default=None)
+    p.add_argument("--method", default=None)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-n-side", type=int, default=512,
                    help="grid side of the CPU-baseline sample (512 = the benchmark system)")
@@ -89,23 +105,32 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     from parallel_krylov_amd.system import Communicator, KrylovSystem, balanced_partition
 
+    cfg = dict(CONFIGS[args.config])
+    method = args.method or cfg["method"]
+    mat = list(cfg["matrix"])
+    if args.n_side is not None and mat[0] == "poisson":
+        mat[1] = args.n_side
+    args.method = method
     comm = None
     if world > 1:
         dist.init_process_group("gloo")
         comm = Communicator.from_torch(None, local)
-    n = args.n_side ** 3
+    n = mat[1] ** mat[2] if mat[0] == "poisson" else mat[1]
     part = balanced_partition(n, world)
     sysm = KrylovSystem(n, [part[rank], part[rank + 1]], [local], comm)
-    sysm.gen_poisson(args.n_side, 3)
+    if mat[0] == "poisson":
+        sysm.gen_poisson(mat[1], mat[2])
+    else:
+        sysm.gen_banded(mat[2], mat[3], mat[4])
     sysm.finalize()
     info = sysm.shard_info(0)
     b = sysm.rhs(1)
-    k = args.k if "kskip" in args.method else 0
-    per_step = (k + 1) if "kskip" in args.method else 1
+    k = (args.k if args.k is not None else cfg["k"]) if "kskip" in method else 0
+    per_step = (k + 1) if "kskip" in method else 1
     maxiter = (args.warmup + args.steps + 4) * per_step + 2
     sysm.begin(args.method, b, None, tol=0.0, maxiter=maxiter, k=k,
                profile=not args.no_profile)
@@ -151,11 +176,12 @@ def main():
                                               if s["name"] == dom),
                         avg_ms=d["avg_ms"])
     base = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        base = cpu_baseline(args.cpu_n_side, args.k, args.method)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "C4":
+        base = cpu_baseline(args.cpu_n_side, k, method)
     if rank == 0:
         rec = {
-            "metric": "solver iterations/sec, k-skip MrR k=4 on 512^3 Poisson CSR",
+            "metric": ("solver iterations/sec, k-skip MrR k=4 on 512^3 Poisson CSR"
+                       if args.config == "C4" else f"solver iterations/sec, {cfg['label']}"),
             "value": round(value, 3),
             "unit": "iterations/s",
             "n_gpus": world,
@@ -166,10 +192,10 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (7-point Poisson CSR and b = 2u-1 generated on device)",
-            "config": {"workload": f"{args.method} k={k} on {args.n_side}^3 7-point Poisson CSR "
-                                   f"(N={n}, nnz/shard={info['nnz']}), tol=0 fixed iterations",
-                       "method": args.method, "k": k, "n_side": args.n_side,
+            "data": "synthetic (CSR matrix and b = 2u-1 generated on device)",
+            "config": {"workload": f"{args.config}: {cfg['label']} (N={n}, "
+                                   f"nnz/shard={info['nnz']}), tol=0 fixed iterations",
+                       "method": method, "k": k, "matrix": mat,
                        "step": f"one outer iteration = {per_step} solver iterations",
                        "parallelism": f"row-partitioned x{world}, RCCL halo + Gram all-gather"},
             "roofline": roofline,
@@ -179,6 +205,8 @@ def main():
         }
         print(json.dumps(rec))
     sysm.close()
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -361,6 +361,7 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
     a.e = e >= 0 ? s.own(e) : nullptr;
     a.partials = s.partials + (size_t)slot0 * s.grid;
     a.grid = s.grid;
+    a.long_rows = s.n > 0 && (double)s.nnz >= kLongRow * (double)s.n;
     hipEvent_t t0 = nullptr;
     const char* nm = epi_name(epi);
     prof_begin(s, nm, t0);

@@ -73,7 +73,10 @@ struct SpmvArgs {
   const double* e = nullptr;   // own rows (extra operand)
   double* partials = nullptr;  // products: partials[p * grid + block]
   int grid = 0;
+  int long_rows = 0;           // 1: product-then-sum kernel (mean nnz/row >= kLongRow)
 };
+// Mean row length from which the product-then-sum SpMV is used.
+constexpr double kLongRow = 12.0;
 void launch_spmv(SpmvEpi epi, const SpmvArgs& a, hipStream_t s);
 
 // ---------------------------------------------------------------------------

@@ -249,10 +249,14 @@ __device__ __forceinline__ void row_window(const double* s_val, const int32_t* s
   }
 }
 
-// Software pipeline over row blocks: while a row block is multiplied out of
-// LDS, the row pointers and the first staged window of the NEXT row block of
-// this workgroup are already in flight (registers), so the load latency of
-// block b+1 hides under the gathers of block b.
+// Software pipeline over a stream of LDS windows. A workgroup walks its row
+// blocks (256 rows each); a row block's entries are one or more 2048-entry
+// windows. While one window is multiplied out of LDS, the NEXT window is
+// already in flight in registers: the next window of the same row block, or
+// the first window of the next row block (whose nnz range was requested as
+// scalar loads one row block earlier). So a window waits on one memory round
+// trip, for short-row (Poisson: one window per row block) and long-row
+// (banded 27-63 nnz/row: 4-8 windows per row block) matrices alike.
 template <typename RP, int EPI, bool VEC, int GATHER = kGather, bool XCD = true, bool NT = false>
 __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
   using T = EpiTraits<EPI>;
@@ -295,69 +299,74 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
     block_reduce_store<NP>(acc, a.partials, a.grid, s_red);
     return;
   }
-  // prologue: row block rb in flight, and the nnz range of the next one
-  // (scalar loads) requested, so that no iteration waits on a row-pointer
-  // load before it can issue the next block's staging.
   auto block_rows = [&](int64_t b) { return (int)min((int64_t)kBlock, a.n - b * kBlock); };
-  Stage st;
+  auto wstart = [](int64_t e) { return VEC ? (e & ~(int64_t)3) : e; };
+
+  // current row block
   int64_t r0 = rb * kBlock;
   int nr = block_rows(rb);
   int64_t bs = (int64_t)rowptr[r0];
   int64_t be = (int64_t)rowptr[r0 + nr];
   int64_t my_end = tid < nr ? (int64_t)rowptr[r0 + tid + 1] : 0;
-  stage_load<VEC, NT>(st, val, col, VEC ? (bs & ~(int64_t)3) : bs, bs, be, tid);
+  // next row block: nnz range as scalars (issued now, used one block later)
   int64_t bsn = 0, ben = 0;
   if (rb + step < limit) {
     const int64_t r0n = (rb + step) * kBlock;
     bsn = (int64_t)rowptr[r0n];
     ben = (int64_t)rowptr[r0n + block_rows(rb + step)];
   }
+  Stage st;  // the window in flight
+  int64_t ws = wstart(bs);
+  stage_load<VEC, NT>(st, val, col, ws, bs, be, tid);
+  bool first_window = true;
+  int rs = 0, re = 0;
+  double sum1 = 0.0, sum2 = 0.0;
+  // the next row block's state, loaded when its first window is issued
+  int64_t r0n = 0, my_end_n = 0, bsnn = 0, bennn = 0;
+  int nrn = 0;
+  (void)bennn;
 
   for (;;) {
-    const int64_t ws0 = VEC ? (bs & ~(int64_t)3) : bs;
-    if (tid < nr) s_rp[tid + 1] = (int32_t)(my_end - bs);
-    if (tid == 0) s_rp[0] = 0;
+    if (first_window) {
+      if (tid < nr) s_rp[tid + 1] = (int32_t)(my_end - bs);
+      if (tid == 0) s_rp[0] = 0;
+    }
     stage_commit(st, s_val, s_col, tid);
     __syncthreads();
     const bool active = tid < nr;
-    const int rs = active ? s_rp[tid] : 0;
-    const int re = active ? s_rp[tid + 1] : 0;
-
-    // issue the next row block's loads before computing this one; its nnz
-    // range (bsn, ben) was requested one iteration ago, the one after it now
+    if (first_window) {
+      rs = active ? s_rp[tid] : 0;
+      re = active ? s_rp[tid + 1] : 0;
+    }
+    // issue the next window before working on this one
+    const bool last_window = ws + kWindow >= be;
     const int64_t rb_next = rb + step;
     const bool has_next = rb_next < limit;
-    int64_t r0n = 0, my_end_n = 0, bsnn = 0, benn = 0;
-    int nrn = 0;
-    if (has_next) {
+    if (!last_window) {
+      stage_load<VEC, NT>(st, val, col, ws + kWindow, bs, be, tid);
+    } else if (has_next) {
       r0n = rb_next * kBlock;
       nrn = block_rows(rb_next);
       my_end_n = tid < nrn ? (int64_t)rowptr[r0n + tid + 1] : 0;
-      stage_load<VEC, NT>(st, val, col, VEC ? (bsn & ~(int64_t)3) : bsn, bsn, ben, tid);
+      stage_load<VEC, NT>(st, val, col, wstart(bsn), bsn, ben, tid);
       const int64_t rb_nn = rb_next + step;
       if (rb_nn < limit) {
         const int64_t r0nn = rb_nn * kBlock;
         bsnn = (int64_t)rowptr[r0nn];
-        benn = (int64_t)rowptr[r0nn + block_rows(rb_nn)];
+        bennn = (int64_t)rowptr[r0nn + block_rows(rb_nn)];
       }
     }
-
-    double sum1 = 0.0, sum2 = 0.0;
-    const int64_t off0 = bs - ws0;  // window offset of this block's entry 0
-    if (active)
-      row_window<NV, GATHER>(s_val, s_col, x1, x2, (int)max((int64_t)rs + off0, (int64_t)0),
-                     (int)min((int64_t)re + off0, (int64_t)kWindow), sum1, sum2);
-    // rare: row blocks whose entries span more than one window
-    for (int64_t ws = ws0 + kWindow; ws < be; ws += kWindow) {
-      __syncthreads();
-      Stage extra;
-      stage_load<VEC>(extra, val, col, ws, bs, be, tid);
-      stage_commit(extra, s_val, s_col, tid);
-      __syncthreads();
+    // this lane's entries inside the window (window offsets)
+    if (active) {
       const int64_t off = bs - ws;
-      if (active)
-        row_window<NV, GATHER>(s_val, s_col, x1, x2, (int)max((int64_t)rs + off, (int64_t)0),
-                       (int)min((int64_t)re + off, (int64_t)kWindow), sum1, sum2);
+      row_window<NV, GATHER>(s_val, s_col, x1, x2, (int)max((int64_t)rs + off, (int64_t)0),
+                             (int)min((int64_t)re + off, (int64_t)kWindow), sum1, sum2);
+    }
+    if (!last_window) {
+      __syncthreads();  // LDS is rewritten by the next window
+      ws += kWindow;
+      first_window = false;
+      continue;
     }
     if (active) {
       const int64_t row = r0 + tid;
@@ -380,8 +389,207 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
     bs = bsn;
     be = ben;
     bsn = bsnn;
-    ben = benn;
+    ben = bennn;
     my_end = my_end_n;
+    ws = wstart(bs);
+    first_window = true;
+    sum1 = 0.0;
+    sum2 = 0.0;
+  }
+  __syncthreads();
+  block_reduce_store<NP>(acc, a.partials, a.grid, s_red);
+}
+
+// Product-then-sum SpMV for long rows (variant 8; chosen by the host when
+// nnz/row is large). Each window's entries are multiplied entry-parallel:
+// lane t owns entries 2(t + 256q) + {0,1} (a 16-byte value load and an 8-byte
+// column load per slot), gathers x for all of them at once, and writes the
+// products fl(v * x) to LDS. Then each lane adds its own row's products in
+// stored order, carrying the running sum across windows -- the same
+// operations in the same order as scipy, so the result is still bitwise.
+// Every lane gathers in every window, however few rows the window holds.
+constexpr int kPSlots = kWindow / (2 * kBlock);
+typedef int int2v __attribute__((ext_vector_type(2)));
+
+struct PStage {
+  dbl2v v[kPSlots];
+  int2v c[kPSlots];
+};
+
+template <bool VEC>
+__device__ __forceinline__ void pstage_load(PStage& st, const double* __restrict__ val,
+                                            const int32_t* __restrict__ col, int64_t ws,
+                                            int64_t bs, int64_t be, int tid) {
+#pragma unroll
+  for (int q = 0; q < kPSlots; ++q) {
+    const int64_t g0 = ws + (int64_t)(tid + q * kBlock) * 2;
+    if (VEC && g0 >= bs && g0 + 2 <= be) {
+      st.v[q] = *reinterpret_cast<const dbl2v*>(val + g0);
+      st.c[q] = *reinterpret_cast<const int2v*>(col + g0);
+    } else {
+      const bool ok0 = g0 >= bs && g0 < be, ok1 = g0 + 1 >= bs && g0 + 1 < be;
+      st.v[q] = dbl2v{ok0 ? val[g0] : 0.0, ok1 ? val[g0 + 1] : 0.0};
+      st.c[q] = int2v{ok0 ? col[g0] : -1, ok1 ? col[g0 + 1] : -1};
+    }
+  }
+}
+
+template <int NV>
+__device__ __forceinline__ void pstage_products(const PStage& st, const double* __restrict__ x1,
+                                                const double* __restrict__ x2, double* s_p1,
+                                                double* s_p2, int tid) {
+  double g1[2 * kPSlots], g2[2 * kPSlots];
+#pragma unroll
+  for (int q = 0; q < kPSlots; ++q) {
+    const int c0 = st.c[q].x, c1 = st.c[q].y;
+    g1[2 * q] = c0 >= 0 ? x1[c0] : 0.0;
+    g1[2 * q + 1] = c1 >= 0 ? x1[c1] : 0.0;
+    if constexpr (NV == 2) {
+      g2[2 * q] = c0 >= 0 ? x2[c0] : 0.0;
+      g2[2 * q + 1] = c1 >= 0 ? x2[c1] : 0.0;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < kPSlots; ++q) {
+    reinterpret_cast<dbl2v*>(s_p1)[tid + q * kBlock] =
+        dbl2v{st.v[q].x * g1[2 * q], st.v[q].y * g1[2 * q + 1]};
+    if constexpr (NV == 2)
+      reinterpret_cast<dbl2v*>(s_p2)[tid + q * kBlock] =
+          dbl2v{st.v[q].x * g2[2 * q], st.v[q].y * g2[2 * q + 1]};
+  }
+}
+
+template <typename RP, int EPI, bool VEC>
+__global__ __launch_bounds__(kBlock) void spmv_kernel_prod(SpmvArgs a) {
+  using T = EpiTraits<EPI>;
+  constexpr int NP = T::NP;
+  constexpr int NV = T::NV;
+  __shared__ __attribute__((aligned(16))) double s_p1[kWindow];
+  __shared__ __attribute__((aligned(16))) double s_p2[NV == 2 ? kWindow : 2];
+  __shared__ int32_t s_rp[kBlock + 1];
+  __shared__ double s_red[(NP > 0 ? NP : 1) * 4];
+
+  const RP* __restrict__ rowptr = static_cast<const RP*>(a.rowptr);
+  const double* __restrict__ val = a.val;
+  const int32_t* __restrict__ col = a.col;
+  const double* __restrict__ x1 = a.x1;
+  const double* __restrict__ x2 = a.x2;
+  const int tid = threadIdx.x;
+
+  double acc[NP > 0 ? NP : 1];
+#pragma unroll
+  for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;
+
+  const int64_t nrb = (a.n + kBlock - 1) / kBlock;
+  int64_t rb, step, limit;
+  if ((gridDim.x & 7) == 0) {  // XCD-contiguous sweep, as spmv_kernel
+    const int64_t chunk = (nrb + 7) / 8;
+    rb = (int64_t)(blockIdx.x & 7) * chunk + (blockIdx.x >> 3);
+    step = gridDim.x >> 3;
+    limit = min(nrb, (int64_t)((blockIdx.x & 7) + 1) * chunk);
+  } else {
+    rb = blockIdx.x;
+    step = gridDim.x;
+    limit = nrb;
+  }
+  if (rb >= limit) {
+    block_reduce_store<NP>(acc, a.partials, a.grid, s_red);
+    return;
+  }
+  auto block_rows = [&](int64_t b) { return (int)min((int64_t)kBlock, a.n - b * kBlock); };
+  auto wstart = [](int64_t e) { return VEC ? (e & ~(int64_t)1) : e; };
+
+  int64_t r0 = rb * kBlock;
+  int nr = block_rows(rb);
+  int64_t bs = (int64_t)rowptr[r0];
+  int64_t be = (int64_t)rowptr[r0 + nr];
+  int64_t my_end = tid < nr ? (int64_t)rowptr[r0 + tid + 1] : 0;
+  int64_t bsn = 0, ben = 0;
+  if (rb + step < limit) {
+    const int64_t r0n = (rb + step) * kBlock;
+    bsn = (int64_t)rowptr[r0n];
+    ben = (int64_t)rowptr[r0n + block_rows(rb + step)];
+  }
+  PStage st;
+  int64_t ws = wstart(bs);
+  pstage_load<VEC>(st, val, col, ws, bs, be, tid);
+  bool first_window = true;
+  int rs = 0, re = 0;
+  double sum1 = 0.0, sum2 = 0.0;
+  int64_t r0n = 0, my_end_n = 0, bsnn = 0, bennn = 0;
+  int nrn = 0;
+
+  for (;;) {
+    if (first_window) {
+      if (tid < nr) s_rp[tid + 1] = (int32_t)(my_end - bs);
+      if (tid == 0) s_rp[0] = 0;
+    }
+    pstage_products<NV>(st, x1, x2, s_p1, s_p2, tid);
+    __syncthreads();
+    const bool active = tid < nr;
+    if (first_window) {
+      rs = active ? s_rp[tid] : 0;
+      re = active ? s_rp[tid + 1] : 0;
+    }
+    const bool last_window = ws + kWindow >= be;
+    const int64_t rb_next = rb + step;
+    const bool has_next = rb_next < limit;
+    if (!last_window) {
+      pstage_load<VEC>(st, val, col, ws + kWindow, bs, be, tid);
+    } else if (has_next) {
+      r0n = rb_next * kBlock;
+      nrn = block_rows(rb_next);
+      my_end_n = tid < nrn ? (int64_t)rowptr[r0n + tid + 1] : 0;
+      pstage_load<VEC>(st, val, col, wstart(bsn), bsn, ben, tid);
+      const int64_t rb_nn = rb_next + step;
+      if (rb_nn < limit) {
+        const int64_t r0nn = rb_nn * kBlock;
+        bsnn = (int64_t)rowptr[r0nn];
+        bennn = (int64_t)rowptr[r0nn + block_rows(rb_nn)];
+      }
+    }
+    if (active) {
+      const int64_t off = bs - ws;
+      const int js = (int)max((int64_t)rs + off, (int64_t)0);
+      const int je = (int)min((int64_t)re + off, (int64_t)kWindow);
+      for (int j = js; j < je; ++j) {
+        sum1 = sum1 + s_p1[j];
+        if constexpr (NV == 2) sum2 = sum2 + s_p2[j];
+      }
+    }
+    if (!last_window) {
+      __syncthreads();
+      ws += kWindow;
+      first_window = false;
+      continue;
+    }
+    if (active) {
+      const int64_t row = r0 + tid;
+      double y1 = sum1;
+      if constexpr (EPI == EPI_BMINUS) y1 = a.b[row] - sum1;
+      a.y1[row] = y1;
+      if constexpr (NV == 2) a.y2[row] = sum2;
+      if constexpr (NP > 0) {
+        const double xv = T::kX ? x1[a.xoff + row] : 0.0;
+        const double x2v = T::kX2 ? x2[a.xoff + row] : 0.0;
+        const double ev = T::kE ? a.e[row] : 0.0;
+        epi_products<EPI>(xv, x2v, y1, sum2, ev, acc);
+      }
+    }
+    if (!has_next) break;
+    __syncthreads();
+    rb = rb_next;
+    r0 = r0n;
+    nr = nrn;
+    bs = bsn;
+    be = ben;
+    bsn = bsnn;
+    ben = bennn;
+    my_end = my_end_n;
+    ws = wstart(bs);
+    first_window = true;
+    sum1 = 0.0;
+    sum2 = 0.0;
   }
   __syncthreads();
   block_reduce_store<NP>(acc, a.partials, a.grid, s_red);
@@ -587,10 +795,12 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_wave(SpmvArgs a) {
 template <typename RP, bool VEC>
 void spmv_dispatch(SpmvEpi epi, const SpmvArgs& a, hipStream_t s) {
   const dim3 grid(a.grid), block(kBlock);
-  // A/B knob (tools/spmv_micro.py): 0 pipelined (default), 1 no prefetch,
-  // 2 wave-independent, 3 pipelined with 4-deep gathers
+  // Row-walk (0) for short rows, product-then-sum (8) for long rows. The
+  // KR_SPMV_VARIANT environment variable overrides the choice for A/B runs
+  // (tools/spmv_micro.py): 1 no prefetch, 2 wave-independent, 3 4-deep gathers,
+  // 6 no XCD schedule, 7 non-temporal staging.
   const char* env = getenv("KR_SPMV_VARIANT");
-  const int variant = env ? atoi(env) : 0;
+  const int variant = env ? atoi(env) : (a.long_rows ? 8 : 0);
   switch (epi) {
 #define KR_CASE(E)                                      \
   case E:                                               \
@@ -600,6 +810,8 @@ void spmv_dispatch(SpmvEpi epi, const SpmvArgs& a, hipStream_t s) {
       spmv_kernel_wave<RP, E, VEC><<<grid, block, 0, s>>>(a); \
     else if (variant == 3)                              \
       spmv_kernel<RP, E, VEC, 4><<<grid, block, 0, s>>>(a); \
+    else if (variant == 8)                              \
+      spmv_kernel_prod<RP, E, VEC><<<grid, block, 0, s>>>(a); \
     else if (variant == 6)                              \
       spmv_kernel<RP, E, VEC, kGather, false><<<grid, block, 0, s>>>(a); \
     else if (variant == 7)                              \
@@ -994,6 +1206,7 @@ void launch_spmv(SpmvEpi epi, const SpmvArgs& a, hipStream_t s) {
   // 16-byte staging needs 16-byte aligned val/col bases
   const bool vec = ((reinterpret_cast<uintptr_t>(a.val) | reinterpret_cast<uintptr_t>(a.col)) &
                     15) == 0;
+  (void)vec;
   if (a.rowptr64) {
     if (vec)
       spmv_dispatch<int64_t, true>(epi, a, s);

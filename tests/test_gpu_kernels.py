@@ -69,9 +69,12 @@ MATRICES = {
 }
 
 
+@pytest.mark.parametrize("variant", ["0", "8"])
 @pytest.mark.parametrize("name", list(MATRICES))
 @pytest.mark.parametrize("rp64", [0, 1])
-def test_spmv_bitwise_vs_scipy(torch_dev, name, rp64):
+def test_spmv_bitwise_vs_scipy(torch_dev, monkeypatch, name, rp64, variant):
+    """Both SpMV kernels (row-walk 0, product-then-sum 8) are bitwise scipy."""
+    monkeypatch.setenv("KR_SPMV_VARIANT", variant)
     A = MATRICES[name]()
     n = A.shape[0]
     rng = np.random.default_rng(7)

@@ -19,15 +19,22 @@ def main():
     ap.add_argument("--n-side", type=int, default=512)
     ap.add_argument("--variants", type=int, nargs="+", default=[0, 1, 2])
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--banded", type=int, nargs=3, metavar=("N", "H", "W"), default=None,
+                    help="use the banded generator instead of Poisson")
     args = ap.parse_args()
     import torch
     from parallel_krylov_amd._lib import library
     from parallel_krylov_amd.system import KrylovSystem
 
     lib = library()
-    n = args.n_side ** 3
-    sysm = KrylovSystem(n, [0, n], [0])
-    sysm.gen_poisson(args.n_side, 3)
+    if args.banded:
+        n = args.banded[0]
+        sysm = KrylovSystem(n, [0, n], [0])
+        sysm.gen_banded(args.banded[1], args.banded[2], 0)
+    else:
+        n = args.n_side ** 3
+        sysm = KrylovSystem(n, [0, n], [0])
+        sysm.gen_poisson(args.n_side, 3)
     sysm.finalize()
     nnz = sysm.shard_info(0)["nnz"]
     c = sysm.csr_pointers(0)
