@@ -97,6 +97,20 @@ def cpu_baseline(n_side: int, k: int, method: str):
                         f"{cores} affinity cores; wall {wall:.1f} s"))
 
 
+def pmc_traffic(kernel):
+    """Beyond-L2 bytes per launch of `kernel` from the committed rocprofv3 PMC
+    summary (profiles/latest.json, made by tools/profile.sh +
+    tools/pmc_summary.py from TCC_EA0_RDREQ_{32B,64B,128B} / WRREQ request
+    counts on this same command). None if no profile of this kernel exists."""
+    path = os.path.join(REPO, "profiles", "latest.json")
+    try:
+        with open(path) as f:
+            rec = json.load(f).get(kernel)
+        return None if rec is None else rec.get("traffic_bytes")
+    except (OSError, ValueError):
+        return None
+
+
 def main():
     args = parse()
     import numpy as np
@@ -171,7 +185,7 @@ def main():
         d = kernels[dom]
         ach = d["gbs"]
         roofline = dict(bound="hbm", kernel=dom, achieved=ach, peak=HBM_PEAK_GBS, unit="GB/s",
-                        frac=round(ach / HBM_PEAK_GBS, 4), traffic=None,
+                        frac=round(ach / HBM_PEAK_GBS, 4), traffic=pmc_traffic(dom),
                         bytes_per_launch=next(s["bytes_per_launch"] for s in stats
                                               if s["name"] == dom),
                         avg_ms=d["avg_ms"])

@@ -46,6 +46,8 @@ int ew_vectors(EwOp op) {
     case EW_KCG: return 7;
     case EW_MRR_S: return 3;
     case EW_COPY: return 2;
+    case EW_MRR_NOX: return 7;
+    case EW_MRR_X2: return 9;
   }
   return 0;
 }
@@ -75,6 +77,8 @@ const char* ew_name(EwOp op) {
     case EW_KCG: return "update_kcg";
     case EW_MRR_S: return "mrr_s";
     case EW_COPY: return "copy";
+    case EW_MRR_NOX: return "update_mrr_nox";
+    case EW_MRR_X2: return "update_mrr_x2";
   }
   return "ew?";
 }
@@ -674,8 +678,16 @@ class KskipMrrSession : public Base {
     std::vector<double> zeta(k + 1), eta(k + 1);
     kskipmrr_recurrence(k, alpha.data(), beta.data(), delta.data(), zeta.data(), eta.data());
     for (int j = 0; j <= k; ++j) {
-      sys->ew(EW_MRR, eta[j], zeta[j], {AY(0), AR(1), Z, AR(0), xsrc, cur}, 0);
-      xsrc = cur;
+      // x -= z is deferred pairwise: step j stores z and leaves x, step j+1
+      // applies x = (x - z_j) - z_{j+1} in registers -- the same two roundings
+      // as the reference's two statements, one x read+write fewer.
+      if (j % 2 == 0 && j < k) {
+        sys->ew(EW_MRR_NOX, eta[j], zeta[j], {AY(0), AR(1), Z, AR(0), -1, -1}, 0);
+      } else {
+        sys->ew(j % 2 == 1 ? EW_MRR_X2 : EW_MRR, eta[j], zeta[j],
+                {AY(0), AR(1), Z, AR(0), xsrc, cur}, 0);
+        xsrc = cur;
+      }
       if (j < k)
         sys->spmv(EPI_NONE, AR(0), -1, AR(1), -1, -1, -1, 0);
       else

@@ -91,6 +91,8 @@ enum EwOp : int {
   EW_KCG,         // x += alpha*ap0; r -= alpha*ap1; ap0 = r + beta*ap0
   EW_MRR_S,       // s = ar - gamma*y; <r,s> <s,s>   (s not stored)
   EW_COPY,        // p0 <- p1
+  EW_MRR_NOX,     // EW_MRR without the x update (x deferred to the next step)
+  EW_MRR_X2,      // EW_MRR with xd = (xs - z_old) - z_new (two steps of x at once)
 };
 int ew_products(EwOp op);
 

@@ -872,6 +872,14 @@ template <>
 struct EwTraits<EW_COPY> {  // p: dst src
   static constexpr int NP = 0, R = 0b000010, W = 0b000001;
 };
+template <>
+struct EwTraits<EW_MRR_NOX> {  // p: y ar1 z r
+  static constexpr int NP = 0, R = 0b001111, W = 0b001101;
+};
+template <>
+struct EwTraits<EW_MRR_X2> {  // p: y ar1 z r xs xd
+  static constexpr int NP = 0, R = 0b011111, W = 0b101101;
+};
 
 template <int OP>
 __device__ __forceinline__ void ew_elem(double c0, double c1, double (&v)[6],
@@ -921,10 +929,24 @@ __device__ __forceinline__ void ew_elem(double c0, double c1, double (&v)[6],
     acc[1] += s * s;
   } else if constexpr (OP == EW_COPY) {
     v[0] = v[1];
+  } else if constexpr (OP == EW_MRR_NOX || OP == EW_MRR_X2) {  // c0 = eta, c1 = zeta
+    const double t1 = c0 * v[0];
+    const double t2 = c1 * v[1];
+    const double y = t1 + t2;
+    const double t3 = c0 * v[2];
+    const double t4 = c1 * v[3];
+    const double z = t3 - t4;
+    if constexpr (OP == EW_MRR_X2) {
+      const double xm = v[4] - v[2];  // the deferred x -= z of the previous step
+      v[5] = xm - z;
+    }
+    v[0] = y;
+    v[2] = z;
+    v[3] = v[3] - y;
   }
 }
 
-template <int OP, bool VEC>
+template <int OP, bool VEC, int U = 1, bool NTS = false>
 __global__ __launch_bounds__(kBlock) void ew_kernel(EwArgs a) {
   using T = EwTraits<OP>;
   constexpr int NP = T::NP;
@@ -935,24 +957,44 @@ __global__ __launch_bounds__(kBlock) void ew_kernel(EwArgs a) {
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   const int64_t t0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if constexpr (VEC) {
+    // U pairs per thread per iteration: all loads of the U pairs are issued
+    // before any store (the operands may alias, so the compiler cannot hoist
+    // the next iteration's loads above this iteration's stores by itself).
     const int64_t npairs = a.n >> 1;
-    for (int64_t q = t0; q < npairs; q += stride) {
-      double va[6], vb[6];
+    for (int64_t q0 = t0; q0 < npairs; q0 += U * stride) {
+      double va[U][6], vb[U][6];
 #pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        if (T::R & (1 << k)) {
-          const double2 d = reinterpret_cast<const double2*>(a.p[k])[q];
-          va[k] = d.x;
-          vb[k] = d.y;
-        } else {
-          va[k] = vb[k] = 0.0;
+      for (int u = 0; u < U; ++u) {
+        const int64_t q = q0 + u * stride;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          if ((T::R & (1 << k)) && q < npairs) {
+            const double2 d = reinterpret_cast<const double2*>(a.p[k])[q];
+            va[u][k] = d.x;
+            vb[u][k] = d.y;
+          } else {
+            va[u][k] = vb[u][k] = 0.0;
+          }
         }
       }
-      ew_elem<OP>(a.c0, a.c1, va, acc);
-      ew_elem<OP>(a.c0, a.c1, vb, acc);
 #pragma unroll
-      for (int k = 0; k < 6; ++k)
-        if (T::W & (1 << k)) reinterpret_cast<double2*>(a.p[k])[q] = make_double2(va[k], vb[k]);
+      for (int u = 0; u < U; ++u) {
+        const int64_t q = q0 + u * stride;
+        if (q >= npairs) break;
+        ew_elem<OP>(a.c0, a.c1, va[u], acc);
+        ew_elem<OP>(a.c0, a.c1, vb[u], acc);
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+          if (T::W & (1 << k)) {
+            double2* dst = reinterpret_cast<double2*>(a.p[k]) + q;
+            if constexpr (NTS) {
+              typedef double dv2 __attribute__((ext_vector_type(2)));
+              __builtin_nontemporal_store(dv2{va[u][k], vb[u][k]}, reinterpret_cast<dv2*>(dst));
+            } else {
+              *dst = make_double2(va[u][k], vb[u][k]);
+            }
+          }
+      }
     }
     if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
       const int64_t i = a.n - 1;
@@ -985,10 +1027,18 @@ void ew_dispatch_op(const EwArgs& a, hipStream_t s) {
     if (((EwTraits<OP>::R | EwTraits<OP>::W) & (1 << k)) &&
         (reinterpret_cast<uintptr_t>(a.p[k]) & 15))
       aligned = false;
-  if (aligned)
-    ew_kernel<OP, true><<<a.grid, kBlock, 0, s>>>(a);
-  else
+  // KR_EW_VARIANT (A/B only): 0 = 1 pair/thread/iteration, 1 = 2 pairs,
+  // 2 = 2 pairs + non-temporal stores.
+  const char* env = getenv("KR_EW_VARIANT");
+  const int variant = env ? atoi(env) : 0;
+  if (!aligned)
     ew_kernel<OP, false><<<a.grid, kBlock, 0, s>>>(a);
+  else if (variant == 1)
+    ew_kernel<OP, true, 2><<<a.grid, kBlock, 0, s>>>(a);
+  else if (variant == 2)
+    ew_kernel<OP, true, 2, true><<<a.grid, kBlock, 0, s>>>(a);
+  else
+    ew_kernel<OP, true><<<a.grid, kBlock, 0, s>>>(a);
 }
 
 // ---------------------------------------------------------------------------
@@ -1231,6 +1281,8 @@ int ew_products(EwOp op) {
     case EW_KCG: return EwTraits<EW_KCG>::NP;
     case EW_MRR_S: return EwTraits<EW_MRR_S>::NP;
     case EW_COPY: return EwTraits<EW_COPY>::NP;
+    case EW_MRR_NOX: return EwTraits<EW_MRR_NOX>::NP;
+    case EW_MRR_X2: return EwTraits<EW_MRR_X2>::NP;
   }
   return 0;
 }
@@ -1246,6 +1298,8 @@ void launch_ew(EwOp op, const EwArgs& a, hipStream_t s) {
     case EW_KCG: ew_dispatch_op<EW_KCG>(a, s); break;
     case EW_MRR_S: ew_dispatch_op<EW_MRR_S>(a, s); break;
     case EW_COPY: ew_dispatch_op<EW_COPY>(a, s); break;
+    case EW_MRR_NOX: ew_dispatch_op<EW_MRR_NOX>(a, s); break;
+    case EW_MRR_X2: ew_dispatch_op<EW_MRR_X2>(a, s); break;
     default: throw Failure(KR_ERR_INVALID, "unknown elementwise op");
   }
   KR_HIP_CHECK(hipGetLastError());
