@@ -164,7 +164,9 @@ __device__ __forceinline__ void epi_products(double x, double x2, double y, doub
 typedef double dbl2v __attribute__((ext_vector_type(2)));
 typedef int int4v __attribute__((ext_vector_type(4)));
 constexpr int kSlots = kWindow / (4 * kBlock);
-constexpr int kGather = 8;
+// x gathers in flight per lane: 7 = one batch for 7-point rows (8 issued a
+// redundant 8th load per row; measured +1-2 %).
+constexpr int kGather = 7;
 static_assert(kSlots * 4 * kBlock == kWindow, "window must be a multiple of 4*kBlock");
 
 // Registers holding one staged window. Values move as one 16-byte double2 per
@@ -810,6 +812,8 @@ void spmv_dispatch(SpmvEpi epi, const SpmvArgs& a, hipStream_t s) {
       spmv_kernel_wave<RP, E, VEC><<<grid, block, 0, s>>>(a); \
     else if (variant == 3)                              \
       spmv_kernel<RP, E, VEC, 4><<<grid, block, 0, s>>>(a); \
+    else if (variant == 9)                              \
+      spmv_kernel<RP, E, VEC, 8><<<grid, block, 0, s>>>(a); \
     else if (variant == 8)                              \
       spmv_kernel_prod<RP, E, VEC><<<grid, block, 0, s>>>(a); \
     else if (variant == 6)                              \
