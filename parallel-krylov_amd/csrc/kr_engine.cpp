@@ -128,6 +128,9 @@ System::~System() {
       (void)hipEventDestroy(p.t1);
     }
     for (auto e : s.event_pool) (void)hipEventDestroy(e);
+    if (s.ev_in) (void)hipEventDestroy(s.ev_in);
+    if (s.ev_out) (void)hipEventDestroy(s.ev_out);
+    if (s.comm_stream) (void)hipStreamDestroy(s.comm_stream);
     if (s.ev_a) (void)hipEventDestroy(s.ev_a);
     if (s.ev_b) (void)hipEventDestroy(s.ev_b);
     if (s.stream) (void)hipStreamDestroy(s.stream);
@@ -209,10 +212,26 @@ void System::finalize() {
       for (auto& p : s.recv) p.peer -= first_global;
       s.send.clear();
     }
-    // 4. rewrite columns to local numbering: local = global - row0 + pad
+    // 4. interior rows (every column owned), computed on global columns
     KR_HIP_CHECK(hipSetDevice(s.dev));
+    {
+      int64_t* d = nullptr;
+      KR_HIP_CHECK(hipMalloc(&d, 2 * sizeof(int64_t)));
+      launch_interior(s.rowptr, s.rowptr64, s.n, s.col, s.row0, s.row0 + s.n - 1, d, s.stream);
+      int64_t h[2];
+      KR_HIP_CHECK(hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, s.stream));
+      KR_HIP_CHECK(hipStreamSynchronize(s.stream));
+      KR_HIP_CHECK(hipFree(d));
+      s.int_lo = h[0];
+      s.int_hi = h[1];
+    }
+    if (!s.comm_stream)
+      KR_HIP_CHECK(hipStreamCreateWithFlags(&s.comm_stream, hipStreamNonBlocking));
+    if (!s.ev_in) KR_HIP_CHECK(hipEventCreateWithFlags(&s.ev_in, hipEventDisableTiming));
+    if (!s.ev_out) KR_HIP_CHECK(hipEventCreateWithFlags(&s.ev_out, hipEventDisableTiming));
+    // 5. rewrite columns to local numbering: local = global - row0 + pad
     launch_col_shift(s.rowptr, s.rowptr64, s.n, s.col, s.pad - s.row0, s.stream);
-    // 5. reduction buffers
+    // 6. reduction buffers
     s.grid = default_grid(s.n);
     KR_HIP_CHECK(hipMalloc(&s.partials, sizeof(double) * (size_t)kMaxSlots * s.grid));
     KR_HIP_CHECK(hipMemsetAsync(s.partials, 0, sizeof(double) * (size_t)kMaxSlots * s.grid,
@@ -223,6 +242,10 @@ void System::finalize() {
     if (!s.ev_a) KR_HIP_CHECK(hipEventCreateWithFlags(&s.ev_a, hipEventDisableTiming));
     if (!s.ev_b) KR_HIP_CHECK(hipEventCreateWithFlags(&s.ev_b, hipEventDisableTiming));
     KR_HIP_CHECK(hipStreamSynchronize(s.stream));
+  }
+  {
+    const char* env = getenv("KR_OVERLAP");  // 0 disables the split SpMV (A/B)
+    overlap = !(env && atoi(env) == 0);
   }
   finalized = true;
 }
@@ -343,40 +366,133 @@ void System::halo(int id1, int id2) {
   }
 }
 
+void System::halo_async(int id1, int id2) {
+  if (comm) {
+    Shard& s = shards[0];
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    KR_HIP_CHECK(hipStreamWaitEvent(s.comm_stream, s.ev_in, 0));
+    KR_NCCL_CHECK(ncclGroupStart());
+    for (int id : {id1, id2}) {
+      if (id < 0) continue;
+      for (auto& p : s.send)
+        KR_NCCL_CHECK(ncclSend(s.vec[id] + s.local_index(p.g0), (size_t)p.count, ncclFloat64,
+                               p.peer, comm->nccl, s.comm_stream));
+      for (auto& p : s.recv)
+        KR_NCCL_CHECK(ncclRecv(s.vec[id] + s.local_index(p.g0), (size_t)p.count, ncclFloat64,
+                               p.peer, comm->nccl, s.comm_stream));
+    }
+    KR_NCCL_CHECK(ncclGroupEnd());
+    KR_HIP_CHECK(hipEventRecord(s.ev_out, s.comm_stream));
+    return;
+  }
+  for (auto& s : shards) {
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    for (auto& p : s.recv) {
+      Shard& t = shards[p.peer];
+      KR_HIP_CHECK(hipStreamWaitEvent(s.comm_stream, t.ev_in, 0));
+      for (int id : {id1, id2}) {
+        if (id < 0) continue;
+        double* dst = s.vec[id] + s.local_index(p.g0);
+        const double* src = t.vec[id] + t.local_index(p.g0);
+        if (s.dev == t.dev)
+          KR_HIP_CHECK(hipMemcpyAsync(dst, src, 8 * (size_t)p.count, hipMemcpyDeviceToDevice,
+                                      s.comm_stream));
+        else
+          KR_HIP_CHECK(hipMemcpyPeerAsync(dst, s.dev, src, t.dev, 8 * (size_t)p.count,
+                                          s.comm_stream));
+      }
+    }
+    KR_HIP_CHECK(hipEventRecord(s.ev_out, s.comm_stream));
+  }
+}
+
 void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int b,
                   int slot0) {
   const bool dual = (epi == EPI_DUAL_NONE || epi == EPI_DUAL_MRR || epi == EPI_DUAL_KCG);
   KR_REQUIRE(slot0 + spmv_products(epi) <= kMaxSlots, "reduction slots exhausted");
-  halo(in1, dual ? in2 : -1);
-  for (auto& s : shards) {
-    KR_HIP_CHECK(hipSetDevice(s.dev));
+  const bool exchange =
+      comm ? !(shards[0].recv.empty() && shards[0].send.empty()) : shards.size() > 1;
+  // Split SpMV: the halo exchange runs on a side stream while the interior
+  // rows (no halo column) are multiplied; the boundary rows follow it. The
+  // boundary launches ADD their reduction partials to the interior launch's
+  // (same stream, fixed order: deterministic).
+  bool split = exchange && overlap;
+  for (auto& s : shards)
+    if (s.int_lo >= s.int_hi) split = false;
+  const char* nm = epi_name(epi);
+
+  auto args_for = [&](Shard& s, int64_t r_begin, int64_t rows, int grid, int acc) {
     SpmvArgs a;
-    a.rowptr = s.rowptr;
+    a.rowptr = s.rowptr64 ? (const void*)((const int64_t*)s.rowptr + r_begin)
+                          : (const void*)((const int32_t*)s.rowptr + r_begin);
     a.rowptr64 = s.rowptr64;
     a.col = s.col;
     a.val = s.val;
-    a.n = s.n;
+    a.n = rows;
     a.x1 = s.vec[in1];
     a.x2 = dual ? s.vec[in2] : nullptr;
-    a.xoff = s.pad;
-    a.y1 = s.own(out1);
-    a.y2 = dual ? s.own(out2) : nullptr;
-    a.b = b >= 0 ? s.own(b) : nullptr;
-    a.e = e >= 0 ? s.own(e) : nullptr;
+    a.xoff = s.pad + r_begin;
+    a.y1 = s.own(out1) + r_begin;
+    a.y2 = dual ? s.own(out2) + r_begin : nullptr;
+    a.b = b >= 0 ? s.own(b) + r_begin : nullptr;
+    a.e = e >= 0 ? s.own(e) + r_begin : nullptr;
     a.partials = s.partials + (size_t)slot0 * s.grid;
-    a.grid = s.grid;
+    a.grid = grid;
     a.long_rows = s.n > 0 && (double)s.nnz >= kLongRow * (double)s.n;
-    hipEvent_t t0 = nullptr;
-    const char* nm = epi_name(epi);
-    prof_begin(s, nm, t0);
-    launch_spmv(epi, a, s.stream);
-    if (profile) {
-      const double nv = dual ? 2.0 : 1.0;
-      const double extra = (b >= 0 || e >= 0) ? 8.0 * s.n : 0.0;
-      const double bytes = 12.0 * s.nnz + (s.rowptr64 ? 8.0 : 4.0) * (s.n + 1) +
-                           nv * 16.0 * s.n + extra;
-      prof_end(s, nm, t0, bytes);
+    a.accumulate = acc;
+    return a;
+  };
+  auto bytes_of = [&](Shard& s) {
+    const double nv = dual ? 2.0 : 1.0;
+    const double extra = (b >= 0 || e >= 0) ? 8.0 * s.n : 0.0;
+    return 12.0 * s.nnz + (s.rowptr64 ? 8.0 : 4.0) * (s.n + 1) + nv * 16.0 * s.n + extra;
+  };
+  // The partial stride is s.grid for every launch; a boundary launch with
+  // fewer blocks adds into the first entries.
+  auto launch_part = [&](Shard& s, int64_t r_begin, int64_t rows, int acc) {
+    if (rows <= 0) return;
+    SpmvArgs a = args_for(s, r_begin, rows, s.grid, acc);
+    const int g = (int)std::min<int64_t>(s.grid, (rows + kBlock - 1) / kBlock);
+    SpmvArgs ag = a;
+    ag.grid = s.grid;  // stride
+    launch_spmv_grid(epi, ag, g, s.stream);
+  };
+
+  if (!split) {
+    halo(in1, dual ? in2 : -1);
+    for (auto& s : shards) {
+      KR_HIP_CHECK(hipSetDevice(s.dev));
+      hipEvent_t t0 = nullptr;
+      prof_begin(s, nm, t0);
+      launch_spmv(epi, args_for(s, 0, s.n, s.grid, 0), s.stream);
+      prof_end(s, nm, t0, bytes_of(s));
     }
+    return;
+  }
+  std::vector<hipEvent_t> t0s(shards.size(), nullptr);
+  for (size_t li = 0; li < shards.size(); ++li) {
+    Shard& s = shards[li];
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    prof_begin(s, nm, t0s[li]);
+    KR_HIP_CHECK(hipEventRecord(s.ev_in, s.stream));
+  }
+  halo_async(in1, dual ? in2 : -1);
+  for (auto& s : shards) {  // interior rows: all blocks write their partials
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    launch_spmv(epi, args_for(s, s.int_lo, s.int_hi - s.int_lo, s.grid, 0), s.stream);
+  }
+  for (size_t li = 0; li < shards.size(); ++li) {
+    Shard& s = shards[li];
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    if (comm) {
+      KR_HIP_CHECK(hipStreamWaitEvent(s.stream, s.ev_out, 0));
+    } else {
+      // own halo copied, and every reader done with this shard's rows
+      for (auto& t : shards) KR_HIP_CHECK(hipStreamWaitEvent(s.stream, t.ev_out, 0));
+    }
+    launch_part(s, 0, s.int_lo, 1);
+    launch_part(s, s.int_hi, s.n - s.int_hi, 1);
+    prof_end(s, nm, t0s[li], bytes_of(s));
   }
 }
 

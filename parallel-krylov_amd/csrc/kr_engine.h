@@ -65,6 +65,9 @@ struct Shard {
   int64_t col_lo = 0, col_hi = -1;
   int64_t halo_lo = 0, halo_hi = 0, pad = 0, ld = 0;
   std::vector<HaloPiece> recv, send;
+  int64_t int_lo = 0, int_hi = 0;  // interior rows: all columns owned (no halo)
+  hipStream_t comm_stream = nullptr;  // halo exchange, overlapped with interior rows
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
   int grid = 1;
   // reductions
   double* partials = nullptr;   // [kMaxSlots][grid]
@@ -102,6 +105,7 @@ struct System {
   int first_global = 0;             // global index of shards[0]
   bool finalized = false;
   bool profile = false;
+  bool overlap = true;              // split SpMV: interior rows || halo exchange
   std::unique_ptr<Session> session;
 
   ~System();
@@ -111,6 +115,9 @@ struct System {
   void alloc_vectors(int count);
   // Halo exchange of up to two vectors (ids), all shards.
   void halo(int id1, int id2 = -1);
+  // The same exchange on the shards' comm streams, ordered after ev_in and
+  // signalling ev_out (overlapped path).
+  void halo_async(int id1, int id2);
   void spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int b, int slot0);
   void ew(EwOp op, double c0, double c1, std::array<int, 6> ids, int slot0);
   // Device->host of the summed slots [0, nslots): the one host sync point.

@@ -74,10 +74,13 @@ struct SpmvArgs {
   double* partials = nullptr;  // products: partials[p * grid + block]
   int grid = 0;
   int long_rows = 0;           // 1: product-then-sum kernel (mean nnz/row >= kLongRow)
+  int accumulate = 0;          // 1: add products to the partials (split SpMV, 2nd+ launch)
 };
 // Mean row length from which the product-then-sum SpMV is used.
 constexpr double kLongRow = 12.0;
 void launch_spmv(SpmvEpi epi, const SpmvArgs& a, hipStream_t s);
+// Same with gridDim = nblocks (<= a.grid, the partial stride).
+void launch_spmv_grid(SpmvEpi epi, const SpmvArgs& a, int nblocks, hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // Elementwise vector steps with fused reductions (all own-row pointers).
@@ -146,6 +149,10 @@ void launch_fill_rhs(uint64_t seed, int64_t row0, int64_t n, double* b, hipStrea
 // Column statistics of a CSR block: min and max column (global numbering).
 void launch_col_minmax(const void* rowptr, int rowptr64, int64_t n, const int32_t* col,
                        int64_t* out2 /* device: {min, max} */, hipStream_t s);
+// Interior rows [out2[0], out2[1]) of a block: rows whose columns all lie in
+// [lo, hi] (global numbering). Boundary rows need the halo.
+void launch_interior(const void* rowptr, int rowptr64, int64_t n, const int32_t* col,
+                     int64_t lo, int64_t hi, int64_t* out2, hipStream_t s);
 // col[j] += delta for all stored entries of the block.
 void launch_col_shift(const void* rowptr, int rowptr64, int64_t n, int32_t* col,
                       int64_t delta, hipStream_t s);

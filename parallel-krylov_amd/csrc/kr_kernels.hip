@@ -26,7 +26,8 @@ namespace {
 template <int NP>
 __device__ __forceinline__ void block_reduce_store(double (&acc)[NP > 0 ? NP : 1],
                                                    double* partials, int grid,
-                                                   double* s_red /* NP*4 */) {
+                                                   double* s_red /* NP*4 */,
+                                                   int accumulate = 0) {
   if constexpr (NP > 0) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -44,7 +45,8 @@ __device__ __forceinline__ void block_reduce_store(double (&acc)[NP > 0 ? NP : 1
       t = t + r[1];
       t = t + r[2];
       t = t + r[3];
-      partials[(int64_t)threadIdx.x * grid + blockIdx.x] = t;
+      double* dst = partials + (int64_t)threadIdx.x * grid + blockIdx.x;
+      *dst = accumulate ? *dst + t : t;  // accumulate: a later launch of the same SpMV
     }
   }
 }
@@ -298,7 +300,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
     limit = nrb;
   }
   if (rb >= limit) {
-    block_reduce_store<NP>(acc, a.partials, a.grid, s_red);
+    block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
     return;
   }
   auto block_rows = [&](int64_t b) { return (int)min((int64_t)kBlock, a.n - b * kBlock); };
@@ -399,7 +401,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
     sum2 = 0.0;
   }
   __syncthreads();
-  block_reduce_store<NP>(acc, a.partials, a.grid, s_red);
+  block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
 }
 
 // Product-then-sum SpMV for long rows (variant 8; chosen by the host when
@@ -495,7 +497,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_prod(SpmvArgs a) {
     limit = nrb;
   }
   if (rb >= limit) {
-    block_reduce_store<NP>(acc, a.partials, a.grid, s_red);
+    block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
     return;
   }
   auto block_rows = [&](int64_t b) { return (int)min((int64_t)kBlock, a.n - b * kBlock); };
@@ -594,7 +596,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_prod(SpmvArgs a) {
     sum2 = 0.0;
   }
   __syncthreads();
-  block_reduce_store<NP>(acc, a.partials, a.grid, s_red);
+  block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
 }
 
 // Variant 1: no cross-row-block prefetch (lower VGPR count, higher occupancy).
@@ -682,7 +684,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_simple(SpmvArgs a) {
     }
     __syncthreads();  // s_rp is rewritten by the next row block
   }
-  block_reduce_store<NP>(acc, a.partials, a.grid, s_red);
+  block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
 }
 
 // Variant 2: wave-independent. Each wave owns 64-row blocks and a private
@@ -791,12 +793,12 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_wave(SpmvArgs a) {
       }
     }
   }
-  block_reduce_store<NP>(acc, a.partials, a.grid, s_red);
+  block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
 }
 
 template <typename RP, bool VEC>
-void spmv_dispatch(SpmvEpi epi, const SpmvArgs& a, hipStream_t s) {
-  const dim3 grid(a.grid), block(kBlock);
+void spmv_dispatch(SpmvEpi epi, const SpmvArgs& a, int nblocks, hipStream_t s) {
+  const dim3 grid(nblocks), block(kBlock);
   // Row-walk (0) for short rows, product-then-sum (8) for long rows. The
   // KR_SPMV_VARIANT environment variable overrides the choice for A/B runs
   // (tools/spmv_micro.py): 1 no prefetch, 2 wave-independent, 3 4-deep gathers,
@@ -1224,6 +1226,22 @@ __global__ void col_minmax_kernel(const RP* rowptr, int64_t n, const int32_t* co
   }
 }
 
+// Interior rows of a shard: out[0] = 1 + the last row with a column below
+// [lo, hi], out[1] = the first row with a column above it (global columns).
+template <typename RP>
+__global__ void interior_kernel(const RP* rowptr, int64_t n, const int32_t* col, int64_t lo,
+                                int64_t hi, unsigned long long* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  bool below = false, above = false;
+  for (int64_t j = (int64_t)rowptr[i]; j < (int64_t)rowptr[i + 1]; ++j) {
+    below |= col[j] < lo;
+    above |= col[j] > hi;
+  }
+  if (below) atomicMax(&out[0], (unsigned long long)(i + 1));
+  if (above) atomicMin(&out[1], (unsigned long long)i);
+}
+
 template <typename RP>
 __global__ void col_shift_kernel(const RP* rowptr, int64_t n, int32_t* col, int64_t delta) {
   const int64_t base = (int64_t)rowptr[0];
@@ -1256,21 +1274,26 @@ int spmv_products(SpmvEpi epi) {
 }
 
 void launch_spmv(SpmvEpi epi, const SpmvArgs& a, hipStream_t s) {
-  KR_REQUIRE(a.grid > 0, "spmv: grid must be positive");
+  launch_spmv_grid(epi, a, a.grid, s);
+}
+
+void launch_spmv_grid(SpmvEpi epi, const SpmvArgs& a, int nblocks, hipStream_t s) {
+  KR_REQUIRE(a.grid > 0 && nblocks > 0 && nblocks <= a.grid,
+             "spmv: need 0 < blocks <= partial stride");
   // 16-byte staging needs 16-byte aligned val/col bases
   const bool vec = ((reinterpret_cast<uintptr_t>(a.val) | reinterpret_cast<uintptr_t>(a.col)) &
                     15) == 0;
   (void)vec;
   if (a.rowptr64) {
     if (vec)
-      spmv_dispatch<int64_t, true>(epi, a, s);
+      spmv_dispatch<int64_t, true>(epi, a, nblocks, s);
     else
-      spmv_dispatch<int64_t, false>(epi, a, s);
+      spmv_dispatch<int64_t, false>(epi, a, nblocks, s);
   } else {
     if (vec)
-      spmv_dispatch<int32_t, true>(epi, a, s);
+      spmv_dispatch<int32_t, true>(epi, a, nblocks, s);
     else
-      spmv_dispatch<int32_t, false>(epi, a, s);
+      spmv_dispatch<int32_t, false>(epi, a, nblocks, s);
   }
   KR_HIP_CHECK(hipGetLastError());
 }
@@ -1413,6 +1436,21 @@ void launch_col_minmax(const void* rowptr, int rowptr64, int64_t n, const int32_
   else
     col_minmax_kernel<int32_t><<<1024, kBlock, 0, s>>>(static_cast<const int32_t*>(rowptr),
                                                         n, col, o);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_interior(const void* rowptr, int rowptr64, int64_t n, const int32_t* col,
+                     int64_t lo, int64_t hi, int64_t* out2, hipStream_t s) {
+  const unsigned long long init[2] = {0ull, (unsigned long long)n};
+  KR_HIP_CHECK(hipMemcpyAsync(out2, init, sizeof(init), hipMemcpyHostToDevice, s));
+  if (n <= 0) return;
+  auto* o = reinterpret_cast<unsigned long long*>(out2);
+  if (rowptr64)
+    interior_kernel<int64_t><<<blocks_for(n, 256), 256, 0, s>>>(
+        static_cast<const int64_t*>(rowptr), n, col, lo, hi, o);
+  else
+    interior_kernel<int32_t><<<blocks_for(n, 256), 256, 0, s>>>(
+        static_cast<const int32_t*>(rowptr), n, col, lo, hi, o);
   KR_HIP_CHECK(hipGetLastError());
 }
 

@@ -115,6 +115,23 @@ def test_in_process_shards_match_reference(monkeypatch, name, shards):
     check_parity(c, g, x, info)
 
 
+@pytest.mark.parametrize("name", ["p3d16_cg", "p3d16_kskipmrr_k4", "band2000_kskipmrr_k4"])
+def test_in_process_shards_serial_halo(monkeypatch, name):
+    """KR_OVERLAP=0: the un-split SpMV (halo exchange, then all rows) keeps the
+    parity too; the default path overlaps the exchange with interior rows."""
+    c = next(c for c in CASES if c["name"] == name)
+    g = golden_case(name)
+    A = golden_matrix(c["matrix"])
+    monkeypatch.setenv("KRYLOV_AMD_SHARDS", "0,0,0")
+    monkeypatch.setenv("KR_OVERLAP", "0")
+    kw = dict(tol=c["tol"], maxiter=c["maxiter"])
+    if c["k"] is not None:
+        kw["k"] = c["k"]
+    with contextlib.redirect_stdout(io.StringIO()):
+        x, info = _solver(c["method"])(A, g["b"], **kw)
+    check_parity(c, g, x, info)
+
+
 @pytest.fixture(scope="module")
 def dist_single():
     import os
