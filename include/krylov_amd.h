@@ -155,6 +155,14 @@ int kr_system_csr(kr_system* sys, int shard, const void** rowptr_dev, int* rowpt
 /* Info: n_local, halo_lo, halo_hi, nnz of shard s. */
 int kr_system_shard_info(kr_system* sys, int shard, int64_t* n_local, int64_t* halo_lo,
                          int64_t* halo_hi, int64_t* nnz);
+/* Storage layout the SpMV uses for shard s (after finalize): mask_bits = 0
+ * for plain CSR columns, else 8/16/32/64 when every row's columns are
+ * row + offsets[b] for the set bits b of a per-row mask over n_offsets
+ * distinct offsets (stencil/banded matrices; the column array is then not
+ * read). interior_lo/hi: rows whose columns need no halo (the part of the
+ * SpMV that overlaps the exchange). Pointers may be NULL. */
+int kr_system_shard_layout(kr_system* sys, int shard, int* mask_bits, int* n_offsets,
+                           int64_t* interior_lo, int64_t* interior_hi);
 
 /* Halo exchange plan (pure host arithmetic, no device; test hook and the
  * planner kr_system_finalize uses). part[0..nshards] is the global row

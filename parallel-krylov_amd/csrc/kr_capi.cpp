@@ -458,6 +458,19 @@ int kr_system_shard_info(kr_system* sys, int shard, int64_t* n_local, int64_t* h
   });
 }
 
+int kr_system_shard_layout(kr_system* sys, int shard, int* mask_bits, int* n_offsets,
+                           int64_t* interior_lo, int64_t* interior_hi) {
+  return guarded([&] {
+    KR_REQUIRE(sys && shard >= 0 && shard < (int)sys->shards.size(), "bad shard");
+    KR_REQUIRE(sys->finalized, "system not finalized");
+    const Shard& s = sys->shards[shard];
+    if (mask_bits) *mask_bits = s.mask ? s.mw : 0;
+    if (n_offsets) *n_offsets = s.mask ? s.nm : 0;
+    if (interior_lo) *interior_lo = s.int_lo;
+    if (interior_hi) *interior_hi = s.int_hi;
+  });
+}
+
 int kr_system_csr(kr_system* sys, int shard, const void** rowptr, int* rowptr64,
                   const int32_t** col, const double** val, int64_t* pad) {
   return guarded([&] {

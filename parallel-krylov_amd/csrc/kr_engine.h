@@ -66,6 +66,12 @@ struct Shard {
   int64_t halo_lo = 0, halo_hi = 0, pad = 0, ld = 0;
   std::vector<HaloPiece> recv, send;
   int64_t int_lo = 0, int_hi = 0;  // interior rows: all columns owned (no halo)
+  int64_t reach = 0;                // max |col - row| of the block
+  int64_t slab = 0;                 // SpMV slab schedule (row blocks per plane), 0: contiguous
+  int64_t slab_sub = 0;             // sub-slab width (row blocks)
+  void* mask = nullptr;             // offset masks (SpmvArgs::mask), owned
+  int32_t* moff = nullptr;
+  int nm = 0, mw = 0;
   hipStream_t comm_stream = nullptr;  // halo exchange, overlapped with interior rows
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   int grid = 1;
@@ -114,6 +120,7 @@ struct System {
   void finalize();
   void alloc_vectors(int count);
   // Halo exchange of up to two vectors (ids), all shards.
+  void build_masks(Shard& s);
   void halo(int id1, int id2 = -1);
   // The same exchange on the shards' comm streams, ordered after ev_in and
   // signalling ev_out (overlapped path).

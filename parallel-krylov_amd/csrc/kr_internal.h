@@ -75,6 +75,15 @@ struct SpmvArgs {
   int grid = 0;
   int long_rows = 0;           // 1: product-then-sum kernel (mean nnz/row >= kLongRow)
   int accumulate = 0;          // 1: add products to the partials (split SpMV, 2nd+ launch)
+  int64_t slab = 0;            // >= 8: slab row-block schedule, S row blocks per plane
+  int64_t slab_sub = 0;        // sub-slab width in row blocks (0: one eighth of a plane)
+  // Offset masks (optional, short-row kernel): row i's columns are
+  // xoff + i + moff[b] for the set bits b of mask[i] (mw bits), in order;
+  // col is then not read.
+  const void* mask = nullptr;
+  const int32_t* moff = nullptr;
+  int nm = 0;
+  int mw = 0;
 };
 // Mean row length from which the product-then-sum SpMV is used.
 constexpr double kLongRow = 12.0;
@@ -149,10 +158,21 @@ void launch_fill_rhs(uint64_t seed, int64_t row0, int64_t n, double* b, hipStrea
 // Column statistics of a CSR block: min and max column (global numbering).
 void launch_col_minmax(const void* rowptr, int rowptr64, int64_t n, const int32_t* col,
                        int64_t* out2 /* device: {min, max} */, hipStream_t s);
-// Interior rows [out2[0], out2[1]) of a block: rows whose columns all lie in
-// [lo, hi] (global numbering). Boundary rows need the halo.
+// Interior rows [out3[0], out3[1]) of a block: rows whose columns all lie in
+// [lo, hi] (global numbering; local row 0 is global row lo). Boundary rows
+// need the halo. out3[2] = the column reach max |col - row|.
 void launch_interior(const void* rowptr, int rowptr64, int64_t n, const int32_t* col,
-                     int64_t lo, int64_t hi, int64_t* out2, hipStream_t s);
+                     int64_t lo, int64_t hi, int64_t* out3, hipStream_t s);
+// Distinct column offsets col - (base + row) of a block into table[256]
+// (key offset + 2^32, 0 empty); flags: 1 = a row not strictly increasing,
+// 2 = more than 256 offsets.
+constexpr int kMaxMaskBits = 64;
+constexpr size_t kOffTableBytes = 256 * sizeof(unsigned long long);
+void launch_offsets(const void* rowptr, int rowptr64, int64_t n, const int32_t* col,
+                    int64_t base, unsigned long long* table, int* flags, hipStream_t s);
+// mask[i] (mw-bit integers) = the bits of row i's offsets in M[0..nm).
+void launch_masks(const void* rowptr, int rowptr64, int64_t n, const int32_t* col, int64_t base,
+                  const int32_t* M, int nm, int mw, void* mask, hipStream_t s);
 // col[j] += delta for all stored entries of the block.
 void launch_col_shift(const void* rowptr, int rowptr64, int64_t n, int32_t* col,
                       int64_t delta, hipStream_t s);

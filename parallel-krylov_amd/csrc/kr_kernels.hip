@@ -11,6 +11,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cstdlib>
+#include <type_traits>
 
 #include "kr_hash.h"
 #include "kr_internal.h"
@@ -182,7 +183,7 @@ struct Stage {
   int4v c[kCSlots];
 };
 
-template <bool VEC, bool NT = false>
+template <bool VEC, bool NT = false, bool COLS = true>
 __device__ __forceinline__ void stage_load(Stage& st, const double* __restrict__ val,
                                            const int32_t* __restrict__ col, int64_t ws,
                                            int64_t bs, int64_t be, int tid) {
@@ -199,6 +200,7 @@ __device__ __forceinline__ void stage_load(Stage& st, const double* __restrict__
       st.v[q] = dbl2v{ok0 ? val[g0] : 0.0, ok1 ? val[g0 + 1] : 0.0};
     }
   }
+  if constexpr (!COLS) return;
 #pragma unroll
   for (int q = 0; q < kCSlots; ++q) {
     const int64_t g0 = ws + (int64_t)(tid + q * kBlock) * 4;
@@ -219,12 +221,68 @@ __device__ __forceinline__ void stage_load(Stage& st, const double* __restrict__
   }
 }
 
+template <bool COLS = true>
 __device__ __forceinline__ void stage_commit(const Stage& st, double* s_val, int32_t* s_col,
                                              int tid) {
 #pragma unroll
   for (int q = 0; q < kVSlots; ++q) reinterpret_cast<dbl2v*>(s_val)[tid + q * kBlock] = st.v[q];
+  if constexpr (COLS) {
 #pragma unroll
-  for (int q = 0; q < kCSlots; ++q) reinterpret_cast<int4v*>(s_col)[tid + q * kBlock] = st.c[q];
+    for (int q = 0; q < kCSlots; ++q)
+      reinterpret_cast<int4v*>(s_col)[tid + q * kBlock] = st.c[q];
+  }
+}
+
+// Offset-mask rows (SpmvArgs::mask): the row's columns are xrow + M[b] for
+// the set bits b of its mask, in increasing order (M ascending, columns
+// strictly increasing in the row), so the k-th stored entry uses the k-th set
+// bit. The lane's remaining mask carries across windows.
+template <int MW>
+struct MaskType {
+  using type = uint64_t;
+};
+template <>
+struct MaskType<8> {
+  using type = uint8_t;
+};
+template <>
+struct MaskType<16> {
+  using type = uint16_t;
+};
+template <>
+struct MaskType<32> {
+  using type = uint32_t;
+};
+
+template <int NV, int GATHER, typename W>
+__device__ __forceinline__ void row_window_mask(const double* s_val, const int32_t* s_M,
+                                                const double* __restrict__ x1,
+                                                const double* __restrict__ x2, int64_t xrow,
+                                                int js, int je, W& mrem, double& sum1,
+                                                double& sum2) {
+  for (int j = js; j < je; j += GATHER) {
+    double v[GATHER], p1[GATHER], p2[GATHER];
+#pragma unroll
+    for (int u = 0; u < GATHER; ++u) {
+      const bool ok = j + u < je;
+      v[u] = s_val[ok ? j + u : js];
+      int64_t c = xrow;
+      if (ok) {
+        c += s_M[sizeof(W) == 8 ? __builtin_ctzll((unsigned long long)mrem)
+                                : __builtin_ctz((unsigned)mrem)];
+        mrem &= mrem - 1;
+      }
+      p1[u] = x1[c];
+      if constexpr (NV == 2) p2[u] = x2[c];
+    }
+#pragma unroll
+    for (int u = 0; u < GATHER; ++u) {
+      if (j + u < je) {
+        sum1 = sum1 + v[u] * p1[u];
+        if constexpr (NV == 2) sum2 = sum2 + v[u] * p2[u];
+      }
+    }
+  }
 }
 
 // One lane's entries [js, je) of the staged window, in stored order.
@@ -261,13 +319,82 @@ __device__ __forceinline__ void row_window(const double* s_val, const int32_t* s
 // scalar loads one row block earlier). So a window waits on one memory round
 // trip, for short-row (Poisson: one window per row block) and long-row
 // (banded 27-63 nnz/row: 4-8 windows per row block) matrices alike.
-template <typename RP, int EPI, bool VEC, int GATHER = kGather, bool XCD = true, bool NT = false>
+// Row-block schedule: a workgroup visits rb(j) for j = j0, j0 + jstep, ...
+// < jcount. XCD-aware: workgroups b and b+8 share an XCD (and its L2) under
+// the observed round-robin dispatch, so the workgroups with equal b % 8 work
+// on rows close together and the x entries that neighbouring row blocks
+// gather stay in one L2. Contiguous mode: each XCD sweeps one eighth of the
+// rows (neighbours +-1, +-n reused). Slab mode (S = the matrix's column reach
+// in row blocks): the rows are cut into "planes" of S row blocks and XCD q
+// owns the q-th eighth of every plane, visited plane after plane, so the x
+// rows one plane away (+-n^2 of a 3-D stencil) are still in its L2 when the
+// next plane reads them. With a sub-slab width (slab_sub), XCD q's eighth is
+// cut further into sub-slabs that are swept plane after plane one at a time,
+// which shortens the reuse distance to what its 4 MB L2 holds. Placement only
+// changes speed: every row block is visited exactly once.
+struct RowSched {
+  int64_t j0, jstep, jcount, base = 0, off = 0, w = 0, S = 0, sub = 0, full = 0, rem = 0;
+  int nc = 0;
+  // row blocks of sub-slab c (width wc, all planes; the last plane is partial)
+  __device__ int64_t chunk_count(int c, int64_t wc) const {
+    return full * wc + min(wc, max((int64_t)0, rem - off - c * sub));
+  }
+  __device__ void init(int64_t nrb, int64_t slab, int64_t slab_sub, bool xcd) {
+    if (xcd && (gridDim.x & 7) == 0) {
+      const int64_t q = blockIdx.x & 7;
+      j0 = blockIdx.x >> 3;
+      jstep = gridDim.x >> 3;
+      if (slab >= 8) {
+        S = slab;
+        off = S * q / 8;
+        w = S * (q + 1) / 8 - off;
+        const int64_t planes = (nrb + S - 1) / S;
+        full = planes - 1;
+        rem = nrb - full * S;
+        sub = slab_sub > 0 ? min(slab_sub, w) : w;
+        nc = (int)((w + sub - 1) / sub);
+        jcount = 0;
+        for (int c = 0; c < nc; ++c) jcount += chunk_count(c, min(sub, w - c * sub));
+      } else {
+        const int64_t chunk = (nrb + 7) / 8;
+        base = q * chunk;
+        jcount = max((int64_t)0, min(nrb, base + chunk) - base);
+      }
+    } else {
+      j0 = blockIdx.x;
+      jstep = gridDim.x;
+      jcount = nrb;
+    }
+  }
+  __device__ int64_t rb(int64_t v) const {
+    if (!w) return base + v;
+    // sub-slab after sub-slab; inside one, plane after plane
+    for (int c = 0; c < nc; ++c) {
+      const int64_t wc = min(sub, w - c * sub);
+      const int64_t cnt = chunk_count(c, wc);
+      if (v < cnt) return (v / wc) * S + off + c * sub + v % wc;
+      v -= cnt;
+    }
+    return -1;  // unreachable: v < jcount
+  }
+};
+
+template <typename RP, int EPI, bool VEC, int GATHER = kGather, bool XCD = true, bool NT = false,
+          int MW = 0>
 __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
   using T = EpiTraits<EPI>;
   constexpr int NP = T::NP;
   constexpr int NV = T::NV;
+  constexpr bool COLS = MW == 0;  // else: offset masks, no column stream
+  using MT = typename MaskType<MW>::type;
+  using W = typename std::conditional<(MW > 32), uint64_t, uint32_t>::type;
   __shared__ __attribute__((aligned(16))) double s_val[kWindow];
-  __shared__ __attribute__((aligned(16))) int32_t s_col[kWindow];
+  __shared__ __attribute__((aligned(16))) int32_t s_col[COLS ? kWindow : 4];
+  __shared__ int32_t s_M[COLS ? 1 : 64];
+  const MT* __restrict__ mask = static_cast<const MT*>(a.mask);
+  if constexpr (!COLS) {
+    if ((int)threadIdx.x < a.nm) s_M[threadIdx.x] = a.moff[threadIdx.x];  // seen after 1st barrier
+  }
   __shared__ int32_t s_rp[kBlock + 1];  // row pointers relative to the block start
   __shared__ double s_red[(NP > 0 ? NP : 1) * 4];
 
@@ -283,23 +410,12 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
   for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;
 
   const int64_t nrb = (a.n + kBlock - 1) / kBlock;
-  // Row-block schedule. XCD-aware: workgroups b and b+8 share an XCD (and its
-  // L2) under the observed round-robin dispatch, so the workgroups with equal
-  // b % 8 sweep one contiguous eighth of the rows together and the x rows
-  // that neighbouring row blocks gather (+-1, +-n) stay in one L2. Placement
-  // only changes speed: every row block is still visited exactly once.
-  int64_t rb, step, limit;
-  if (XCD && (gridDim.x & 7) == 0) {
-    const int64_t chunk = (nrb + 7) / 8;
-    rb = (int64_t)(blockIdx.x & 7) * chunk + (blockIdx.x >> 3);
-    step = gridDim.x >> 3;
-    limit = min(nrb, (int64_t)((blockIdx.x & 7) + 1) * chunk);
-  } else {
-    rb = blockIdx.x;
-    step = gridDim.x;
-    limit = nrb;
-  }
-  if (rb >= limit) {
+  RowSched sched;
+  sched.init(nrb, a.slab, a.slab_sub, XCD);
+  int64_t j = sched.j0;
+  const int64_t jstep = sched.jstep, jcount = sched.jcount;
+  auto rb_of = [&](int64_t v) { return sched.rb(v); };
+  if (j >= jcount) {
     block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
     return;
   }
@@ -307,21 +423,24 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
   auto wstart = [](int64_t e) { return VEC ? (e & ~(int64_t)3) : e; };
 
   // current row block
-  int64_t r0 = rb * kBlock;
-  int nr = block_rows(rb);
+  int64_t r0 = rb_of(j) * kBlock;
+  int nr = block_rows(rb_of(j));
   int64_t bs = (int64_t)rowptr[r0];
   int64_t be = (int64_t)rowptr[r0 + nr];
   int64_t my_end = tid < nr ? (int64_t)rowptr[r0 + tid + 1] : 0;
+  W my_mask = 0, my_mask_n = 0, mrem = 0;
+  if constexpr (!COLS) my_mask = tid < nr ? (W)mask[r0 + tid] : 0;
   // next row block: nnz range as scalars (issued now, used one block later)
   int64_t bsn = 0, ben = 0;
-  if (rb + step < limit) {
-    const int64_t r0n = (rb + step) * kBlock;
+  if (j + jstep < jcount) {
+    const int64_t rbn = rb_of(j + jstep);
+    const int64_t r0n = rbn * kBlock;
     bsn = (int64_t)rowptr[r0n];
-    ben = (int64_t)rowptr[r0n + block_rows(rb + step)];
+    ben = (int64_t)rowptr[r0n + block_rows(rbn)];
   }
   Stage st;  // the window in flight
   int64_t ws = wstart(bs);
-  stage_load<VEC, NT>(st, val, col, ws, bs, be, tid);
+  stage_load<VEC, NT, COLS>(st, val, col, ws, bs, be, tid);
   bool first_window = true;
   int rs = 0, re = 0;
   double sum1 = 0.0, sum2 = 0.0;
@@ -335,26 +454,29 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
       if (tid < nr) s_rp[tid + 1] = (int32_t)(my_end - bs);
       if (tid == 0) s_rp[0] = 0;
     }
-    stage_commit(st, s_val, s_col, tid);
+    stage_commit<COLS>(st, s_val, s_col, tid);
     __syncthreads();
     const bool active = tid < nr;
     if (first_window) {
       rs = active ? s_rp[tid] : 0;
       re = active ? s_rp[tid + 1] : 0;
+      mrem = my_mask;
     }
     // issue the next window before working on this one
     const bool last_window = ws + kWindow >= be;
-    const int64_t rb_next = rb + step;
-    const bool has_next = rb_next < limit;
+    const int64_t j_next = j + jstep;
+    const bool has_next = j_next < jcount;
+    const int64_t rb_next = has_next ? rb_of(j_next) : 0;
     if (!last_window) {
-      stage_load<VEC, NT>(st, val, col, ws + kWindow, bs, be, tid);
+      stage_load<VEC, NT, COLS>(st, val, col, ws + kWindow, bs, be, tid);
     } else if (has_next) {
       r0n = rb_next * kBlock;
       nrn = block_rows(rb_next);
       my_end_n = tid < nrn ? (int64_t)rowptr[r0n + tid + 1] : 0;
-      stage_load<VEC, NT>(st, val, col, wstart(bsn), bsn, ben, tid);
-      const int64_t rb_nn = rb_next + step;
-      if (rb_nn < limit) {
+      if constexpr (!COLS) my_mask_n = tid < nrn ? (W)mask[r0n + tid] : 0;
+      stage_load<VEC, NT, COLS>(st, val, col, wstart(bsn), bsn, ben, tid);
+      if (j_next + jstep < jcount) {
+        const int64_t rb_nn = rb_of(j_next + jstep);
         const int64_t r0nn = rb_nn * kBlock;
         bsnn = (int64_t)rowptr[r0nn];
         bennn = (int64_t)rowptr[r0nn + block_rows(rb_nn)];
@@ -363,8 +485,13 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
     // this lane's entries inside the window (window offsets)
     if (active) {
       const int64_t off = bs - ws;
-      row_window<NV, GATHER>(s_val, s_col, x1, x2, (int)max((int64_t)rs + off, (int64_t)0),
-                             (int)min((int64_t)re + off, (int64_t)kWindow), sum1, sum2);
+      const int js = (int)max((int64_t)rs + off, (int64_t)0);
+      const int je = (int)min((int64_t)re + off, (int64_t)kWindow);
+      if constexpr (COLS)
+        row_window<NV, GATHER>(s_val, s_col, x1, x2, js, je, sum1, sum2);
+      else
+        row_window_mask<NV, GATHER>(s_val, s_M, x1, x2, a.xoff + r0 + tid, js, je, mrem, sum1,
+                                    sum2);
     }
     if (!last_window) {
       __syncthreads();  // LDS is rewritten by the next window
@@ -387,7 +514,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
     }
     if (!has_next) break;
     __syncthreads();  // LDS and s_rp are rewritten by the next row block
-    rb = rb_next;
+    j = j_next;
     r0 = r0n;
     nr = nrn;
     bs = bsn;
@@ -395,6 +522,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
     bsn = bsnn;
     ben = bennn;
     my_end = my_end_n;
+    my_mask = my_mask_n;
     ws = wstart(bs);
     first_window = true;
     sum1 = 0.0;
@@ -485,34 +613,29 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_prod(SpmvArgs a) {
   for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;
 
   const int64_t nrb = (a.n + kBlock - 1) / kBlock;
-  int64_t rb, step, limit;
-  if ((gridDim.x & 7) == 0) {  // XCD-contiguous sweep, as spmv_kernel
-    const int64_t chunk = (nrb + 7) / 8;
-    rb = (int64_t)(blockIdx.x & 7) * chunk + (blockIdx.x >> 3);
-    step = gridDim.x >> 3;
-    limit = min(nrb, (int64_t)((blockIdx.x & 7) + 1) * chunk);
-  } else {
-    rb = blockIdx.x;
-    step = gridDim.x;
-    limit = nrb;
-  }
-  if (rb >= limit) {
+  RowSched sched;  // as spmv_kernel
+  sched.init(nrb, a.slab, a.slab_sub, true);
+  int64_t j = sched.j0;
+  const int64_t jstep = sched.jstep, jcount = sched.jcount;
+  auto rb_of = [&](int64_t v) { return sched.rb(v); };
+  if (j >= jcount) {
     block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
     return;
   }
   auto block_rows = [&](int64_t b) { return (int)min((int64_t)kBlock, a.n - b * kBlock); };
   auto wstart = [](int64_t e) { return VEC ? (e & ~(int64_t)1) : e; };
 
-  int64_t r0 = rb * kBlock;
-  int nr = block_rows(rb);
+  int64_t r0 = rb_of(j) * kBlock;
+  int nr = block_rows(rb_of(j));
   int64_t bs = (int64_t)rowptr[r0];
   int64_t be = (int64_t)rowptr[r0 + nr];
   int64_t my_end = tid < nr ? (int64_t)rowptr[r0 + tid + 1] : 0;
   int64_t bsn = 0, ben = 0;
-  if (rb + step < limit) {
-    const int64_t r0n = (rb + step) * kBlock;
+  if (j + jstep < jcount) {
+    const int64_t rbn = rb_of(j + jstep);
+    const int64_t r0n = rbn * kBlock;
     bsn = (int64_t)rowptr[r0n];
-    ben = (int64_t)rowptr[r0n + block_rows(rb + step)];
+    ben = (int64_t)rowptr[r0n + block_rows(rbn)];
   }
   PStage st;
   int64_t ws = wstart(bs);
@@ -536,8 +659,9 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_prod(SpmvArgs a) {
       re = active ? s_rp[tid + 1] : 0;
     }
     const bool last_window = ws + kWindow >= be;
-    const int64_t rb_next = rb + step;
-    const bool has_next = rb_next < limit;
+    const int64_t j_next = j + jstep;
+    const bool has_next = j_next < jcount;
+    const int64_t rb_next = has_next ? rb_of(j_next) : 0;
     if (!last_window) {
       pstage_load<VEC>(st, val, col, ws + kWindow, bs, be, tid);
     } else if (has_next) {
@@ -545,8 +669,8 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_prod(SpmvArgs a) {
       nrn = block_rows(rb_next);
       my_end_n = tid < nrn ? (int64_t)rowptr[r0n + tid + 1] : 0;
       pstage_load<VEC>(st, val, col, wstart(bsn), bsn, ben, tid);
-      const int64_t rb_nn = rb_next + step;
-      if (rb_nn < limit) {
+      if (j_next + jstep < jcount) {
+        const int64_t rb_nn = rb_of(j_next + jstep);
         const int64_t r0nn = rb_nn * kBlock;
         bsnn = (int64_t)rowptr[r0nn];
         bennn = (int64_t)rowptr[r0nn + block_rows(rb_nn)];
@@ -582,7 +706,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_prod(SpmvArgs a) {
     }
     if (!has_next) break;
     __syncthreads();
-    rb = rb_next;
+    j = j_next;
     r0 = r0n;
     nr = nrn;
     bs = bsn;
@@ -796,6 +920,21 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_wave(SpmvArgs a) {
   block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
 }
 
+// The offset-mask row walk (SpmvArgs::mask); false if not applicable.
+template <typename RP, int E, bool VEC>
+bool spmv_masked(const SpmvArgs& a, dim3 grid, dim3 block, hipStream_t s) {
+  if constexpr (VEC) {
+    switch (a.mw) {
+      case 8: spmv_kernel<RP, E, VEC, kGather, true, false, 8><<<grid, block, 0, s>>>(a); return true;
+      case 16: spmv_kernel<RP, E, VEC, kGather, true, false, 16><<<grid, block, 0, s>>>(a); return true;
+      case 32: spmv_kernel<RP, E, VEC, kGather, true, false, 32><<<grid, block, 0, s>>>(a); return true;
+      case 64: spmv_kernel<RP, E, VEC, kGather, true, false, 64><<<grid, block, 0, s>>>(a); return true;
+      default: return false;
+    }
+  }
+  return false;
+}
+
 template <typename RP, bool VEC>
 void spmv_dispatch(SpmvEpi epi, const SpmvArgs& a, int nblocks, hipStream_t s) {
   const dim3 grid(nblocks), block(kBlock);
@@ -822,7 +961,7 @@ void spmv_dispatch(SpmvEpi epi, const SpmvArgs& a, int nblocks, hipStream_t s) {
       spmv_kernel<RP, E, VEC, kGather, false><<<grid, block, 0, s>>>(a); \
     else if (variant == 7)                              \
       spmv_kernel<RP, E, VEC, kGather, true, true><<<grid, block, 0, s>>>(a); \
-    else                                                \
+    else if (!(a.mask && spmv_masked<RP, E, VEC>(a, grid, block, s))) \
       spmv_kernel<RP, E, VEC><<<grid, block, 0, s>>>(a); \
     break;
     KR_CASE(EPI_NONE)
@@ -1228,18 +1367,77 @@ __global__ void col_minmax_kernel(const RP* rowptr, int64_t n, const int32_t* co
 
 // Interior rows of a shard: out[0] = 1 + the last row with a column below
 // [lo, hi], out[1] = the first row with a column above it (global columns).
+// out[2] = the column reach max |col - row| (global row = lo + local row).
 template <typename RP>
 __global__ void interior_kernel(const RP* rowptr, int64_t n, const int32_t* col, int64_t lo,
                                 int64_t hi, unsigned long long* out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   bool below = false, above = false;
+  int64_t reach = 0;
   for (int64_t j = (int64_t)rowptr[i]; j < (int64_t)rowptr[i + 1]; ++j) {
     below |= col[j] < lo;
     above |= col[j] > hi;
+    const int64_t d = (int64_t)col[j] - (lo + i);
+    reach = max(reach, d < 0 ? -d : d);
   }
   if (below) atomicMax(&out[0], (unsigned long long)(i + 1));
   if (above) atomicMin(&out[1], (unsigned long long)i);
+  if (reach > 0) atomicMax(&out[2], (unsigned long long)reach);
+}
+
+// Offset-mask detection. The distinct offsets col - (base + row) of a block
+// go into a small open-addressing table (key = offset + 2^32, 0 = empty);
+// flags bit 0: a row whose columns are not strictly increasing, bit 1: table
+// full.
+constexpr int kOffTable = 256;
+
+template <typename RP>
+__global__ void offsets_kernel(const RP* rowptr, int64_t n, const int32_t* col, int64_t base,
+                               unsigned long long* table, int* flags) {
+  int bad = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t prev = INT64_MIN;
+    for (int64_t j = (int64_t)rowptr[i]; j < (int64_t)rowptr[i + 1]; ++j) {
+      const int64_t off = (int64_t)col[j] - (base + i);
+      if (off <= prev) bad |= 1;
+      prev = off;
+      const unsigned long long key = (unsigned long long)(off + (1ll << 32));
+      unsigned h = (unsigned)((key * 0x9E3779B97F4A7C15ull) >> 56) & (kOffTable - 1);
+      int probe = 0;
+      for (; probe < kOffTable; ++probe) {
+        const unsigned long long v = __atomic_load_n(&table[h], __ATOMIC_RELAXED);
+        if (v == key) break;
+        if (v == 0) {
+          const unsigned long long old = atomicCAS(&table[h], 0ull, key);
+          if (old == 0 || old == key) break;
+        }
+        h = (h + 1) & (kOffTable - 1);
+      }
+      if (probe == kOffTable) bad |= 2;
+    }
+  }
+  if (bad) atomicOr(flags, bad);
+}
+
+template <typename RP, typename MT>
+__global__ void mask_kernel(const RP* rowptr, int64_t n, const int32_t* col, int64_t base,
+                            const int32_t* M, int nm, MT* mask) {
+  __shared__ int32_t sM[64];
+  if ((int)threadIdx.x < nm) sM[threadIdx.x] = M[threadIdx.x];
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    MT m = 0;
+    for (int64_t j = (int64_t)rowptr[i]; j < (int64_t)rowptr[i + 1]; ++j) {
+      const int64_t off = (int64_t)col[j] - (base + i);
+      int b = 0;
+      while (b < nm - 1 && sM[b] != off) ++b;
+      m |= (MT)((MT)1 << b);
+    }
+    mask[i] = m;
+  }
 }
 
 template <typename RP>
@@ -1441,7 +1639,7 @@ void launch_col_minmax(const void* rowptr, int rowptr64, int64_t n, const int32_
 
 void launch_interior(const void* rowptr, int rowptr64, int64_t n, const int32_t* col,
                      int64_t lo, int64_t hi, int64_t* out2, hipStream_t s) {
-  const unsigned long long init[2] = {0ull, (unsigned long long)n};
+  const unsigned long long init[3] = {0ull, (unsigned long long)n, 0ull};
   KR_HIP_CHECK(hipMemcpyAsync(out2, init, sizeof(init), hipMemcpyHostToDevice, s));
   if (n <= 0) return;
   auto* o = reinterpret_cast<unsigned long long*>(out2);
@@ -1451,6 +1649,45 @@ void launch_interior(const void* rowptr, int rowptr64, int64_t n, const int32_t*
   else
     interior_kernel<int32_t><<<blocks_for(n, 256), 256, 0, s>>>(
         static_cast<const int32_t*>(rowptr), n, col, lo, hi, o);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_offsets(const void* rowptr, int rowptr64, int64_t n, const int32_t* col,
+                    int64_t base, unsigned long long* table, int* flags, hipStream_t s) {
+  KR_HIP_CHECK(hipMemsetAsync(table, 0, kOffTable * sizeof(unsigned long long), s));
+  KR_HIP_CHECK(hipMemsetAsync(flags, 0, sizeof(int), s));
+  if (n <= 0) return;
+  const unsigned g = std::min<unsigned>(blocks_for(n, 256), 4096);
+  if (rowptr64)
+    offsets_kernel<int64_t><<<g, 256, 0, s>>>(static_cast<const int64_t*>(rowptr), n, col, base,
+                                              table, flags);
+  else
+    offsets_kernel<int32_t><<<g, 256, 0, s>>>(static_cast<const int32_t*>(rowptr), n, col, base,
+                                              table, flags);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
+template <typename MT>
+static void masks_typed(const void* rowptr, int rowptr64, int64_t n, const int32_t* col,
+                        int64_t base, const int32_t* M, int nm, void* mask, hipStream_t s) {
+  const unsigned g = std::min<unsigned>(blocks_for(n, 256), 4096);
+  if (rowptr64)
+    mask_kernel<int64_t, MT><<<g, 256, 0, s>>>(static_cast<const int64_t*>(rowptr), n, col, base,
+                                               M, nm, static_cast<MT*>(mask));
+  else
+    mask_kernel<int32_t, MT><<<g, 256, 0, s>>>(static_cast<const int32_t*>(rowptr), n, col, base,
+                                               M, nm, static_cast<MT*>(mask));
+}
+
+void launch_masks(const void* rowptr, int rowptr64, int64_t n, const int32_t* col, int64_t base,
+                  const int32_t* M, int nm, int mw, void* mask, hipStream_t s) {
+  KR_REQUIRE(nm >= 1 && nm <= mw && (mw == 8 || mw == 16 || mw == 32 || mw == 64),
+             "offset masks: bad width");
+  if (n <= 0) return;
+  if (mw == 8) masks_typed<uint8_t>(rowptr, rowptr64, n, col, base, M, nm, mask, s);
+  else if (mw == 16) masks_typed<uint16_t>(rowptr, rowptr64, n, col, base, M, nm, mask, s);
+  else if (mw == 32) masks_typed<uint32_t>(rowptr, rowptr64, n, col, base, M, nm, mask, s);
+  else masks_typed<uint64_t>(rowptr, rowptr64, n, col, base, M, nm, mask, s);
   KR_HIP_CHECK(hipGetLastError());
 }
 

@@ -217,6 +217,16 @@ class KrylovSystem:
         call("kr_system_shard_info", self.handle, s, *[ctypes.byref(t) for t in v])
         return dict(zip(("n_local", "halo_lo", "halo_hi", "nnz"), [t.value for t in v]))
 
+    def shard_layout(self, s: int) -> dict:
+        """SpMV storage of shard s: mask_bits (0 = CSR columns), n_offsets,
+        interior row range [interior_lo, interior_hi)."""
+        mb, no = ctypes.c_int(), ctypes.c_int()
+        lo, hi = ctypes.c_int64(), ctypes.c_int64()
+        call("kr_system_shard_layout", self.handle, s, ctypes.byref(mb), ctypes.byref(no),
+             ctypes.byref(lo), ctypes.byref(hi))
+        return dict(mask_bits=mb.value, n_offsets=no.value, interior_lo=lo.value,
+                    interior_hi=hi.value)
+
     def csr_pointers(self, s: int) -> dict:
         """Raw device CSR of shard s (local columns after finalize)."""
         rp, col, val = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()

@@ -182,3 +182,50 @@ def test_halo_plan_is_consistent(P):
     # one shard: no exchange at all
     if P == 1:
         assert plans[0] == ([], [])
+
+
+def _row_sched(nrb, slab, grid, sub=0):
+    """Host restatement of the SpMV row-block schedule (RowSched in
+    kr_kernels.hip): the row blocks every workgroup visits."""
+    out = []
+    for blk in range(grid):
+        if grid % 8 == 0:
+            q, j, step = blk & 7, blk >> 3, grid >> 3
+            if slab >= 8:
+                off, w = slab * q // 8, slab * (q + 1) // 8 - slab * q // 8
+                planes = (nrb + slab - 1) // slab
+                full, rem = planes - 1, nrb - (planes - 1) * slab
+                sw = min(sub, w) if sub > 0 else w
+                nc = (w + sw - 1) // sw
+                chunks = []
+                for c in range(nc):
+                    wc = min(sw, w - c * sw)
+                    chunks.append((c, wc, full * wc + min(wc, max(0, rem - off - c * sw))))
+                count = sum(ch[2] for ch in chunks)
+
+                def rb(v, off=off, sw=sw, chunks=chunks):
+                    for c, wc, cnt in chunks:
+                        if v < cnt:
+                            return (v // wc) * slab + off + c * sw + v % wc
+                        v -= cnt
+                    raise AssertionError("v out of range")
+            else:
+                chunk = (nrb + 7) // 8
+                base = q * chunk
+                count = max(0, min(nrb, base + chunk) - base)
+                rb = lambda v, base=base: base + v  # noqa: E731
+        else:
+            j, step, count = blk, grid, nrb
+            rb = lambda v: v  # noqa: E731
+        while j < count:
+            out.append(rb(j))
+            j += step
+    return out
+
+
+@pytest.mark.parametrize("nrb", [1, 7, 8, 250, 1023, 5003])
+@pytest.mark.parametrize("slab", [0, 8, 13, 250, 1024, 100000])
+@pytest.mark.parametrize("grid", [1, 24, 2048])
+@pytest.mark.parametrize("sub", [0, 1, 5, 32])
+def test_row_schedule_visits_every_block_once(nrb, slab, grid, sub):
+    assert sorted(_row_sched(nrb, slab, grid, sub)) == list(range(nrb))

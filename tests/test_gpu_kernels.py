@@ -224,3 +224,103 @@ def test_adopted_csr_sharded_spmv_bitwise(torch_dev):
         y = sysm.gather(sysm.spmv(sysm.split(x))).cpu().numpy()
         np.testing.assert_array_equal(y, A.dot(x))
         sysm.close()
+
+
+@pytest.mark.parametrize("slab", ["0", "8", "13", "37", "250", "4000", "37/2", "250/16"])
+@pytest.mark.parametrize("spec", [("poisson", 40, 3), ("banded", 64000, 13, 64, 0)])
+def test_slab_schedule_spmv_bitwise(torch_dev, monkeypatch, spec, slab):
+    """KR_SLAB=S forces the slab row-block schedule (S row blocks per plane):
+    every row block visited once, for the short-row and the product kernels,
+    with a partial last plane and S not a multiple of 8."""
+    from parallel_krylov_amd.system import KrylovSystem
+    slab, _, sub = slab.partition("/")
+    monkeypatch.setenv("KR_SLAB", slab)
+    monkeypatch.setenv("KR_SLAB_SUB", sub or "0")
+    A = golden_matrix(list(spec))
+    n = A.shape[0]
+    sysm = KrylovSystem(n, [0, n], [0])
+    if spec[0] == "poisson":
+        sysm.gen_poisson(spec[1], spec[2])
+    else:
+        sysm.gen_banded(spec[2], spec[3], spec[4])
+    sysm.finalize()
+    x = np.random.default_rng(5).standard_normal(n)
+    y = sysm.gather(sysm.spmv(sysm.split(x))).cpu().numpy()
+    np.testing.assert_array_equal(y, A.dot(x))
+    # the fused dual SpMV's Gram partials cover every row too (dot order
+    # differs between schedules: compare with the contiguous one to rounding)
+    out = sysm.solve("kskipmrr", sysm.rhs(1), tol=0.0, maxiter=10, k=4)
+    sysm.close()
+    monkeypatch.setenv("KR_SLAB", "0")
+    ref_sys = KrylovSystem(n, [0, n], [0])
+    ref_sys.set_matrix(A)
+    ref_sys.finalize()
+    ref = ref_sys.solve("kskipmrr", ref_sys.rhs(1), tol=0.0, maxiter=10, k=4)
+    ref_sys.close()
+    np.testing.assert_array_equal(out.info["nosl"], ref.info["nosl"])
+    np.testing.assert_allclose(out.info["residual"], ref.info["residual"], rtol=1e-10)
+
+
+def _offset_matrix(n, offsets, per_row, seed, sort=True):
+    """Rows with `per_row` entries at column offsets drawn from `offsets`
+    (clipped at the edges): a short-row matrix with len(offsets) distinct
+    offsets, for the offset-mask layout."""
+    rng = np.random.default_rng(seed)
+    offsets = np.asarray(offsets)
+    rows, cols = [], []
+    for i in range(n):
+        c = i + rng.choice(offsets, size=per_row, replace=False)
+        c = c[(c >= 0) & (c < n)]
+        rows.append(np.full(c.size, i))
+        cols.append(c)
+    A = sp.csr_matrix((rng.standard_normal(sum(c.size for c in cols)),
+                       (np.concatenate(rows), np.concatenate(cols))), shape=(n, n))
+    A.sort_indices()
+    if not sort:  # reverse each row's stored order (same matrix, unsorted)
+        for i in range(n):
+            a, b = A.indptr[i], A.indptr[i + 1]
+            A.indices[a:b] = A.indices[a:b][::-1].copy()
+            A.data[a:b] = A.data[a:b][::-1].copy()
+        A.has_sorted_indices = False
+    return A
+
+
+MASKED = {
+    # name: (builder, expected mask bits)
+    "poisson2d_40": (lambda: golden_matrix(["poisson", 40, 2]), 8),
+    "poisson3d_21": (lambda: golden_matrix(["poisson", 21, 3]), 8),
+    "banded7_4099": (lambda: golden_matrix(["banded", 4099, 3, 64, 0]), 8),
+    "offsets13": (lambda: _offset_matrix(6000, np.arange(-6, 7) * 37, 5, 1), 16),
+    "offsets31": (lambda: _offset_matrix(6000, np.arange(-15, 16) * 5, 6, 2), 32),
+    "offsets64": (lambda: _offset_matrix(6000, np.arange(-32, 32) * 3 + 1, 8, 3), 64),
+    "offsets65": (lambda: _offset_matrix(6000, np.arange(-32, 33) * 3, 8, 4), 0),
+    "unsorted": (lambda: _offset_matrix(3000, np.arange(-3, 4), 4, 5, sort=False), 0),
+    "long_rows": (lambda: golden_matrix(["banded", 3001, 13, 64, 0]), 0),
+}
+
+
+@pytest.mark.parametrize("shards", [1, 3])
+@pytest.mark.parametrize("name", list(MASKED))
+def test_offset_mask_layout_spmv_bitwise(torch_dev, monkeypatch, name, shards):
+    """Short-row matrices with <= 64 distinct column offsets use the offset-
+    mask layout (no column stream); the SpMV stays bitwise scipy's, with
+    KR_MASK=0 (plain columns) as the control."""
+    from parallel_krylov_amd.system import KrylovSystem, balanced_partition
+    builder, bits = MASKED[name]
+    A = builder()
+    n = A.shape[0]
+    x = np.random.default_rng(9).standard_normal(n)
+    ref = sp.csr_matrix(A).dot(x) if name != "unsorted" else A.toarray().dot(x)
+    for mask_env in ("1", "0"):
+        monkeypatch.setenv("KR_MASK", mask_env)
+        sysm = KrylovSystem(n, balanced_partition(n, shards), [0] * shards)
+        sysm.set_matrix(A)
+        sysm.finalize()
+        lay = sysm.shard_layout(0)
+        assert lay["mask_bits"] == (bits if mask_env == "1" else 0)
+        y = sysm.gather(sysm.spmv(sysm.split(x))).cpu().numpy()
+        if name == "unsorted":  # stored order differs from scipy's sorted sum
+            np.testing.assert_allclose(y, ref, rtol=1e-13, atol=1e-13)
+        else:
+            np.testing.assert_array_equal(y, A.dot(x))
+        sysm.close()
