@@ -63,6 +63,10 @@ const char* epi_name(SpmvEpi e) {
     case EPI_DUAL_NONE: return "spmv2";
     case EPI_DUAL_MRR: return "spmv2_gram_mrr";
     case EPI_DUAL_KCG: return "spmv2_gram_kcg";
+    case EPI_STEP_MRR_NOX: return "spmv_step_mrr_nox";
+    case EPI_STEP_MRR_X2: return "spmv_step_mrr_x2";
+    case EPI_STEP_MRR_X: return "spmv_step_mrr_x";
+    case EPI_STEP_KCG: return "spmv_step_kcg";
   }
   return "spmv?";
 }
@@ -296,6 +300,18 @@ void System::finalize() {
   {
     const char* env = getenv("KR_OVERLAP");  // 0 disables the split SpMV (A/B)
     overlap = !(env && atoi(env) == 0);
+    const char* fz = getenv("KR_FUSE");  // 0: separate vector-step kernels (A/B)
+    // Fusion pays for the short-row (row-walk) kernel: C4 +6 %. With the
+    // product-then-sum kernel (long rows) the fused SpMV costs more than the
+    // separate vector pass (C5: +0.9 ms vs +0.5 ms), so long rows keep it.
+    bool long_rows = false;
+    for (auto& s : shards)
+      if (s.n > 0 && (double)s.nnz >= kLongRow * (double)s.n) long_rows = true;
+    fuse_steps = fz ? atoi(fz) != 0 : !long_rows;
+    // Own-row epilogue operands loaded at the row end (default) or at the
+    // row-block start (KR_EPI_LATE=0): late measured 1-3 % faster on C4.
+    const char* el = getenv("KR_EPI_LATE");
+    epi_late = el ? atoi(el) != 0 : 1;
   }
   finalized = true;
 }
@@ -457,8 +473,14 @@ void System::halo_async(int id1, int id2) {
 }
 
 void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int b,
-                  int slot0) {
+                  int slot0, const StepOps* st) {
   const bool dual = (epi == EPI_DUAL_NONE || epi == EPI_DUAL_MRR || epi == EPI_DUAL_KCG);
+  const bool step = (epi == EPI_STEP_MRR_NOX || epi == EPI_STEP_MRR_X2 ||
+                     epi == EPI_STEP_MRR_X || epi == EPI_STEP_KCG);
+  KR_REQUIRE(!step || (st && st->u1 >= 0 && st->u2 >= 0 && out1 != in1),
+             "fused step: operands missing or output aliases the input");
+  const bool step_x = (epi == EPI_STEP_MRR_X2 || epi == EPI_STEP_MRR_X);
+  KR_REQUIRE(!step_x || (st->us >= 0 && st->ud >= 0), "fused step: x operands missing");
   KR_REQUIRE(slot0 + spmv_products(epi) <= kMaxSlots, "reduction slots exhausted");
   const bool exchange =
       comm ? !(shards[0].recv.empty() && shards[0].send.empty()) : shards.size() > 1;
@@ -498,11 +520,24 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
       a.nm = s.nm;
       a.mw = s.mw;
     }
+    a.epi_late = epi_late;
+    if (step) {
+      a.u1 = s.own(st->u1) + r_begin;
+      a.u2 = s.own(st->u2) + r_begin;
+      if (step_x) {
+        a.us = s.own(st->us) + r_begin;
+        a.ud = s.own(st->ud) + r_begin;
+      }
+      a.c0 = st->c0;
+      a.c1 = st->c1;
+    }
     return a;
   };
   auto bytes_of = [&](Shard& s) {
     const double nv = dual ? 2.0 : 1.0;
-    const double extra = (b >= 0 || e >= 0) ? 8.0 * s.n : 0.0;
+    // fused step: u1, u2 read and written (+ x read and written)
+    const double extra = step ? (step_x ? 48.0 : 32.0) * s.n
+                              : (b >= 0 || e >= 0) ? 8.0 * s.n : 0.0;
     return 12.0 * s.nnz + (s.rowptr64 ? 8.0 : 4.0) * (s.n + 1) + nv * 16.0 * s.n + extra;
   };
   // The partial stride is s.grid for every launch; a boundary launch with
@@ -747,31 +782,39 @@ class MrrSession : public Base {
 // v3/gpu/kskipmrr.py:9-110 (oracle v3/cpu/kskipmrr.py:8-108) and, with
 // adaptive = true, v3/cpu/adaptivekskipmrr.py:8-141 semantics.
 class KskipMrrSession : public Base {
-  // vector ids: fixed ones, then Ar[0..k0+1], Ay[0..k0]
-  enum { XA, XB, B, Z, FIXED };
+  // vector ids: fixed ones, then Ar[0..k0+1], Ay[0..k0]. Ar[0] (r) lives in
+  // one of two buffers, r0 / r_alt: a fused step SpMV reads r from one and
+  // writes the next r into the other (other rows still gather the old r).
+  enum { XA, XB, B, Z, RALT, FIXED };
   int k0 = 0;
   bool adaptive = false;
   int cur = XA, pre = XB;  // current x buffer / adaptive snapshot buffer
   int xsrc = XA;           // source of the next x update
+  int r0 = FIXED, r_alt = RALT;
   double pre_residual = 0;
   int AR(int j) const { return FIXED + j; }
   int AY(int j) const { return FIXED + (k0 + 2) + j; }
   static constexpr int kHead = 5;
   int gram_slots(int kk) const { return kHead + 7 * kk; }
 
-  void head() { sys->spmv(EPI_HEAD_MRR, AR(0), -1, AR(1), -1, AY(0), -1, 0); }
+  void head() { sys->spmv(EPI_HEAD_MRR, r0, -1, AR(1), -1, AY(0), -1, 0); }
   void chain(int kk) {
     for (int m = 0; m < kk; ++m)
       sys->spmv(EPI_DUAL_MRR, AR(m + 1), AY(m), AR(m + 2), AY(m + 1), -1, -1, kHead + 7 * m);
   }
   // Initial / restart MrR step (v3/cpu/kskipmrr.py:26-31).
   void mrr_first(int x_from) {
-    sys->spmv(EPI_XY, AR(0), -1, AR(1), -1, -1, -1, 0);
+    sys->spmv(EPI_XY, r0, -1, AR(1), -1, -1, -1, 0);
     const auto g = sys->reduce(3);
     const double zeta = g[1] / g[2];
-    sys->ew(EW_MRR_FIRST, 0, zeta, {AY(0), AR(1), Z, AR(0), x_from, cur}, 0);
+    sys->ew(EW_MRR_FIRST, 0, zeta, {AY(0), AR(1), Z, r0, x_from, cur}, 0);
     xsrc = cur;
   }
+  // x -= z is deferred pairwise: step j stores z and leaves x (kind 0), step
+  // j+1 applies x = (x - z_j) - z_{j+1} in registers (kind 1) -- the same two
+  // roundings as the reference's two statements, one x read+write fewer. The
+  // last step of an outer iteration applies its own x -= z (kind 2).
+  int step_kind(int j) const { return (j % 2 == 0 && j < k) ? 0 : (j % 2 == 1 ? 1 : 2); }
 
  public:
   explicit KskipMrrSession(bool adapt) : adaptive(adapt) {}
@@ -781,9 +824,11 @@ class KskipMrrSession : public Base {
     k0 = k;
     KR_REQUIRE(k >= 0 && gram_slots(k) <= kMaxSlots, "k out of range");
     sys->alloc_vectors(FIXED + (k0 + 2) + (k0 + 1));
+    r0 = AR(0);
+    r_alt = RALT;
     load_bx(B, XA, b, x0);
     if (adaptive) sys->copy_own(XB, XA);  // pre_x guard = x0
-    sys->spmv(EPI_BMINUS, XA, -1, AR(0), -1, -1, B, 0);
+    sys->spmv(EPI_BMINUS, XA, -1, r0, -1, -1, B, 0);
     set_entry(0, rel(sys->reduce(1)[0]));
     pre_residual = residual[0];
     set_nosl(0, 0);
@@ -810,7 +855,7 @@ class KskipMrrSession : public Base {
     if (adaptive) {
       if (residual[index] > pre_residual) {
         // roll back to the snapshot and restart (v3/cpu/adaptivekskipmrr.py:45-66)
-        sys->spmv(EPI_BMINUS, pre, -1, AR(0), -1, -1, B, 0);
+        sys->spmv(EPI_BMINUS, pre, -1, r0, -1, -1, B, 0);
         mrr_first(pre);
         i += 1;
         index += 1;
@@ -851,22 +896,44 @@ class KskipMrrSession : public Base {
     }
     std::vector<double> zeta(k + 1), eta(k + 1);
     kskipmrr_recurrence(k, alpha.data(), beta.data(), delta.data(), zeta.data(), eta.data());
-    for (int j = 0; j <= k; ++j) {
-      // x -= z is deferred pairwise: step j stores z and leaves x, step j+1
-      // applies x = (x - z_j) - z_{j+1} in registers -- the same two roundings
-      // as the reference's two statements, one x read+write fewer.
-      if (j % 2 == 0 && j < k) {
-        sys->ew(EW_MRR_NOX, eta[j], zeta[j], {AY(0), AR(1), Z, AR(0), -1, -1}, 0);
+    // Step j (v3/gpu/kskipmrr.py:64-71, 88-95): Ay0 = eta Ay0 + zeta Ar1;
+    // z = eta z - zeta Ar0; Ar0 -= Ay0; x -= z; Ar1 = A Ar0. All k+1 (zeta,
+    // eta) pairs are known here, so step j+1's vector update runs in the
+    // epilogue of step j's SpMV (EPI_STEP_MRR_*): Ar1 is never stored.
+    auto ew_step = [&](int j) {
+      const int kind = step_kind(j);
+      if (kind == 0) {
+        sys->ew(EW_MRR_NOX, eta[j], zeta[j], {AY(0), AR(1), Z, r0, -1, -1}, 0);
       } else {
-        sys->ew(j % 2 == 1 ? EW_MRR_X2 : EW_MRR, eta[j], zeta[j],
-                {AY(0), AR(1), Z, AR(0), xsrc, cur}, 0);
+        sys->ew(kind == 1 ? EW_MRR_X2 : EW_MRR, eta[j], zeta[j],
+                {AY(0), AR(1), Z, r0, xsrc, cur}, 0);
         xsrc = cur;
       }
-      if (j < k)
-        sys->spmv(EPI_NONE, AR(0), -1, AR(1), -1, -1, -1, 0);
-      else
-        head();
+    };
+    ew_step(0);
+    for (int j = 1; j <= k; ++j) {
+      if (sys->fuse_steps) {
+        const int kind = step_kind(j);
+        StepOps st;
+        st.u1 = AY(0);
+        st.u2 = Z;
+        if (kind != 0) {
+          st.us = xsrc;
+          st.ud = cur;
+        }
+        st.c0 = eta[j];
+        st.c1 = zeta[j];
+        const SpmvEpi e = kind == 0 ? EPI_STEP_MRR_NOX
+                                    : kind == 1 ? EPI_STEP_MRR_X2 : EPI_STEP_MRR_X;
+        sys->spmv(e, r0, -1, r_alt, -1, -1, -1, 0, &st);
+        if (kind != 0) xsrc = cur;
+        std::swap(r0, r_alt);
+      } else {
+        sys->spmv(EPI_NONE, r0, -1, AR(1), -1, -1, -1, 0);
+        ew_step(j);
+      }
     }
+    head();
     i += k + 1;
     index += 1;
     set_nosl(index, i);
@@ -880,22 +947,26 @@ class KskipMrrSession : public Base {
 // ------------------------------------------------------------- k-skip CG
 // v3/gpu/kskipcg.py:9-92 (oracle v3/cpu/kskipcg.py:8-87)
 class KskipCgSession : public Base {
-  enum { X, B, FIXED };
+  // Ap[0] lives in one of two buffers, p0 / p_alt (see KskipMrrSession).
+  enum { X, B, PALT, FIXED };
+  int p0 = 0, p_alt = PALT;
   int AR(int j) const { return FIXED + j; }
   int AP(int j) const { return FIXED + (k + 2) + j; }
   static constexpr int kHead = 6;
   int gram_slots() const { return kHead + 7 * k; }
-  void head() { sys->spmv(EPI_HEAD_KCG, AP(0), -1, AP(1), -1, AR(0), -1, 0); }
+  void head() { sys->spmv(EPI_HEAD_KCG, p0, -1, AP(1), -1, AR(0), -1, 0); }
 
  public:
   void begin(const double* const* b, const double* const* x0) override {
     k = prm.k;
     KR_REQUIRE(k >= 0 && gram_slots() <= kMaxSlots, "k out of range");
     sys->alloc_vectors(FIXED + (k + 2) + (k + 3));
+    p0 = AP(0);
+    p_alt = PALT;
     load_bx(B, X, b, x0);
     sys->spmv(EPI_BMINUS, X, -1, AR(0), -1, -1, B, 0);  // Ar[0] = b - A x
     sys->reduce(1);
-    sys->copy_own(AP(0), AR(0));  // Ap[0] = Ar[0]
+    sys->copy_own(p0, AR(0));  // Ap[0] = Ar[0]
     i = 0;
     index = 0;
     set_nosl(0, 0);
@@ -936,13 +1007,24 @@ class KskipCgSession : public Base {
     // f[2k+3] = <Ap[k+1], Ap[k+2]> with Ap[k+2] never computed: 0.
     std::vector<double> al(k + 1), be(k + 1);
     kskipcg_recurrence(k, a.data(), f.data(), c.data(), al.data(), be.data());
-    for (int j = 0; j <= k; ++j) {
-      sys->ew(EW_KCG, al[j], be[j], {X, AP(0), AR(0), AP(1), -1, -1}, 0);
-      if (j < k)
-        sys->spmv(EPI_NONE, AP(0), -1, AP(1), -1, -1, -1, 0);
-      else
-        head();
+    // Step j (v3/gpu/kskipcg.py:55-60, 71-76); as in k-skip MrR, step j+1's
+    // vector update runs in the epilogue of step j's SpMV (EPI_STEP_KCG).
+    sys->ew(EW_KCG, al[0], be[0], {X, p0, AR(0), AP(1), -1, -1}, 0);
+    for (int j = 1; j <= k; ++j) {
+      if (sys->fuse_steps) {
+        StepOps st;
+        st.u1 = X;
+        st.u2 = AR(0);
+        st.c0 = al[j];
+        st.c1 = be[j];
+        sys->spmv(EPI_STEP_KCG, p0, -1, p_alt, -1, -1, -1, 0, &st);
+        std::swap(p0, p_alt);
+      } else {
+        sys->spmv(EPI_NONE, p0, -1, AP(1), -1, -1, -1, 0);
+        sys->ew(EW_KCG, al[j], be[j], {X, p0, AR(0), AP(1), -1, -1}, 0);
+      }
     }
+    head();
     i += k + 1;
     index += 1;
     set_nosl(index, i);

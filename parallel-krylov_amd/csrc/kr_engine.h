@@ -98,6 +98,13 @@ struct Shard {
 
 class Session;
 
+// Operands of a fused k-skip step (SpmvEpi EPI_STEP_*): vector ids of the
+// in/out vectors u1, u2, the x source/destination, and the step's scalars.
+struct StepOps {
+  int u1 = -1, u2 = -1, us = -1, ud = -1;
+  double c0 = 0, c1 = 0;
+};
+
 // Exchange plan of global shard `me`: the rows it receives from / sends to
 // every other shard, as contiguous global ranges (pure host arithmetic).
 void plan_halo(int P, const int64_t* part, const int64_t* need_lo, const int64_t* need_hi,
@@ -112,6 +119,8 @@ struct System {
   bool finalized = false;
   bool profile = false;
   bool overlap = true;              // split SpMV: interior rows || halo exchange
+  bool fuse_steps = true;           // k-skip steps fused into the SpMV epilogue
+  int epi_late = 0;                 // SpmvArgs::epi_late (A/B knob)
   std::unique_ptr<Session> session;
 
   ~System();
@@ -125,7 +134,8 @@ struct System {
   // The same exchange on the shards' comm streams, ordered after ev_in and
   // signalling ev_out (overlapped path).
   void halo_async(int id1, int id2);
-  void spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int b, int slot0);
+  void spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int b, int slot0,
+            const StepOps* st = nullptr);
   void ew(EwOp op, double c0, double c1, std::array<int, 6> ids, int slot0);
   // Device->host of the summed slots [0, nslots): the one host sync point.
   std::vector<double> reduce(int nslots);

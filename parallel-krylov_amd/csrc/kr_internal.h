@@ -55,6 +55,14 @@ enum SpmvEpi : int {
   EPI_DUAL_NONE,  // y1 = A x1, y2 = A x2
   EPI_DUAL_MRR,   // 7 products, see kernels
   EPI_DUAL_KCG,   // 7 products, see kernels
+  // Fused k-skip inner steps: y = A x is consumed in the epilogue by the
+  // NEXT vector step (its scalars are known from the Gram sync), and only the
+  // step's outputs are stored. y1 receives the step's new input vector (a
+  // different buffer than x1: other rows still gather x1).
+  EPI_STEP_MRR_NOX,  // t=Ax; u1=c0*u1+c1*t; u2=c0*u2-c1*x; y1=x-u1          (u1=Ay0 u2=z)
+  EPI_STEP_MRR_X2,   //   ... and ud = (us - u2_old) - u2_new (deferred x -= z, two steps)
+  EPI_STEP_MRR_X,    //   ... and ud = us - u2_new
+  EPI_STEP_KCG,      // t=Ax; u1+=c0*x; u2-=c0*t; y1=u2+c1*x                 (u1=x u2=Ar0, x=Ap0)
 };
 int spmv_products(SpmvEpi epi);
 
@@ -84,6 +92,13 @@ struct SpmvArgs {
   const int32_t* moff = nullptr;
   int nm = 0;
   int mw = 0;
+  // Fused-step operands (EPI_STEP_*), own rows: in/out u1, u2, x source/dest.
+  double* u1 = nullptr;
+  double* u2 = nullptr;
+  const double* us = nullptr;
+  double* ud = nullptr;
+  double c0 = 0, c1 = 0;
+  int epi_late = 0;  // 1: load own-row epilogue operands at the row end (A/B, KR_EPI_LATE)
 };
 // Mean row length from which the product-then-sum SpMV is used.
 constexpr double kLongRow = 12.0;

@@ -15,969 +15,26 @@
 
 #include "kr_hash.h"
 #include "kr_internal.h"
+#include "kr_spmv.h"
 
 namespace kr {
 
+// SpMV kernels are instantiated per epilogue in kr_spmv_inst.hip.
+extern template void spmv_launch_epi<EPI_NONE>(const SpmvArgs&, int, hipStream_t);
+extern template void spmv_launch_epi<EPI_BMINUS>(const SpmvArgs&, int, hipStream_t);
+extern template void spmv_launch_epi<EPI_XY>(const SpmvArgs&, int, hipStream_t);
+extern template void spmv_launch_epi<EPI_HEAD_MRR>(const SpmvArgs&, int, hipStream_t);
+extern template void spmv_launch_epi<EPI_HEAD_KCG>(const SpmvArgs&, int, hipStream_t);
+extern template void spmv_launch_epi<EPI_MRR_LOOP>(const SpmvArgs&, int, hipStream_t);
+extern template void spmv_launch_epi<EPI_DUAL_NONE>(const SpmvArgs&, int, hipStream_t);
+extern template void spmv_launch_epi<EPI_DUAL_MRR>(const SpmvArgs&, int, hipStream_t);
+extern template void spmv_launch_epi<EPI_DUAL_KCG>(const SpmvArgs&, int, hipStream_t);
+extern template void spmv_launch_epi<EPI_STEP_MRR_NOX>(const SpmvArgs&, int, hipStream_t);
+extern template void spmv_launch_epi<EPI_STEP_MRR_X2>(const SpmvArgs&, int, hipStream_t);
+extern template void spmv_launch_epi<EPI_STEP_MRR_X>(const SpmvArgs&, int, hipStream_t);
+extern template void spmv_launch_epi<EPI_STEP_KCG>(const SpmvArgs&, int, hipStream_t);
+
 namespace {
-
-// ---------------------------------------------------------------------------
-// Block-level deterministic reduction of NP per-thread accumulators into
-// partials[p * grid + blockIdx.x].
-// ---------------------------------------------------------------------------
-template <int NP>
-__device__ __forceinline__ void block_reduce_store(double (&acc)[NP > 0 ? NP : 1],
-                                                   double* partials, int grid,
-                                                   double* s_red /* NP*4 */,
-                                                   int accumulate = 0) {
-  if constexpr (NP > 0) {
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      double v = acc[p];
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-      if (lane == 0) s_red[p * 4 + wave] = v;
-    }
-    __syncthreads();
-    if (threadIdx.x < NP) {
-      const double* r = s_red + threadIdx.x * 4;
-      double t = r[0];
-      t = t + r[1];
-      t = t + r[2];
-      t = t + r[3];
-      double* dst = partials + (int64_t)threadIdx.x * grid + blockIdx.x;
-      *dst = accumulate ? *dst + t : t;  // accumulate: a later launch of the same SpMV
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// SpMV epilogue product tables.
-// ---------------------------------------------------------------------------
-template <int EPI>
-struct EpiTraits;
-template <>
-struct EpiTraits<EPI_NONE> {
-  static constexpr int NP = 0, NV = 1;
-  static constexpr bool kX = false, kX2 = false, kE = false;
-};
-template <>
-struct EpiTraits<EPI_BMINUS> {
-  static constexpr int NP = 1, NV = 1;
-  static constexpr bool kX = false, kX2 = false, kE = false;
-};
-template <>
-struct EpiTraits<EPI_XY> {
-  static constexpr int NP = 3, NV = 1;
-  static constexpr bool kX = true, kX2 = false, kE = false;
-};
-template <>
-struct EpiTraits<EPI_HEAD_MRR> {
-  static constexpr int NP = 5, NV = 1;
-  static constexpr bool kX = true, kX2 = false, kE = true;
-};
-template <>
-struct EpiTraits<EPI_HEAD_KCG> {
-  static constexpr int NP = 6, NV = 1;
-  static constexpr bool kX = true, kX2 = false, kE = true;
-};
-template <>
-struct EpiTraits<EPI_MRR_LOOP> {
-  static constexpr int NP = 3, NV = 1;
-  static constexpr bool kX = true, kX2 = false, kE = true;
-};
-template <>
-struct EpiTraits<EPI_DUAL_NONE> {
-  static constexpr int NP = 0, NV = 2;
-  static constexpr bool kX = false, kX2 = false, kE = false;
-};
-template <>
-struct EpiTraits<EPI_DUAL_MRR> {
-  static constexpr int NP = 7, NV = 2;
-  static constexpr bool kX = true, kX2 = true, kE = false;
-};
-template <>
-struct EpiTraits<EPI_DUAL_KCG> {
-  static constexpr int NP = 7, NV = 2;
-  static constexpr bool kX = true, kX2 = true, kE = false;
-};
-
-// Products of one row. x/x2: inputs at the row, y/y2: results, e: extra.
-template <int EPI>
-__device__ __forceinline__ void epi_products(double x, double x2, double y, double y2,
-                                             double e,
-                                             double (&acc)[EpiTraits<EPI>::NP > 0
-                                                               ? EpiTraits<EPI>::NP
-                                                               : 1]) {
-  if constexpr (EPI == EPI_BMINUS) {
-    acc[0] += y * y;
-  } else if constexpr (EPI == EPI_XY) {
-    acc[0] += x * x;
-    acc[1] += x * y;
-    acc[2] += y * y;
-  } else if constexpr (EPI == EPI_HEAD_MRR) {  // x=Ar0 y=Ar1 e=Ay0
-    acc[0] += x * x;                           // alpha[0]
-    acc[1] += x * y;                           // alpha[1]
-    acc[2] += y * y;                           // alpha[2]
-    acc[3] += e * y;                           // beta[1]
-    acc[4] += e * e;                           // delta[0]
-  } else if constexpr (EPI == EPI_HEAD_KCG) {  // x=Ap0 y=Ap1 e=Ar0
-    acc[0] += e * e;                           // a[0]
-    acc[1] += x * x;                           // f[0]
-    acc[2] += x * y;                           // f[1]
-    acc[3] += y * y;                           // f[2]
-    acc[4] += e * x;                           // c[0]
-    acc[5] += e * y;                           // c[1]
-  } else if constexpr (EPI == EPI_MRR_LOOP) {  // x=r y=Ar e=y
-    acc[0] += x * x;                           // <r,r>
-    acc[1] += e * e;                           // mu
-    acc[2] += e * y;                           // nu
-  } else if constexpr (EPI == EPI_DUAL_MRR) {  // x=Ar[m+1] x2=Ay[m] y=Ar[m+2] y2=Ay[m+1]
-    acc[0] += x * y;                           // alpha[2m+3]
-    acc[1] += y * y;                           // alpha[2m+4]
-    acc[2] += y2 * y2;                         // delta[2m+2]
-    acc[3] += x2 * y2;                         // delta[2m+1]
-    acc[4] += y2 * y;                          // beta[2m+3]
-    acc[5] += x2 * x;                          // beta[2m+1]
-    acc[6] += y2 * x;                          // beta[2m+2]
-  } else if constexpr (EPI == EPI_DUAL_KCG) {  // x=Ar[j-1] x2=Ap[j] y=Ar[j] y2=Ap[j+1]
-    acc[0] += x * y;                           // a[2j-1]
-    acc[1] += y * y;                           // a[2j]
-    acc[2] += x2 * y2;                         // f[2j+1]
-    acc[3] += y2 * y2;                         // f[2j+2]
-    acc[4] += x * x2;                          // c[2j-1]
-    acc[5] += y * x2;                          // c[2j]
-    acc[6] += y * y2;                          // c[2j+1]
-  }
-}
-
-// ---------------------------------------------------------------------------
-// CSR SpMV, one lane per row, matrix entries staged through LDS.
-//   Row block = kBlock consecutive rows. Its nnz range is staged into LDS in
-//   windows of kWindow entries: every lane first issues all of its 16-byte
-//   loads (4 entries per slot, kSlots slots: vals as 2 x 16 B, cols as 16 B),
-//   then writes them to LDS, so a wave has 3*kSlots loads in flight instead of
-//   a load/wait/store chain. Each lane then walks its own row inside the
-//   window in stored order, issuing up to kGather x-gathers before it adds
-//   them -- in order -- to its running sum (bitwise scipy csr_matvec).
-//   Grid-stride over row blocks; reductions accumulate per lane across row
-//   blocks and are reduced once per workgroup at the end.
-// ---------------------------------------------------------------------------
-typedef double dbl2v __attribute__((ext_vector_type(2)));
-typedef int int4v __attribute__((ext_vector_type(4)));
-constexpr int kSlots = kWindow / (4 * kBlock);
-// x gathers in flight per lane: 7 = one batch for 7-point rows (8 issued a
-// redundant 8th load per row; measured +1-2 %).
-constexpr int kGather = 7;
-static_assert(kSlots * 4 * kBlock == kWindow, "window must be a multiple of 4*kBlock");
-
-// Registers holding one staged window. Values move as one 16-byte double2 per
-// lane per slot and columns as one 16-byte int4, so consecutive lanes touch
-// consecutive 16-byte LDS slots (bank-conflict-free ds_write_b128) and every
-// wave-instruction reads 1 KiB of contiguous HBM.
-constexpr int kVSlots = kWindow / (2 * kBlock);
-constexpr int kCSlots = kWindow / (4 * kBlock);
-struct Stage {
-  dbl2v v[kVSlots];
-  int4v c[kCSlots];
-};
-
-template <bool VEC, bool NT = false, bool COLS = true>
-__device__ __forceinline__ void stage_load(Stage& st, const double* __restrict__ val,
-                                           const int32_t* __restrict__ col, int64_t ws,
-                                           int64_t bs, int64_t be, int tid) {
-#pragma unroll
-  for (int q = 0; q < kVSlots; ++q) {
-    const int64_t g0 = ws + (int64_t)(tid + q * kBlock) * 2;
-    if (VEC && g0 >= bs && g0 + 2 <= be) {
-      if constexpr (NT)
-        st.v[q] = __builtin_nontemporal_load(reinterpret_cast<const dbl2v*>(val + g0));
-      else
-        st.v[q] = *reinterpret_cast<const dbl2v*>(val + g0);
-    } else {
-      const bool ok0 = g0 >= bs && g0 < be, ok1 = g0 + 1 >= bs && g0 + 1 < be;
-      st.v[q] = dbl2v{ok0 ? val[g0] : 0.0, ok1 ? val[g0 + 1] : 0.0};
-    }
-  }
-  if constexpr (!COLS) return;
-#pragma unroll
-  for (int q = 0; q < kCSlots; ++q) {
-    const int64_t g0 = ws + (int64_t)(tid + q * kBlock) * 4;
-    if (VEC && g0 >= bs && g0 + 4 <= be) {
-      if constexpr (NT)
-        st.c[q] = __builtin_nontemporal_load(reinterpret_cast<const int4v*>(col + g0));
-      else
-        st.c[q] = *reinterpret_cast<const int4v*>(col + g0);
-    } else {
-      int tc[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int64_t g = g0 + u;
-        tc[u] = (g >= bs && g < be) ? col[g] : 0;
-      }
-      st.c[q] = int4v{tc[0], tc[1], tc[2], tc[3]};
-    }
-  }
-}
-
-template <bool COLS = true>
-__device__ __forceinline__ void stage_commit(const Stage& st, double* s_val, int32_t* s_col,
-                                             int tid) {
-#pragma unroll
-  for (int q = 0; q < kVSlots; ++q) reinterpret_cast<dbl2v*>(s_val)[tid + q * kBlock] = st.v[q];
-  if constexpr (COLS) {
-#pragma unroll
-    for (int q = 0; q < kCSlots; ++q)
-      reinterpret_cast<int4v*>(s_col)[tid + q * kBlock] = st.c[q];
-  }
-}
-
-// Offset-mask rows (SpmvArgs::mask): the row's columns are xrow + M[b] for
-// the set bits b of its mask, in increasing order (M ascending, columns
-// strictly increasing in the row), so the k-th stored entry uses the k-th set
-// bit. The lane's remaining mask carries across windows.
-template <int MW>
-struct MaskType {
-  using type = uint64_t;
-};
-template <>
-struct MaskType<8> {
-  using type = uint8_t;
-};
-template <>
-struct MaskType<16> {
-  using type = uint16_t;
-};
-template <>
-struct MaskType<32> {
-  using type = uint32_t;
-};
-
-template <int NV, int GATHER, typename W>
-__device__ __forceinline__ void row_window_mask(const double* s_val, const int32_t* s_M,
-                                                const double* __restrict__ x1,
-                                                const double* __restrict__ x2, int64_t xrow,
-                                                int js, int je, W& mrem, double& sum1,
-                                                double& sum2) {
-  for (int j = js; j < je; j += GATHER) {
-    double v[GATHER], p1[GATHER], p2[GATHER];
-#pragma unroll
-    for (int u = 0; u < GATHER; ++u) {
-      const bool ok = j + u < je;
-      v[u] = s_val[ok ? j + u : js];
-      int64_t c = xrow;
-      if (ok) {
-        c += s_M[sizeof(W) == 8 ? __builtin_ctzll((unsigned long long)mrem)
-                                : __builtin_ctz((unsigned)mrem)];
-        mrem &= mrem - 1;
-      }
-      p1[u] = x1[c];
-      if constexpr (NV == 2) p2[u] = x2[c];
-    }
-#pragma unroll
-    for (int u = 0; u < GATHER; ++u) {
-      if (j + u < je) {
-        sum1 = sum1 + v[u] * p1[u];
-        if constexpr (NV == 2) sum2 = sum2 + v[u] * p2[u];
-      }
-    }
-  }
-}
-
-// One lane's entries [js, je) of the staged window, in stored order.
-template <int NV, int GATHER = kGather>
-__device__ __forceinline__ void row_window(const double* s_val, const int32_t* s_col,
-                                           const double* __restrict__ x1,
-                                           const double* __restrict__ x2, int js, int je,
-                                           double& sum1, double& sum2) {
-  for (int j = js; j < je; j += GATHER) {
-    double v[GATHER], p1[GATHER], p2[GATHER];
-#pragma unroll
-    for (int u = 0; u < GATHER; ++u) {
-      const int jj = (j + u < je) ? j + u : js;
-      v[u] = s_val[jj];
-      const int c = s_col[jj];
-      p1[u] = x1[c];
-      if constexpr (NV == 2) p2[u] = x2[c];
-    }
-#pragma unroll
-    for (int u = 0; u < GATHER; ++u) {
-      if (j + u < je) {
-        sum1 = sum1 + v[u] * p1[u];
-        if constexpr (NV == 2) sum2 = sum2 + v[u] * p2[u];
-      }
-    }
-  }
-}
-
-// Software pipeline over a stream of LDS windows. A workgroup walks its row
-// blocks (256 rows each); a row block's entries are one or more 2048-entry
-// windows. While one window is multiplied out of LDS, the NEXT window is
-// already in flight in registers: the next window of the same row block, or
-// the first window of the next row block (whose nnz range was requested as
-// scalar loads one row block earlier). So a window waits on one memory round
-// trip, for short-row (Poisson: one window per row block) and long-row
-// (banded 27-63 nnz/row: 4-8 windows per row block) matrices alike.
-// Row-block schedule: a workgroup visits rb(j) for j = j0, j0 + jstep, ...
-// < jcount. XCD-aware: workgroups b and b+8 share an XCD (and its L2) under
-// the observed round-robin dispatch, so the workgroups with equal b % 8 work
-// on rows close together and the x entries that neighbouring row blocks
-// gather stay in one L2. Contiguous mode: each XCD sweeps one eighth of the
-// rows (neighbours +-1, +-n reused). Slab mode (S = the matrix's column reach
-// in row blocks): the rows are cut into "planes" of S row blocks and XCD q
-// owns the q-th eighth of every plane, visited plane after plane, so the x
-// rows one plane away (+-n^2 of a 3-D stencil) are still in its L2 when the
-// next plane reads them. With a sub-slab width (slab_sub), XCD q's eighth is
-// cut further into sub-slabs that are swept plane after plane one at a time,
-// which shortens the reuse distance to what its 4 MB L2 holds. Placement only
-// changes speed: every row block is visited exactly once.
-struct RowSched {
-  int64_t j0, jstep, jcount, base = 0, off = 0, w = 0, S = 0, sub = 0, full = 0, rem = 0;
-  int nc = 0;
-  // row blocks of sub-slab c (width wc, all planes; the last plane is partial)
-  __device__ int64_t chunk_count(int c, int64_t wc) const {
-    return full * wc + min(wc, max((int64_t)0, rem - off - c * sub));
-  }
-  __device__ void init(int64_t nrb, int64_t slab, int64_t slab_sub, bool xcd) {
-    if (xcd && (gridDim.x & 7) == 0) {
-      const int64_t q = blockIdx.x & 7;
-      j0 = blockIdx.x >> 3;
-      jstep = gridDim.x >> 3;
-      if (slab >= 8) {
-        S = slab;
-        off = S * q / 8;
-        w = S * (q + 1) / 8 - off;
-        const int64_t planes = (nrb + S - 1) / S;
-        full = planes - 1;
-        rem = nrb - full * S;
-        sub = slab_sub > 0 ? min(slab_sub, w) : w;
-        nc = (int)((w + sub - 1) / sub);
-        jcount = 0;
-        for (int c = 0; c < nc; ++c) jcount += chunk_count(c, min(sub, w - c * sub));
-      } else {
-        const int64_t chunk = (nrb + 7) / 8;
-        base = q * chunk;
-        jcount = max((int64_t)0, min(nrb, base + chunk) - base);
-      }
-    } else {
-      j0 = blockIdx.x;
-      jstep = gridDim.x;
-      jcount = nrb;
-    }
-  }
-  __device__ int64_t rb(int64_t v) const {
-    if (!w) return base + v;
-    // sub-slab after sub-slab; inside one, plane after plane
-    for (int c = 0; c < nc; ++c) {
-      const int64_t wc = min(sub, w - c * sub);
-      const int64_t cnt = chunk_count(c, wc);
-      if (v < cnt) return (v / wc) * S + off + c * sub + v % wc;
-      v -= cnt;
-    }
-    return -1;  // unreachable: v < jcount
-  }
-};
-
-template <typename RP, int EPI, bool VEC, int GATHER = kGather, bool XCD = true, bool NT = false,
-          int MW = 0>
-__global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
-  using T = EpiTraits<EPI>;
-  constexpr int NP = T::NP;
-  constexpr int NV = T::NV;
-  constexpr bool COLS = MW == 0;  // else: offset masks, no column stream
-  using MT = typename MaskType<MW>::type;
-  using W = typename std::conditional<(MW > 32), uint64_t, uint32_t>::type;
-  __shared__ __attribute__((aligned(16))) double s_val[kWindow];
-  __shared__ __attribute__((aligned(16))) int32_t s_col[COLS ? kWindow : 4];
-  __shared__ int32_t s_M[COLS ? 1 : 64];
-  const MT* __restrict__ mask = static_cast<const MT*>(a.mask);
-  if constexpr (!COLS) {
-    if ((int)threadIdx.x < a.nm) s_M[threadIdx.x] = a.moff[threadIdx.x];  // seen after 1st barrier
-  }
-  __shared__ int32_t s_rp[kBlock + 1];  // row pointers relative to the block start
-  __shared__ double s_red[(NP > 0 ? NP : 1) * 4];
-
-  const RP* __restrict__ rowptr = static_cast<const RP*>(a.rowptr);
-  const double* __restrict__ val = a.val;
-  const int32_t* __restrict__ col = a.col;
-  const double* __restrict__ x1 = a.x1;
-  const double* __restrict__ x2 = a.x2;
-  const int tid = threadIdx.x;
-
-  double acc[NP > 0 ? NP : 1];
-#pragma unroll
-  for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;
-
-  const int64_t nrb = (a.n + kBlock - 1) / kBlock;
-  RowSched sched;
-  sched.init(nrb, a.slab, a.slab_sub, XCD);
-  int64_t j = sched.j0;
-  const int64_t jstep = sched.jstep, jcount = sched.jcount;
-  auto rb_of = [&](int64_t v) { return sched.rb(v); };
-  if (j >= jcount) {
-    block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
-    return;
-  }
-  auto block_rows = [&](int64_t b) { return (int)min((int64_t)kBlock, a.n - b * kBlock); };
-  auto wstart = [](int64_t e) { return VEC ? (e & ~(int64_t)3) : e; };
-
-  // current row block
-  int64_t r0 = rb_of(j) * kBlock;
-  int nr = block_rows(rb_of(j));
-  int64_t bs = (int64_t)rowptr[r0];
-  int64_t be = (int64_t)rowptr[r0 + nr];
-  int64_t my_end = tid < nr ? (int64_t)rowptr[r0 + tid + 1] : 0;
-  W my_mask = 0, my_mask_n = 0, mrem = 0;
-  if constexpr (!COLS) my_mask = tid < nr ? (W)mask[r0 + tid] : 0;
-  // next row block: nnz range as scalars (issued now, used one block later)
-  int64_t bsn = 0, ben = 0;
-  if (j + jstep < jcount) {
-    const int64_t rbn = rb_of(j + jstep);
-    const int64_t r0n = rbn * kBlock;
-    bsn = (int64_t)rowptr[r0n];
-    ben = (int64_t)rowptr[r0n + block_rows(rbn)];
-  }
-  Stage st;  // the window in flight
-  int64_t ws = wstart(bs);
-  stage_load<VEC, NT, COLS>(st, val, col, ws, bs, be, tid);
-  bool first_window = true;
-  int rs = 0, re = 0;
-  double sum1 = 0.0, sum2 = 0.0;
-  // the next row block's state, loaded when its first window is issued
-  int64_t r0n = 0, my_end_n = 0, bsnn = 0, bennn = 0;
-  int nrn = 0;
-  (void)bennn;
-
-  for (;;) {
-    if (first_window) {
-      if (tid < nr) s_rp[tid + 1] = (int32_t)(my_end - bs);
-      if (tid == 0) s_rp[0] = 0;
-    }
-    stage_commit<COLS>(st, s_val, s_col, tid);
-    __syncthreads();
-    const bool active = tid < nr;
-    if (first_window) {
-      rs = active ? s_rp[tid] : 0;
-      re = active ? s_rp[tid + 1] : 0;
-      mrem = my_mask;
-    }
-    // issue the next window before working on this one
-    const bool last_window = ws + kWindow >= be;
-    const int64_t j_next = j + jstep;
-    const bool has_next = j_next < jcount;
-    const int64_t rb_next = has_next ? rb_of(j_next) : 0;
-    if (!last_window) {
-      stage_load<VEC, NT, COLS>(st, val, col, ws + kWindow, bs, be, tid);
-    } else if (has_next) {
-      r0n = rb_next * kBlock;
-      nrn = block_rows(rb_next);
-      my_end_n = tid < nrn ? (int64_t)rowptr[r0n + tid + 1] : 0;
-      if constexpr (!COLS) my_mask_n = tid < nrn ? (W)mask[r0n + tid] : 0;
-      stage_load<VEC, NT, COLS>(st, val, col, wstart(bsn), bsn, ben, tid);
-      if (j_next + jstep < jcount) {
-        const int64_t rb_nn = rb_of(j_next + jstep);
-        const int64_t r0nn = rb_nn * kBlock;
-        bsnn = (int64_t)rowptr[r0nn];
-        bennn = (int64_t)rowptr[r0nn + block_rows(rb_nn)];
-      }
-    }
-    // this lane's entries inside the window (window offsets)
-    if (active) {
-      const int64_t off = bs - ws;
-      const int js = (int)max((int64_t)rs + off, (int64_t)0);
-      const int je = (int)min((int64_t)re + off, (int64_t)kWindow);
-      if constexpr (COLS)
-        row_window<NV, GATHER>(s_val, s_col, x1, x2, js, je, sum1, sum2);
-      else
-        row_window_mask<NV, GATHER>(s_val, s_M, x1, x2, a.xoff + r0 + tid, js, je, mrem, sum1,
-                                    sum2);
-    }
-    if (!last_window) {
-      __syncthreads();  // LDS is rewritten by the next window
-      ws += kWindow;
-      first_window = false;
-      continue;
-    }
-    if (active) {
-      const int64_t row = r0 + tid;
-      double y1 = sum1;
-      if constexpr (EPI == EPI_BMINUS) y1 = a.b[row] - sum1;
-      a.y1[row] = y1;
-      if constexpr (NV == 2) a.y2[row] = sum2;
-      if constexpr (NP > 0) {
-        const double xv = T::kX ? x1[a.xoff + row] : 0.0;
-        const double x2v = T::kX2 ? x2[a.xoff + row] : 0.0;
-        const double ev = T::kE ? a.e[row] : 0.0;
-        epi_products<EPI>(xv, x2v, y1, sum2, ev, acc);
-      }
-    }
-    if (!has_next) break;
-    __syncthreads();  // LDS and s_rp are rewritten by the next row block
-    j = j_next;
-    r0 = r0n;
-    nr = nrn;
-    bs = bsn;
-    be = ben;
-    bsn = bsnn;
-    ben = bennn;
-    my_end = my_end_n;
-    my_mask = my_mask_n;
-    ws = wstart(bs);
-    first_window = true;
-    sum1 = 0.0;
-    sum2 = 0.0;
-  }
-  __syncthreads();
-  block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
-}
-
-// Product-then-sum SpMV for long rows (variant 8; chosen by the host when
-// nnz/row is large). Each window's entries are multiplied entry-parallel:
-// lane t owns entries 2(t + 256q) + {0,1} (a 16-byte value load and an 8-byte
-// column load per slot), gathers x for all of them at once, and writes the
-// products fl(v * x) to LDS. Then each lane adds its own row's products in
-// stored order, carrying the running sum across windows -- the same
-// operations in the same order as scipy, so the result is still bitwise.
-// Every lane gathers in every window, however few rows the window holds.
-constexpr int kPSlots = kWindow / (2 * kBlock);
-typedef int int2v __attribute__((ext_vector_type(2)));
-
-struct PStage {
-  dbl2v v[kPSlots];
-  int2v c[kPSlots];
-};
-
-template <bool VEC>
-__device__ __forceinline__ void pstage_load(PStage& st, const double* __restrict__ val,
-                                            const int32_t* __restrict__ col, int64_t ws,
-                                            int64_t bs, int64_t be, int tid) {
-#pragma unroll
-  for (int q = 0; q < kPSlots; ++q) {
-    const int64_t g0 = ws + (int64_t)(tid + q * kBlock) * 2;
-    if (VEC && g0 >= bs && g0 + 2 <= be) {
-      st.v[q] = *reinterpret_cast<const dbl2v*>(val + g0);
-      st.c[q] = *reinterpret_cast<const int2v*>(col + g0);
-    } else {
-      const bool ok0 = g0 >= bs && g0 < be, ok1 = g0 + 1 >= bs && g0 + 1 < be;
-      st.v[q] = dbl2v{ok0 ? val[g0] : 0.0, ok1 ? val[g0 + 1] : 0.0};
-      st.c[q] = int2v{ok0 ? col[g0] : -1, ok1 ? col[g0 + 1] : -1};
-    }
-  }
-}
-
-template <int NV>
-__device__ __forceinline__ void pstage_products(const PStage& st, const double* __restrict__ x1,
-                                                const double* __restrict__ x2, double* s_p1,
-                                                double* s_p2, int tid) {
-  double g1[2 * kPSlots], g2[2 * kPSlots];
-#pragma unroll
-  for (int q = 0; q < kPSlots; ++q) {
-    const int c0 = st.c[q].x, c1 = st.c[q].y;
-    g1[2 * q] = c0 >= 0 ? x1[c0] : 0.0;
-    g1[2 * q + 1] = c1 >= 0 ? x1[c1] : 0.0;
-    if constexpr (NV == 2) {
-      g2[2 * q] = c0 >= 0 ? x2[c0] : 0.0;
-      g2[2 * q + 1] = c1 >= 0 ? x2[c1] : 0.0;
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < kPSlots; ++q) {
-    reinterpret_cast<dbl2v*>(s_p1)[tid + q * kBlock] =
-        dbl2v{st.v[q].x * g1[2 * q], st.v[q].y * g1[2 * q + 1]};
-    if constexpr (NV == 2)
-      reinterpret_cast<dbl2v*>(s_p2)[tid + q * kBlock] =
-          dbl2v{st.v[q].x * g2[2 * q], st.v[q].y * g2[2 * q + 1]};
-  }
-}
-
-template <typename RP, int EPI, bool VEC>
-__global__ __launch_bounds__(kBlock) void spmv_kernel_prod(SpmvArgs a) {
-  using T = EpiTraits<EPI>;
-  constexpr int NP = T::NP;
-  constexpr int NV = T::NV;
-  __shared__ __attribute__((aligned(16))) double s_p1[kWindow];
-  __shared__ __attribute__((aligned(16))) double s_p2[NV == 2 ? kWindow : 2];
-  __shared__ int32_t s_rp[kBlock + 1];
-  __shared__ double s_red[(NP > 0 ? NP : 1) * 4];
-
-  const RP* __restrict__ rowptr = static_cast<const RP*>(a.rowptr);
-  const double* __restrict__ val = a.val;
-  const int32_t* __restrict__ col = a.col;
-  const double* __restrict__ x1 = a.x1;
-  const double* __restrict__ x2 = a.x2;
-  const int tid = threadIdx.x;
-
-  double acc[NP > 0 ? NP : 1];
-#pragma unroll
-  for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;
-
-  const int64_t nrb = (a.n + kBlock - 1) / kBlock;
-  RowSched sched;  // as spmv_kernel
-  sched.init(nrb, a.slab, a.slab_sub, true);
-  int64_t j = sched.j0;
-  const int64_t jstep = sched.jstep, jcount = sched.jcount;
-  auto rb_of = [&](int64_t v) { return sched.rb(v); };
-  if (j >= jcount) {
-    block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
-    return;
-  }
-  auto block_rows = [&](int64_t b) { return (int)min((int64_t)kBlock, a.n - b * kBlock); };
-  auto wstart = [](int64_t e) { return VEC ? (e & ~(int64_t)1) : e; };
-
-  int64_t r0 = rb_of(j) * kBlock;
-  int nr = block_rows(rb_of(j));
-  int64_t bs = (int64_t)rowptr[r0];
-  int64_t be = (int64_t)rowptr[r0 + nr];
-  int64_t my_end = tid < nr ? (int64_t)rowptr[r0 + tid + 1] : 0;
-  int64_t bsn = 0, ben = 0;
-  if (j + jstep < jcount) {
-    const int64_t rbn = rb_of(j + jstep);
-    const int64_t r0n = rbn * kBlock;
-    bsn = (int64_t)rowptr[r0n];
-    ben = (int64_t)rowptr[r0n + block_rows(rbn)];
-  }
-  PStage st;
-  int64_t ws = wstart(bs);
-  pstage_load<VEC>(st, val, col, ws, bs, be, tid);
-  bool first_window = true;
-  int rs = 0, re = 0;
-  double sum1 = 0.0, sum2 = 0.0;
-  int64_t r0n = 0, my_end_n = 0, bsnn = 0, bennn = 0;
-  int nrn = 0;
-
-  for (;;) {
-    if (first_window) {
-      if (tid < nr) s_rp[tid + 1] = (int32_t)(my_end - bs);
-      if (tid == 0) s_rp[0] = 0;
-    }
-    pstage_products<NV>(st, x1, x2, s_p1, s_p2, tid);
-    __syncthreads();
-    const bool active = tid < nr;
-    if (first_window) {
-      rs = active ? s_rp[tid] : 0;
-      re = active ? s_rp[tid + 1] : 0;
-    }
-    const bool last_window = ws + kWindow >= be;
-    const int64_t j_next = j + jstep;
-    const bool has_next = j_next < jcount;
-    const int64_t rb_next = has_next ? rb_of(j_next) : 0;
-    if (!last_window) {
-      pstage_load<VEC>(st, val, col, ws + kWindow, bs, be, tid);
-    } else if (has_next) {
-      r0n = rb_next * kBlock;
-      nrn = block_rows(rb_next);
-      my_end_n = tid < nrn ? (int64_t)rowptr[r0n + tid + 1] : 0;
-      pstage_load<VEC>(st, val, col, wstart(bsn), bsn, ben, tid);
-      if (j_next + jstep < jcount) {
-        const int64_t rb_nn = rb_of(j_next + jstep);
-        const int64_t r0nn = rb_nn * kBlock;
-        bsnn = (int64_t)rowptr[r0nn];
-        bennn = (int64_t)rowptr[r0nn + block_rows(rb_nn)];
-      }
-    }
-    if (active) {
-      const int64_t off = bs - ws;
-      const int js = (int)max((int64_t)rs + off, (int64_t)0);
-      const int je = (int)min((int64_t)re + off, (int64_t)kWindow);
-      for (int j = js; j < je; ++j) {
-        sum1 = sum1 + s_p1[j];
-        if constexpr (NV == 2) sum2 = sum2 + s_p2[j];
-      }
-    }
-    if (!last_window) {
-      __syncthreads();
-      ws += kWindow;
-      first_window = false;
-      continue;
-    }
-    if (active) {
-      const int64_t row = r0 + tid;
-      double y1 = sum1;
-      if constexpr (EPI == EPI_BMINUS) y1 = a.b[row] - sum1;
-      a.y1[row] = y1;
-      if constexpr (NV == 2) a.y2[row] = sum2;
-      if constexpr (NP > 0) {
-        const double xv = T::kX ? x1[a.xoff + row] : 0.0;
-        const double x2v = T::kX2 ? x2[a.xoff + row] : 0.0;
-        const double ev = T::kE ? a.e[row] : 0.0;
-        epi_products<EPI>(xv, x2v, y1, sum2, ev, acc);
-      }
-    }
-    if (!has_next) break;
-    __syncthreads();
-    j = j_next;
-    r0 = r0n;
-    nr = nrn;
-    bs = bsn;
-    be = ben;
-    bsn = bsnn;
-    ben = bennn;
-    my_end = my_end_n;
-    ws = wstart(bs);
-    first_window = true;
-    sum1 = 0.0;
-    sum2 = 0.0;
-  }
-  __syncthreads();
-  block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
-}
-
-// Variant 1: no cross-row-block prefetch (lower VGPR count, higher occupancy).
-template <typename RP, int EPI, bool VEC>
-__global__ __launch_bounds__(kBlock) void spmv_kernel_simple(SpmvArgs a) {
-  using T = EpiTraits<EPI>;
-  constexpr int NP = T::NP;
-  constexpr int NV = T::NV;
-  __shared__ __attribute__((aligned(16))) double s_val[kWindow];
-  __shared__ __attribute__((aligned(16))) int32_t s_col[kWindow];
-  __shared__ int32_t s_rp[kBlock + 1];  // row pointers relative to the block start
-  __shared__ double s_red[(NP > 0 ? NP : 1) * 4];
-
-  const RP* __restrict__ rowptr = static_cast<const RP*>(a.rowptr);
-  const double* __restrict__ val = a.val;
-  const int32_t* __restrict__ col = a.col;
-  const double* __restrict__ x1 = a.x1;
-  const double* __restrict__ x2 = a.x2;
-  const int tid = threadIdx.x;
-
-  double acc[NP > 0 ? NP : 1];
-#pragma unroll
-  for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;
-
-  const int64_t nrb = (a.n + kBlock - 1) / kBlock;
-  for (int64_t rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
-    const int64_t r0 = rb * kBlock;
-    const int nr = (int)min((int64_t)kBlock, a.n - r0);
-    const int64_t bs = (int64_t)rowptr[r0];
-    const int64_t be = (int64_t)rowptr[r0 + nr];
-    if (tid < nr) s_rp[tid + 1] = (int32_t)((int64_t)rowptr[r0 + tid + 1] - bs);
-    if (tid == 0) s_rp[0] = 0;
-    __syncthreads();
-    const bool active = tid < nr;
-    const int rs = active ? s_rp[tid] : 0;
-    const int re = active ? s_rp[tid + 1] : 0;
-    double sum1 = 0.0, sum2 = 0.0;
-    // windows start 4-aligned so every slot is one 16-byte access
-    const int64_t w0 = VEC ? (bs & ~(int64_t)3) : bs;
-    for (int64_t ws = w0; ws < be; ws += kWindow) {
-      {
-        Stage st;
-        stage_load<VEC>(st, val, col, ws, bs, be, tid);
-        stage_commit(st, s_val, s_col, tid);
-      }
-      __syncthreads();
-      if (active) {
-        // this lane's entries inside the window, as window offsets
-        const int64_t off = bs - ws;  // window offset of the block's entry 0
-        const int js = (int)max((int64_t)rs + off, (int64_t)0);
-        const int je = (int)min((int64_t)re + off, (int64_t)kWindow);
-        for (int j = js; j < je; j += kGather) {
-          double v[kGather], p1[kGather], p2[kGather];
-#pragma unroll
-          for (int u = 0; u < kGather; ++u) {
-            const int jj = (j + u < je) ? j + u : js;
-            v[u] = s_val[jj];
-            const int c = s_col[jj];
-            p1[u] = x1[c];
-            if constexpr (NV == 2) p2[u] = x2[c];
-          }
-#pragma unroll
-          for (int u = 0; u < kGather; ++u) {
-            if (j + u < je) {
-              sum1 = sum1 + v[u] * p1[u];
-              if constexpr (NV == 2) sum2 = sum2 + v[u] * p2[u];
-            }
-          }
-        }
-      }
-      __syncthreads();
-    }
-    if (active) {
-      const int64_t row = r0 + tid;
-      double y1 = sum1;
-      if constexpr (EPI == EPI_BMINUS) y1 = a.b[row] - sum1;
-      a.y1[row] = y1;
-      if constexpr (NV == 2) a.y2[row] = sum2;
-      if constexpr (NP > 0) {
-        const double xv = T::kX ? x1[a.xoff + row] : 0.0;
-        const double x2v = T::kX2 ? x2[a.xoff + row] : 0.0;
-        const double ev = T::kE ? a.e[row] : 0.0;
-        epi_products<EPI>(xv, x2v, y1, sum2, ev, acc);
-      }
-    }
-    __syncthreads();  // s_rp is rewritten by the next row block
-  }
-  block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
-}
-
-// Variant 2: wave-independent. Each wave owns 64-row blocks and a private
-// LDS window; staging and the row walk need only wave-local ordering (an
-// s_waitcnt on the LDS counter), never a workgroup barrier, so the four waves
-// of a workgroup stream independently.
-constexpr int kWaveRows = 64;
-constexpr int kWaveWindow = 512;  // entries per wave window (2 slots of 4 per lane)
-constexpr int kWaveSlots = kWaveWindow / (4 * kWaveRows);
-static_assert(kWaveSlots * 4 * kWaveRows == kWaveWindow, "wave window layout");
-
-__device__ __forceinline__ void lds_fence() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
-
-template <typename RP, int EPI, bool VEC>
-__global__ __launch_bounds__(kBlock) void spmv_kernel_wave(SpmvArgs a) {
-  using T = EpiTraits<EPI>;
-  constexpr int NP = T::NP;
-  constexpr int NV = T::NV;
-  constexpr int kWaves = kBlock / 64;
-  __shared__ __attribute__((aligned(16))) double s_val_all[kWaves][kWaveWindow];
-  __shared__ __attribute__((aligned(16))) int32_t s_col_all[kWaves][kWaveWindow];
-  __shared__ double s_red[(NP > 0 ? NP : 1) * 4];
-
-  const RP* __restrict__ rowptr = static_cast<const RP*>(a.rowptr);
-  const double* __restrict__ val = a.val;
-  const int32_t* __restrict__ col = a.col;
-  const double* __restrict__ x1 = a.x1;
-  const double* __restrict__ x2 = a.x2;
-  const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  double* s_val = s_val_all[w];
-  int32_t* s_col = s_col_all[w];
-
-  double acc[NP > 0 ? NP : 1];
-#pragma unroll
-  for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;
-
-  const int64_t nwb = (a.n + kWaveRows - 1) / kWaveRows;
-  const int64_t gw = (int64_t)blockIdx.x * kWaves + w;
-  const int64_t nwaves = (int64_t)gridDim.x * kWaves;
-  for (int64_t wb = gw; wb < nwb; wb += nwaves) {
-    const int64_t r0 = wb * kWaveRows;
-    const int nr = (int)min((int64_t)kWaveRows, a.n - r0);
-    const int64_t bs = (int64_t)rowptr[r0];
-    const int64_t be = (int64_t)rowptr[r0 + nr];
-    const bool active = lane < nr;
-    const int64_t my_end = active ? (int64_t)rowptr[r0 + lane + 1] : be;
-    // row start = previous lane's end (lane 0: block start)
-    const int64_t my_beg = !active ? be : lane == 0 ? bs : (int64_t)rowptr[r0 + lane];
-    const int rs = (int)(my_beg - bs), re = (int)(my_end - bs);
-    double sum1 = 0.0, sum2 = 0.0;
-    const int64_t w0 = VEC ? (bs & ~(int64_t)3) : bs;
-    for (int64_t ws = w0; ws < be; ws += kWaveWindow) {
-      dbl2v lo[kWaveSlots], hi[kWaveSlots];
-      int4v c4[kWaveSlots];
-#pragma unroll
-      for (int q = 0; q < kWaveSlots; ++q) {
-        const int64_t g0 = ws + (int64_t)(lane + q * 64) * 4;
-        if (VEC && g0 >= bs && g0 + 4 <= be) {
-          lo[q] = *reinterpret_cast<const dbl2v*>(val + g0);
-          hi[q] = *reinterpret_cast<const dbl2v*>(val + g0 + 2);
-          c4[q] = *reinterpret_cast<const int4v*>(col + g0);
-        } else {
-          double tv[4];
-          int tc[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int64_t g = g0 + u;
-            const bool ok = g >= bs && g < be;
-            tv[u] = ok ? val[g] : 0.0;
-            tc[u] = ok ? col[g] : 0;
-          }
-          lo[q] = dbl2v{tv[0], tv[1]};
-          hi[q] = dbl2v{tv[2], tv[3]};
-          c4[q] = int4v{tc[0], tc[1], tc[2], tc[3]};
-        }
-      }
-      lds_fence();  // previous window fully read by every lane of the wave
-#pragma unroll
-      for (int q = 0; q < kWaveSlots; ++q) {
-        const int e0 = (lane + q * 64) * 4;
-        *reinterpret_cast<dbl2v*>(&s_val[e0]) = lo[q];
-        *reinterpret_cast<dbl2v*>(&s_val[e0 + 2]) = hi[q];
-        *reinterpret_cast<int4v*>(&s_col[e0]) = c4[q];
-      }
-      lds_fence();  // window visible to every lane of the wave
-      if (active) {
-        const int64_t off = bs - ws;
-        row_window<NV>(s_val, s_col, x1, x2, (int)max((int64_t)rs + off, (int64_t)0),
-                       (int)min((int64_t)re + off, (int64_t)kWaveWindow), sum1, sum2);
-      }
-    }
-    if (active) {
-      const int64_t row = r0 + lane;
-      double y1 = sum1;
-      if constexpr (EPI == EPI_BMINUS) y1 = a.b[row] - sum1;
-      a.y1[row] = y1;
-      if constexpr (NV == 2) a.y2[row] = sum2;
-      if constexpr (NP > 0) {
-        const double xv = T::kX ? x1[a.xoff + row] : 0.0;
-        const double x2v = T::kX2 ? x2[a.xoff + row] : 0.0;
-        const double ev = T::kE ? a.e[row] : 0.0;
-        epi_products<EPI>(xv, x2v, y1, sum2, ev, acc);
-      }
-    }
-  }
-  block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
-}
-
-// The offset-mask row walk (SpmvArgs::mask); false if not applicable.
-template <typename RP, int E, bool VEC>
-bool spmv_masked(const SpmvArgs& a, dim3 grid, dim3 block, hipStream_t s) {
-  if constexpr (VEC) {
-    switch (a.mw) {
-      case 8: spmv_kernel<RP, E, VEC, kGather, true, false, 8><<<grid, block, 0, s>>>(a); return true;
-      case 16: spmv_kernel<RP, E, VEC, kGather, true, false, 16><<<grid, block, 0, s>>>(a); return true;
-      case 32: spmv_kernel<RP, E, VEC, kGather, true, false, 32><<<grid, block, 0, s>>>(a); return true;
-      case 64: spmv_kernel<RP, E, VEC, kGather, true, false, 64><<<grid, block, 0, s>>>(a); return true;
-      default: return false;
-    }
-  }
-  return false;
-}
-
-template <typename RP, bool VEC>
-void spmv_dispatch(SpmvEpi epi, const SpmvArgs& a, int nblocks, hipStream_t s) {
-  const dim3 grid(nblocks), block(kBlock);
-  // Row-walk (0) for short rows, product-then-sum (8) for long rows. The
-  // KR_SPMV_VARIANT environment variable overrides the choice for A/B runs
-  // (tools/spmv_micro.py): 1 no prefetch, 2 wave-independent, 3 4-deep gathers,
-  // 6 no XCD schedule, 7 non-temporal staging.
-  const char* env = getenv("KR_SPMV_VARIANT");
-  const int variant = env ? atoi(env) : (a.long_rows ? 8 : 0);
-  switch (epi) {
-#define KR_CASE(E)                                      \
-  case E:                                               \
-    if (variant == 1)                                   \
-      spmv_kernel_simple<RP, E, VEC><<<grid, block, 0, s>>>(a); \
-    else if (variant == 2)                              \
-      spmv_kernel_wave<RP, E, VEC><<<grid, block, 0, s>>>(a); \
-    else if (variant == 3)                              \
-      spmv_kernel<RP, E, VEC, 4><<<grid, block, 0, s>>>(a); \
-    else if (variant == 9)                              \
-      spmv_kernel<RP, E, VEC, 8><<<grid, block, 0, s>>>(a); \
-    else if (variant == 8)                              \
-      spmv_kernel_prod<RP, E, VEC><<<grid, block, 0, s>>>(a); \
-    else if (variant == 6)                              \
-      spmv_kernel<RP, E, VEC, kGather, false><<<grid, block, 0, s>>>(a); \
-    else if (variant == 7)                              \
-      spmv_kernel<RP, E, VEC, kGather, true, true><<<grid, block, 0, s>>>(a); \
-    else if (!(a.mask && spmv_masked<RP, E, VEC>(a, grid, block, s))) \
-      spmv_kernel<RP, E, VEC><<<grid, block, 0, s>>>(a); \
-    break;
-    KR_CASE(EPI_NONE)
-    KR_CASE(EPI_BMINUS)
-    KR_CASE(EPI_XY)
-    KR_CASE(EPI_HEAD_MRR)
-    KR_CASE(EPI_HEAD_KCG)
-    KR_CASE(EPI_MRR_LOOP)
-    KR_CASE(EPI_DUAL_NONE)
-    KR_CASE(EPI_DUAL_MRR)
-    KR_CASE(EPI_DUAL_KCG)
-#undef KR_CASE
-    default:
-      throw Failure(KR_ERR_INVALID, "unknown SpMV epilogue");
-  }
-}
 
 // ---------------------------------------------------------------------------
 // Elementwise vector steps. Operand slots p[0..5]; READ/WRITE masks say which
@@ -1467,6 +524,10 @@ int spmv_products(SpmvEpi epi) {
     case EPI_DUAL_NONE: return EpiTraits<EPI_DUAL_NONE>::NP;
     case EPI_DUAL_MRR: return EpiTraits<EPI_DUAL_MRR>::NP;
     case EPI_DUAL_KCG: return EpiTraits<EPI_DUAL_KCG>::NP;
+    case EPI_STEP_MRR_NOX:
+    case EPI_STEP_MRR_X2:
+    case EPI_STEP_MRR_X:
+    case EPI_STEP_KCG: return 0;
   }
   return 0;
 }
@@ -1478,20 +539,25 @@ void launch_spmv(SpmvEpi epi, const SpmvArgs& a, hipStream_t s) {
 void launch_spmv_grid(SpmvEpi epi, const SpmvArgs& a, int nblocks, hipStream_t s) {
   KR_REQUIRE(a.grid > 0 && nblocks > 0 && nblocks <= a.grid,
              "spmv: need 0 < blocks <= partial stride");
-  // 16-byte staging needs 16-byte aligned val/col bases
-  const bool vec = ((reinterpret_cast<uintptr_t>(a.val) | reinterpret_cast<uintptr_t>(a.col)) &
-                    15) == 0;
-  (void)vec;
-  if (a.rowptr64) {
-    if (vec)
-      spmv_dispatch<int64_t, true>(epi, a, nblocks, s);
-    else
-      spmv_dispatch<int64_t, false>(epi, a, nblocks, s);
-  } else {
-    if (vec)
-      spmv_dispatch<int32_t, true>(epi, a, nblocks, s);
-    else
-      spmv_dispatch<int32_t, false>(epi, a, nblocks, s);
+  switch (epi) {
+#define KR_CASE(E) \
+  case E: spmv_launch_epi<E>(a, nblocks, s); break;
+    KR_CASE(EPI_NONE)
+    KR_CASE(EPI_BMINUS)
+    KR_CASE(EPI_XY)
+    KR_CASE(EPI_HEAD_MRR)
+    KR_CASE(EPI_HEAD_KCG)
+    KR_CASE(EPI_MRR_LOOP)
+    KR_CASE(EPI_DUAL_NONE)
+    KR_CASE(EPI_DUAL_MRR)
+    KR_CASE(EPI_DUAL_KCG)
+    KR_CASE(EPI_STEP_MRR_NOX)
+    KR_CASE(EPI_STEP_MRR_X2)
+    KR_CASE(EPI_STEP_MRR_X)
+    KR_CASE(EPI_STEP_KCG)
+#undef KR_CASE
+    default:
+      throw Failure(KR_ERR_INVALID, "unknown SpMV epilogue");
   }
   KR_HIP_CHECK(hipGetLastError());
 }

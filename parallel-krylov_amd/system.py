@@ -185,9 +185,12 @@ class KrylovSystem:
         nnz = int(indptr[-1] - indptr[0])
         rp64 = nnz >= 2 ** 31 - 1 or indptr.dtype == np.int64 and int(indptr[-1]) >= 2 ** 31 - 1
         dev = self.device(s)
-        t_rp = torch.from_numpy(np.ascontiguousarray(indptr, dtype=np.int64 if rp64 else np.int32)).to(dev)
-        t_col = torch.from_numpy(np.ascontiguousarray(indices, dtype=np.int32)).to(dev)
-        t_val = torch.from_numpy(np.ascontiguousarray(data, dtype=np.float64)).to(dev)
+        def host(a, dt):  # contiguous + writable (memory-mapped files are read-only)
+            return torch.from_numpy(np.require(a, dt, ["C", "W"]))
+
+        t_rp = host(indptr, np.int64 if rp64 else np.int32).to(dev)
+        t_col = host(indices, np.int32).to(dev)
+        t_val = host(data, np.float64).to(dev)
         torch.cuda.synchronize(dev)
         self._keep += [t_rp, t_col, t_val]
         call("kr_system_adopt_csr", self.handle, s, t_rp.data_ptr(), int(rp64),

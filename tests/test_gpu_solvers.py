@@ -192,3 +192,38 @@ def test_large_true_residual_matches_history(method, k):
     res = out.info["residual"]
     assert res[0] == pytest.approx(1.0)
     sysm.close()
+
+
+def _run_env(monkeypatch, env, method, A, b, **kw):
+    for key, val in env.items():
+        monkeypatch.setenv(key, val)
+    with contextlib.redirect_stdout(io.StringIO()):
+        x, info = _solver(method)(A, b, **kw)
+    return x.cpu().numpy(), info
+
+
+@pytest.mark.parametrize("shards", ["0", "0,0,0"])
+@pytest.mark.parametrize("method,matrix,k", [
+    ("kskipmrr", ["poisson", 12, 3], 1), ("kskipmrr", ["poisson", 12, 3], 2),
+    ("kskipmrr", ["poisson", 12, 3], 3), ("kskipmrr", ["poisson", 12, 3], 5),
+    ("kskipmrr", ["banded", 3000, 13, 64, 0], 4), ("kskipcg", ["poisson", 12, 3], 3),
+    ("kskipcg", ["banded", 3000, 13, 64, 0], 2), ("adaptivekskipmrr", ["poisson", 16, 2], 6)])
+def test_fused_steps_bitwise_equal_unfused(monkeypatch, shards, method, matrix, k):
+    """The k-skip inner steps fused into the SpMV epilogue (EPI_STEP_*, the
+    default for short rows) perform the same operations in the same order as
+    the separate vector-step kernels followed by the SpMV: histories and x are
+    bitwise identical, for odd/even k (every deferred-x step kind), short and
+    long rows (row-walk and product-then-sum kernels), sharded or not, and
+    with the epilogue operands loaded early or late."""
+    A = golden_matrix(matrix)
+    b = np.random.default_rng(3).standard_normal(A.shape[0])
+    kw = dict(tol=1e-10, maxiter=400, k=k)
+    base = {"KRYLOV_AMD_SHARDS": shards}
+    x0, i0 = _run_env(monkeypatch, {**base, "KR_FUSE": "0"}, method, A, b, **kw)
+    for env in ({"KR_FUSE": "1", "KR_EPI_LATE": "1"}, {"KR_FUSE": "1", "KR_EPI_LATE": "0"}):
+        x1, i1 = _run_env(monkeypatch, {**base, **env}, method, A, b, **kw)
+        np.testing.assert_array_equal(i1["nosl"], i0["nosl"])
+        np.testing.assert_array_equal(i1["residual"], i0["residual"])
+        if "khistory" in i0:
+            np.testing.assert_array_equal(i1["khistory"], i0["khistory"])
+        np.testing.assert_array_equal(x1, x0)
