@@ -73,6 +73,24 @@ int kr_device_count(int* count) {
 }
 
 // ----------------------------------------------------------------- primitives
+// Entries of a CSR block (rowptr[n] - rowptr[0]), read back for the kernel
+// choice (spmv_kernel2 needs >= 4): the primitives are not on the solver path.
+static int64_t csr_nnz(const void* rowptr, int rowptr64, int64_t n, hipStream_t s) {
+  int64_t e[2] = {0, 0};
+  if (rowptr64) {
+    KR_HIP_CHECK(hipMemcpyAsync(&e[0], rowptr, 8, hipMemcpyDeviceToHost, s));
+    KR_HIP_CHECK(hipMemcpyAsync(&e[1], (const int64_t*)rowptr + n, 8, hipMemcpyDeviceToHost, s));
+  } else {
+    int32_t f[2] = {0, 0};
+    KR_HIP_CHECK(hipMemcpyAsync(&f[0], rowptr, 4, hipMemcpyDeviceToHost, s));
+    KR_HIP_CHECK(hipMemcpyAsync(&f[1], (const int32_t*)rowptr + n, 4, hipMemcpyDeviceToHost, s));
+    KR_HIP_CHECK(hipStreamSynchronize(s));
+    return (int64_t)f[1] - f[0];
+  }
+  KR_HIP_CHECK(hipStreamSynchronize(s));
+  return e[1] - e[0];
+}
+
 int kr_spmv_csr_f64(const void* rowptr, int rowptr64, const int32_t* col, const double* val,
                     int64_t n_rows, const double* x, double* y, void* stream) {
   return guarded([&] {
@@ -89,6 +107,7 @@ int kr_spmv_csr_f64(const void* rowptr, int rowptr64, const int32_t* col, const 
     a.y1 = y;
     a.grid = default_grid(n_rows);
     a.partials = primitive_scratch(1);
+    a.nnz_total = csr_nnz(rowptr, rowptr64, n_rows, static_cast<hipStream_t>(stream));
     launch_spmv(EPI_NONE, a, static_cast<hipStream_t>(stream));
   });
 }
@@ -112,6 +131,7 @@ int kr_spmv2_csr_f64(const void* rowptr, int rowptr64, const int32_t* col, const
     a.y2 = y2;
     a.grid = default_grid(n_rows);
     a.partials = primitive_scratch(1);
+    a.nnz_total = csr_nnz(rowptr, rowptr64, n_rows, static_cast<hipStream_t>(stream));
     launch_spmv(EPI_DUAL_NONE, a, static_cast<hipStream_t>(stream));
   });
 }

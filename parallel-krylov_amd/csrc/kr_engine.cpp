@@ -521,6 +521,7 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
       a.mw = s.mw;
     }
     a.epi_late = epi_late;
+    a.nnz_total = s.nnz;
     if (step) {
       a.u1 = s.own(st->u1) + r_begin;
       a.u2 = s.own(st->u2) + r_begin;

@@ -99,6 +99,7 @@ struct SpmvArgs {
   double* ud = nullptr;
   double c0 = 0, c1 = 0;
   int epi_late = 0;  // 1: load own-row epilogue operands at the row end (A/B, KR_EPI_LATE)
+  int64_t nnz_total = -1;  // entries of val/col (-1: unknown; spmv_kernel2 needs >= 4)
 };
 // Mean row length from which the product-then-sum SpMV is used.
 constexpr double kLongRow = 12.0;

@@ -178,12 +178,14 @@ __device__ __forceinline__ void epi_products(double x, double x2, double y, doub
 // The row's own-row operands (EpiIn) are loaded when the row block starts,
 // so their latency hides under the row walk (epi_load / epi_row_in).
 struct EpiIn {
-  double u1 = 0, u2 = 0, us = 0, e = 0;
+  double u1 = 0, u2 = 0, us = 0, e = 0, x = 0, x2 = 0;
 };
 template <int EPI>
 __device__ __forceinline__ EpiIn epi_load(const SpmvArgs& a, int64_t row) {
   using T = EpiTraits<EPI>;
   EpiIn in;
+  if constexpr (is_step<EPI>() || T::kX) in.x = a.x1[a.xoff + row];
+  if constexpr (T::kX2) in.x2 = a.x2[a.xoff + row];
   if constexpr (is_step<EPI>()) {
     in.u1 = a.u1[row];
     in.u2 = a.u2[row];
@@ -205,7 +207,7 @@ __device__ __forceinline__ void epi_row_in(const SpmvArgs& a, int64_t row, doubl
                                                              : 1]) {
   using T = EpiTraits<EPI>;
   if constexpr (is_step<EPI>()) {
-    const double xv = x1[a.xoff + row];
+    const double xv = in.x;
     if constexpr (EPI == EPI_STEP_KCG) {  // x = Ap0, sum1 = Ap1; u1 = x, u2 = Ar0
       const double a0 = a.c0 * xv;
       const double a1 = a.c0 * sum1;
@@ -236,11 +238,7 @@ __device__ __forceinline__ void epi_row_in(const SpmvArgs& a, int64_t row, doubl
     if constexpr (EPI == EPI_BMINUS) y1 = in.e - sum1;
     a.y1[row] = y1;
     if constexpr (T::NV == 2) a.y2[row] = sum2;
-    if constexpr (T::NP > 0) {
-      const double xv = T::kX ? x1[a.xoff + row] : 0.0;
-      const double x2v = T::kX2 ? x2[a.xoff + row] : 0.0;
-      epi_products<EPI>(xv, x2v, y1, sum2, in.e, acc);
-    }
+    if constexpr (T::NP > 0) epi_products<EPI>(in.x, in.x2, y1, sum2, in.e, acc);
   }
 }
 
@@ -988,6 +986,252 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_wave(SpmvArgs a) {
   block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
 }
 
+// Uniform loads through the scalar cache: the row-block boundaries
+// rowptr[r0], rowptr[r0 + nr] are the same for every lane, and the matrix is
+// constant while the kernel runs, so they are read as constant-address-space
+// (s_load) values. A vector load here would make the next window's address
+// computation wait (vmcnt, in order) for every vector load issued before it.
+template <typename T>
+__device__ __forceinline__ T load_uniform(const T* p, int64_t i) {
+  return ((const __attribute__((address_space(4))) T*)p)[i];
+}
+
+// Window staging for spmv_kernel2. EVERY lane issues exactly the same loads
+// whatever the window: a slot past the window's last entry re-reads the
+// 16-byte chunk holding that entry (same line, no new traffic) instead of
+// being skipped, and there is no edge branch. Entries outside [bs, be) land
+// in LDS but no row reads them. Equal load counts on every path let the
+// compiler wait for exactly the loads it needs (vmcnt counts in issue order;
+// with a skippable load it has to assume the fewer-loads path and waits for
+// everything). Needs >= 4 entries in the matrix (host check).
+template <bool COLS>
+__device__ __forceinline__ void stage_load2(Stage& st, const double* __restrict__ val,
+                                            const int32_t* __restrict__ col, int64_t ws,
+                                            int64_t be, int tid) {
+  const int64_t vlast = max((be - 1) & ~(int64_t)1, (int64_t)0);
+#pragma unroll
+  for (int q = 0; q < kVSlots; ++q) {
+    const int64_t g0 = min(ws + (int64_t)(tid + q * kBlock) * 2, vlast);
+    st.v[q] = *reinterpret_cast<const dbl2v*>(val + g0);
+  }
+  if constexpr (COLS) {
+    const int64_t clast = max((be - 1) & ~(int64_t)3, (int64_t)0);
+#pragma unroll
+    for (int q = 0; q < kCSlots; ++q) {
+      const int64_t g0 = min(ws + (int64_t)(tid + q * kBlock) * 4, clast);
+      st.c[q] = *reinterpret_cast<const int4v*>(col + g0);
+    }
+  }
+}
+
+// Row walk, version 2 (default for short rows). Same arithmetic and order as
+// spmv_kernel (bitwise scipy csr_matvec), reorganised around the in-order
+// completion of vector loads (vmcnt): per window, a lane FIRST issues its
+// first batch of x gathers, THEN the loads of the next window (values, its
+// row range and mask), so waiting for the gathers does not wait for the
+// next window's HBM round trip, which stays in flight across the row sums,
+// the epilogue and the next LDS commit. The block boundaries come through
+// the scalar cache (load_uniform), the LDS windows are double-buffered (one
+// barrier per window), and each lane loads its own row range (no LDS
+// exchange of row pointers).
+template <typename RP, int EPI, bool VEC, int MW>
+__global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
+  using T = EpiTraits<EPI>;
+  constexpr int NP = T::NP;
+  constexpr int NV = T::NV;
+  constexpr int G = kGather;
+  constexpr bool COLS = MW == 0;  // else: offset masks, no column stream
+  using MT = typename MaskType<(MW > 0 ? MW : 64)>::type;
+  using W = typename std::conditional<(MW > 32), uint64_t, uint32_t>::type;
+  __shared__ __attribute__((aligned(16))) double s_val[2][kWindow];
+  __shared__ __attribute__((aligned(16))) int32_t s_col[COLS ? 2 : 1][COLS ? kWindow : 4];
+  __shared__ int32_t s_M[COLS ? 1 : 64];
+  __shared__ double s_red[(NP > 0 ? NP : 1) * 4];
+
+  const RP* __restrict__ rowptr = static_cast<const RP*>(a.rowptr);
+  const MT* __restrict__ mask = static_cast<const MT*>(a.mask);
+  const double* __restrict__ val = a.val;
+  const int32_t* __restrict__ col = a.col;
+  const double* __restrict__ x1 = a.x1;
+  const double* __restrict__ x2 = a.x2;
+  const int tid = threadIdx.x;
+  if constexpr (!COLS) {
+    if (tid < a.nm) s_M[tid] = a.moff[tid];  // seen after the first barrier
+  }
+
+  double acc[NP > 0 ? NP : 1];
+#pragma unroll
+  for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;
+
+  const int64_t nrb = (a.n + kBlock - 1) / kBlock;
+  RowSched sched;
+  sched.init(nrb, a.slab, a.slab_sub, true);
+  int64_t j = sched.j0;
+  const int64_t jstep = sched.jstep, jcount = sched.jcount;
+  if (j >= jcount) {
+    block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
+    return;
+  }
+  auto block_rows = [&](int64_t b) { return (int)min((int64_t)kBlock, a.n - b * kBlock); };
+  auto wstart = [](int64_t e) { return VEC ? (e & ~(int64_t)3) : e; };
+
+  // current row block: boundaries (uniform), this lane's row range and mask
+  int64_t r0 = sched.rb(j) * kBlock;
+  int nr = block_rows(sched.rb(j));
+  int64_t bs = (int64_t)load_uniform(rowptr, r0);
+  int64_t be = (int64_t)load_uniform(rowptr, r0 + nr);
+  RP rlo = 0, rhi = 0;  // converted at use: a conversion here would wait on the load
+  W my_mask = 0;
+  {
+    const int64_t ri = min(r0 + tid, a.n - 1);
+    rlo = rowptr[ri];
+    rhi = rowptr[ri + 1];
+    if constexpr (!COLS) my_mask = (W)mask[ri];
+  }
+  int64_t bsn = 0, ben = 0;  // next row block's boundaries
+  if (j + jstep < jcount) {
+    const int64_t rbn = sched.rb(j + jstep);
+    bsn = (int64_t)load_uniform(rowptr, rbn * kBlock);
+    ben = (int64_t)load_uniform(rowptr, rbn * kBlock + block_rows(rbn));
+  }
+  Stage st;
+  int64_t ws = wstart(bs);
+  auto stage = [&](int64_t w, int64_t lo, int64_t hi) {
+    if constexpr (VEC)
+      stage_load2<COLS>(st, val, col, w, hi, tid);
+    else
+      stage_load<false, false, COLS>(st, val, col, w, lo, hi, tid);
+  };
+  stage(ws, bs, be);
+  int buf = 0;
+  bool first_window = true;
+  W mrem = 0;
+  EpiIn pin;
+  double sum1 = 0.0, sum2 = 0.0;
+  // next row block's lane state (loaded while the current window is summed)
+  int64_t r0n = 0;
+  RP rlo_n = 0, rhi_n = 0;
+  int nrn = 0;
+  W mask_n = 0;
+
+  for (;;) {
+    double* sv = s_val[buf];
+    int32_t* sc = s_col[COLS ? buf : 0];
+    stage_commit<COLS>(st, sv, sc, tid);
+    __syncthreads();
+    const bool active = tid < nr;
+    if (first_window) {
+      mrem = my_mask;
+      // own-row epilogue operands, issued before the gathers so that
+      // waiting for the gathers covers them
+      pin = epi_load<EPI>(a, active ? r0 + tid : r0);
+    }
+    const int64_t off = bs - ws;
+    const int js = active ? (int)max((int64_t)rlo - bs + off, (int64_t)0) : 0;
+    const int je = active ? (int)min((int64_t)rhi - bs + off, (int64_t)kWindow) : 0;
+    const int64_t xrow = a.xoff + r0 + tid;
+
+    // (1) first gather batch of this window
+    double v[G], p1[G], p2[G];
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const bool ok = js + u < je;
+      v[u] = sv[ok ? js + u : 0];
+      int64_t c;
+      if constexpr (COLS) {
+        c = sc[ok ? js + u : 0];
+      } else {
+        c = xrow;
+        if (ok) {
+          c += s_M[sizeof(W) == 8 ? __builtin_ctzll((unsigned long long)mrem)
+                                  : __builtin_ctz((unsigned)mrem)];
+          mrem &= mrem - 1;
+        }
+      }
+      p1[u] = x1[c];
+      if constexpr (NV == 2) p2[u] = x2[c];
+    }
+
+    // (2) the next window's loads: they stay in flight while this one is summed
+    const bool last_window = ws + kWindow >= be;
+    const int64_t j_next = j + jstep;
+    const bool has_next = j_next < jcount;
+    // Issued unconditionally, from ONE call site, with the same count on
+    // every path (see stage_load2): the last window of the last row block
+    // re-reads itself. Two call sites would get two register sets and a copy
+    // that waits for the loads.
+    {
+      const bool nb = last_window && has_next;  // next row block
+      const int64_t nws = !last_window ? ws + kWindow : nb ? wstart(bsn) : ws;
+      stage(nws, nb ? bsn : bs, nb ? ben : be);
+      if (nb) {
+        const int64_t rb_next = sched.rb(j_next);
+        r0n = rb_next * kBlock;
+        nrn = block_rows(rb_next);
+      }
+      const int64_t ri = min((nb ? r0n : r0) + tid, a.n - 1);  // clamped: no branch
+      rlo_n = rowptr[ri];
+      rhi_n = rowptr[ri + 1];
+      if constexpr (!COLS) mask_n = (W)mask[ri];
+    }
+
+    // (3) sums, in stored order: the first batch, then any further batches
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      if (js + u < je) {
+        sum1 = sum1 + v[u] * p1[u];
+        if constexpr (NV == 2) sum2 = sum2 + v[u] * p2[u];
+      }
+    }
+    if (je - js > G) {
+      if constexpr (COLS)
+        row_window<NV, G>(sv, sc, x1, x2, js + G, je, sum1, sum2);
+      else
+        row_window_mask<NV, G>(sv, s_M, x1, x2, xrow, js + G, je, mrem, sum1, sum2);
+    }
+    buf ^= 1;
+    if (!last_window) {
+      ws += kWindow;
+      first_window = false;
+      continue;
+    }
+    if (active) epi_row_in<EPI>(a, r0 + tid, sum1, sum2, x1, x2, pin, acc);
+    if (!has_next) break;
+    // advance to the next row block; its boundaries after it come through
+    // the scalar cache now (used one row block later)
+    j = j_next;
+    r0 = r0n;
+    nr = nrn;
+    bs = bsn;
+    be = ben;
+    rlo = rlo_n;
+    rhi = rhi_n;
+    my_mask = mask_n;
+    if (j + jstep < jcount) {
+      const int64_t rbnn = sched.rb(j + jstep);
+      bsn = (int64_t)load_uniform(rowptr, rbnn * kBlock);
+      ben = (int64_t)load_uniform(rowptr, rbnn * kBlock + block_rows(rbnn));
+    }
+    ws = wstart(bs);
+    first_window = true;
+    sum1 = 0.0;
+    sum2 = 0.0;
+  }
+  __syncthreads();
+  block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
+}
+
+template <typename RP, int E, bool VEC>
+void spmv2_launch(const SpmvArgs& a, dim3 grid, dim3 block, hipStream_t s) {
+  switch (a.mask ? a.mw : 0) {
+    case 8: spmv_kernel2<RP, E, VEC, 8><<<grid, block, 0, s>>>(a); return;
+    case 16: spmv_kernel2<RP, E, VEC, 16><<<grid, block, 0, s>>>(a); return;
+    case 32: spmv_kernel2<RP, E, VEC, 32><<<grid, block, 0, s>>>(a); return;
+    case 64: spmv_kernel2<RP, E, VEC, 64><<<grid, block, 0, s>>>(a); return;
+    default: spmv_kernel2<RP, E, VEC, 0><<<grid, block, 0, s>>>(a); return;
+  }
+}
+
 // The offset-mask row walk (SpmvArgs::mask); false if not applicable.
 template <typename RP, int E, bool VEC>
 bool spmv_masked(const SpmvArgs& a, dim3 grid, dim3 block, hipStream_t s) {
@@ -1006,16 +1250,21 @@ bool spmv_masked(const SpmvArgs& a, dim3 grid, dim3 block, hipStream_t s) {
 template <typename RP, bool VEC, int E>
 void spmv_dispatch_epi(const SpmvArgs& a, int nblocks, hipStream_t s) {
   const dim3 grid(nblocks), block(kBlock);
-  // Row-walk (0) for short rows, product-then-sum (8) for long rows. The
+  // Row walk v2 (10) for short rows, product-then-sum (8) for long rows. The
   // KR_SPMV_VARIANT environment variable overrides the choice for A/B runs
-  // (tools/spmv_micro.py): 1 no prefetch, 2 wave-independent, 3 4-deep gathers,
+  // (tools/spmv_micro.py): 0 row walk v1, 1 no prefetch, 2 wave-independent, 3 4-deep gathers,
   // 6 no XCD schedule, 7 non-temporal staging, 9 8-deep gathers. Fused steps
   // instantiate only the production kernels (row walk, offset masks,
   // product-then-sum); the A/B variants fall back to the row walk for them.
   const char* env = getenv("KR_SPMV_VARIANT");
-  const int variant = env ? atoi(env) : (a.long_rows ? 8 : 0);
+  int variant = env ? atoi(env) : (a.long_rows ? 8 : 10);
+  if (variant == 10 && a.nnz_total < 4) variant = 0;  // spmv_kernel2 needs 4 entries
   if (variant == 8) {
     spmv_kernel_prod<RP, E, VEC><<<grid, block, 0, s>>>(a);
+    return;
+  }
+  if (variant == 10) {
+    spmv2_launch<RP, E, VEC>(a, grid, block, s);
     return;
   }
   if constexpr (!is_step<E>()) {
