@@ -35,6 +35,7 @@ struct Comm {
 
 // Slots of fused reduction products per shard (enough for k <= 16).
 constexpr int kMaxSlots = 6 + 7 * 16 + 8;
+static_assert(kMaxSlots <= kFinalizeSlots, "finalize slot table too small");
 
 // A contiguous range of global rows exchanged with one peer shard/rank.
 struct HaloPiece {
@@ -74,9 +75,12 @@ struct Shard {
   int nm = 0, mw = 0;
   hipStream_t comm_stream = nullptr;  // halo exchange, overlapped with interior rows
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
-  int grid = 1;
+  int grid = 1;                 // workgroups of the vector kernels
+  int spmv_grid = 1;            // workgroups of the SpMV kernels
+  int pstride = 1;              // partial stride per slot: max(grid, spmv_grid)
+  std::array<int, kMaxSlots> slot_n{};  // partials written per slot by its last producer
   // reductions
-  double* partials = nullptr;   // [kMaxSlots][grid]
+  double* partials = nullptr;   // [kMaxSlots][pstride]
   double* slots = nullptr;      // [kMaxSlots]
   double* gather = nullptr;     // [nranks][kMaxSlots] (RCCL)
   double* host = nullptr;       // pinned [nranks][kMaxSlots]

@@ -129,7 +129,8 @@ struct EwArgs {
   double* p[6] = {};               // operand pointers, meaning per op
   int64_t n = 0;
   double* partials = nullptr;
-  int grid = 0;
+  int grid = 0;                    // workgroups launched
+  int stride = 0;                  // partial stride per slot (0: grid)
 };
 void launch_ew(EwOp op, const EwArgs& a, hipStream_t s);
 
@@ -137,6 +138,15 @@ void launch_ew(EwOp op, const EwArgs& a, hipStream_t s);
 // in a fixed order (deterministic).
 void launch_finalize(const double* partials, int grid, int nslots, double* out,
                      hipStream_t s);
+// Upper bound on reduction slots of one finalize (engine: kMaxSlots).
+constexpr int kFinalizeSlots = 128;
+// Same with stride `stride` per slot and count[slot] partials in slot `slot`
+// (launches of different grid sizes feed different slots).
+struct SlotCounts {
+  int n[kFinalizeSlots];
+};
+void launch_finalize_counts(const double* partials, int stride, const SlotCounts& counts,
+                            int nslots, double* out, hipStream_t s);
 
 // Many independent dot products in one pass (count <= 64).
 struct MultiDotArgs {
@@ -201,5 +211,7 @@ void banded_offsets(int h, int64_t width, uint64_t seed, int64_t* out_sorted);
 double* primitive_scratch(size_t doubles);
 
 int default_grid(int64_t n);
+// Workgroups of the SpMV kernels for a block of n rows with column reach `reach` rows.
+int spmv_grid_for(int64_t n, int64_t reach);
 
 }  // namespace kr

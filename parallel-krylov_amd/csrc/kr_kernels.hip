@@ -219,7 +219,7 @@ __global__ __launch_bounds__(kBlock) void ew_kernel(EwArgs a) {
         if (T::W & (1 << k)) a.p[k][i] = v[k];
     }
   }
-  block_reduce_store<NP>(acc, a.partials, a.grid, s_red);
+  block_reduce_store<NP>(acc, a.partials, a.stride > 0 ? a.stride : a.grid, s_red);
 }
 
 template <int OP>
@@ -252,6 +252,27 @@ __global__ __launch_bounds__(kBlock) void finalize_kernel(const double* __restri
   const int slot = blockIdx.x;
   double t = 0.0;
   for (int i = threadIdx.x; i < grid; i += kBlock) t += part[(int64_t)slot * grid + i];
+  for (int off = 32; off > 0; off >>= 1) t += __shfl_down(t, off, 64);
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double r = s_red[0];
+    r = r + s_red[1];
+    r = r + s_red[2];
+    r = r + s_red[3];
+    out[slot] = r;
+  }
+}
+
+// As finalize_kernel, with a per-slot partial count (same fixed order).
+__global__ __launch_bounds__(kBlock) void finalize_counts_kernel(const double* __restrict__ part,
+                                                                 int stride, SlotCounts c,
+                                                                 double* __restrict__ out) {
+  __shared__ double s_red[4];
+  const int slot = blockIdx.x;
+  const int cnt = c.n[slot];
+  double t = 0.0;
+  for (int i = threadIdx.x; i < cnt; i += kBlock) t += part[(int64_t)slot * stride + i];
   for (int off = 32; off > 0; off >>= 1) t += __shfl_down(t, off, 64);
   if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = t;
   __syncthreads();
@@ -600,6 +621,14 @@ void launch_finalize(const double* partials, int grid, int nslots, double* out,
                      hipStream_t s) {
   if (nslots <= 0) return;
   finalize_kernel<<<nslots, kBlock, 0, s>>>(partials, grid, out);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_finalize_counts(const double* partials, int stride, const SlotCounts& counts,
+                            int nslots, double* out, hipStream_t s) {
+  if (nslots <= 0) return;
+  KR_REQUIRE(nslots <= kFinalizeSlots, "too many reduction slots");
+  finalize_counts_kernel<<<nslots, kBlock, 0, s>>>(partials, stride, counts, out);
   KR_HIP_CHECK(hipGetLastError());
 }
 

@@ -1004,7 +1004,7 @@ __device__ __forceinline__ T load_uniform(const T* p, int64_t i) {
 // compiler wait for exactly the loads it needs (vmcnt counts in issue order;
 // with a skippable load it has to assume the fewer-loads path and waits for
 // everything). Needs >= 4 entries in the matrix (host check).
-template <bool COLS>
+template <bool COLS, bool NT = false>
 __device__ __forceinline__ void stage_load2(Stage& st, const double* __restrict__ val,
                                             const int32_t* __restrict__ col, int64_t ws,
                                             int64_t be, int tid) {
@@ -1012,14 +1012,20 @@ __device__ __forceinline__ void stage_load2(Stage& st, const double* __restrict_
 #pragma unroll
   for (int q = 0; q < kVSlots; ++q) {
     const int64_t g0 = min(ws + (int64_t)(tid + q * kBlock) * 2, vlast);
-    st.v[q] = *reinterpret_cast<const dbl2v*>(val + g0);
+    if constexpr (NT)
+      st.v[q] = __builtin_nontemporal_load(reinterpret_cast<const dbl2v*>(val + g0));
+    else
+      st.v[q] = *reinterpret_cast<const dbl2v*>(val + g0);
   }
   if constexpr (COLS) {
     const int64_t clast = max((be - 1) & ~(int64_t)3, (int64_t)0);
 #pragma unroll
     for (int q = 0; q < kCSlots; ++q) {
       const int64_t g0 = min(ws + (int64_t)(tid + q * kBlock) * 4, clast);
-      st.c[q] = *reinterpret_cast<const int4v*>(col + g0);
+      if constexpr (NT)
+        st.c[q] = __builtin_nontemporal_load(reinterpret_cast<const int4v*>(col + g0));
+      else
+        st.c[q] = *reinterpret_cast<const int4v*>(col + g0);
     }
   }
 }
@@ -1034,7 +1040,7 @@ __device__ __forceinline__ void stage_load2(Stage& st, const double* __restrict_
 // the scalar cache (load_uniform), the LDS windows are double-buffered (one
 // barrier per window), and each lane loads its own row range (no LDS
 // exchange of row pointers).
-template <typename RP, int EPI, bool VEC, int MW>
+template <typename RP, int EPI, bool VEC, int MW, bool DB = true, bool NT = false>
 __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
   using T = EpiTraits<EPI>;
   constexpr int NP = T::NP;
@@ -1043,8 +1049,11 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
   constexpr bool COLS = MW == 0;  // else: offset masks, no column stream
   using MT = typename MaskType<(MW > 0 ? MW : 64)>::type;
   using W = typename std::conditional<(MW > 32), uint64_t, uint32_t>::type;
-  __shared__ __attribute__((aligned(16))) double s_val[2][kWindow];
-  __shared__ __attribute__((aligned(16))) int32_t s_col[COLS ? 2 : 1][COLS ? kWindow : 4];
+  // DB: double-buffered windows, one barrier per window; else one buffer
+  // (half the LDS: more workgroups per CU) and a second barrier.
+  constexpr int NB = DB ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) double s_val[NB][kWindow];
+  __shared__ __attribute__((aligned(16))) int32_t s_col[COLS ? NB : 1][COLS ? kWindow : 4];
   __shared__ int32_t s_M[COLS ? 1 : 64];
   __shared__ double s_red[(NP > 0 ? NP : 1) * 4];
 
@@ -1098,7 +1107,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
   int64_t ws = wstart(bs);
   auto stage = [&](int64_t w, int64_t lo, int64_t hi) {
     if constexpr (VEC)
-      stage_load2<COLS>(st, val, col, w, hi, tid);
+      stage_load2<COLS, NT>(st, val, col, w, hi, tid);
     else
       stage_load<false, false, COLS>(st, val, col, w, lo, hi, tid);
   };
@@ -1115,8 +1124,8 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
   W mask_n = 0;
 
   for (;;) {
-    double* sv = s_val[buf];
-    int32_t* sc = s_col[COLS ? buf : 0];
+    double* sv = s_val[DB ? buf : 0];
+    int32_t* sc = s_col[COLS && DB ? buf : 0];
     stage_commit<COLS>(st, sv, sc, tid);
     __syncthreads();
     const bool active = tid < nr;
@@ -1190,6 +1199,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
         row_window_mask<NV, G>(sv, s_M, x1, x2, xrow, js + G, je, mrem, sum1, sum2);
     }
     buf ^= 1;
+    if constexpr (!DB) __syncthreads();  // the single buffer is rewritten next
     if (!last_window) {
       ws += kWindow;
       first_window = false;
@@ -1221,14 +1231,14 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
   block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
 }
 
-template <typename RP, int E, bool VEC>
+template <typename RP, int E, bool VEC, bool DB = true, bool NT = false>
 void spmv2_launch(const SpmvArgs& a, dim3 grid, dim3 block, hipStream_t s) {
   switch (a.mask ? a.mw : 0) {
-    case 8: spmv_kernel2<RP, E, VEC, 8><<<grid, block, 0, s>>>(a); return;
-    case 16: spmv_kernel2<RP, E, VEC, 16><<<grid, block, 0, s>>>(a); return;
-    case 32: spmv_kernel2<RP, E, VEC, 32><<<grid, block, 0, s>>>(a); return;
-    case 64: spmv_kernel2<RP, E, VEC, 64><<<grid, block, 0, s>>>(a); return;
-    default: spmv_kernel2<RP, E, VEC, 0><<<grid, block, 0, s>>>(a); return;
+    case 8: spmv_kernel2<RP, E, VEC, 8, DB, NT><<<grid, block, 0, s>>>(a); return;
+    case 16: spmv_kernel2<RP, E, VEC, 16, DB, NT><<<grid, block, 0, s>>>(a); return;
+    case 32: spmv_kernel2<RP, E, VEC, 32, DB, NT><<<grid, block, 0, s>>>(a); return;
+    case 64: spmv_kernel2<RP, E, VEC, 64, DB, NT><<<grid, block, 0, s>>>(a); return;
+    default: spmv_kernel2<RP, E, VEC, 0, DB, NT><<<grid, block, 0, s>>>(a); return;
   }
 }
 
@@ -1250,21 +1260,31 @@ bool spmv_masked(const SpmvArgs& a, dim3 grid, dim3 block, hipStream_t s) {
 template <typename RP, bool VEC, int E>
 void spmv_dispatch_epi(const SpmvArgs& a, int nblocks, hipStream_t s) {
   const dim3 grid(nblocks), block(kBlock);
-  // Row walk v2 (10) for short rows, product-then-sum (8) for long rows. The
+  // Row walk v2 with a non-temporal matrix stream (13; +1 % over 10) for short
+  // rows, product-then-sum (8) for long rows. The
   // KR_SPMV_VARIANT environment variable overrides the choice for A/B runs
   // (tools/spmv_micro.py): 0 row walk v1, 1 no prefetch, 2 wave-independent, 3 4-deep gathers,
   // 6 no XCD schedule, 7 non-temporal staging, 9 8-deep gathers. Fused steps
   // instantiate only the production kernels (row walk, offset masks,
   // product-then-sum); the A/B variants fall back to the row walk for them.
   const char* env = getenv("KR_SPMV_VARIANT");
-  int variant = env ? atoi(env) : (a.long_rows ? 8 : 10);
-  if (variant == 10 && a.nnz_total < 4) variant = 0;  // spmv_kernel2 needs 4 entries
+  int variant = env ? atoi(env) : (a.long_rows ? 8 : 13);
+  if ((variant == 10 || variant == 12 || variant == 13) && a.nnz_total < 4)
+    variant = 0;  // v2 needs 4 entries
   if (variant == 8) {
     spmv_kernel_prod<RP, E, VEC><<<grid, block, 0, s>>>(a);
     return;
   }
   if (variant == 10) {
     spmv2_launch<RP, E, VEC>(a, grid, block, s);
+    return;
+  }
+  if (variant == 12) {  // row walk v2, single-buffered window (A/B)
+    spmv2_launch<RP, E, VEC, false>(a, grid, block, s);
+    return;
+  }
+  if (variant == 13) {  // row walk v2, non-temporal matrix stream (A/B)
+    spmv2_launch<RP, E, VEC, true, true>(a, grid, block, s);
     return;
   }
   if constexpr (!is_step<E>()) {

@@ -17,7 +17,8 @@ import sys
 
 # Names follow kr_internal.h's SpmvEpi / EwOp enums (and kr_engine's epi_name/ew_name).
 EPI = ["spmv", "spmv_bminus", "spmv_xy", "spmv_head_mrr", "spmv_head_kcg", "spmv_mrr_loop",
-       "spmv2", "spmv2_gram_mrr", "spmv2_gram_kcg"]
+       "spmv2", "spmv2_gram_mrr", "spmv2_gram_kcg", "spmv_step_mrr_nox", "spmv_step_mrr_x2",
+       "spmv_step_mrr_x", "spmv_step_kcg"]
 EW = ["dot", "update_mrr_first", "update_mrr", "update_cg", "update_cg_p", "update_kcg",
       "mrr_s", "copy", "update_mrr_nox", "update_mrr_x2"]
 
@@ -63,10 +64,15 @@ def main(d):
             rec["write_size_kb"] = c["WRITE_SIZE"]
         if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
             rec["l2_hit"] = c["TCC_HIT_sum"] / max(1.0, c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
+        if "TCC_EA0_RDREQ_DRAM_sum" in c and "TCC_EA0_RDREQ_sum" in c:
+            # share of the beyond-L2 read requests that go to DRAM (the rest
+            # are served by the fabric / Infinity Cache side)
+            rec["dram_read_share"] = c["TCC_EA0_RDREQ_DRAM_sum"] / max(1.0, c["TCC_EA0_RDREQ_sum"])
         rec["counters"] = c
         out[k] = rec
     json.dump(out, open(os.path.join(d, "summary.json"), "w"), indent=1)
-    print(f"{'kernel':28s} {'n':>4s} {'avg_ms':>8s} {'read GB':>8s} {'write GB':>8s} {'GB/s':>8s} {'L2hit':>6s}")
+    print(f"{'kernel':28s} {'n':>4s} {'avg_ms':>8s} {'read GB':>8s} {'write GB':>8s} {'GB/s':>8s} "
+          f"{'L2hit':>6s} {'DRAMrd':>6s}")
     for k, r in out.items():
         if r["avg_ms"] is None:
             continue
@@ -74,7 +80,7 @@ def main(d):
         wr = r.get("write_bytes", float("nan")) / 1e9
         bw = (r.get("traffic_bytes", float("nan")) / (r["avg_ms"] * 1e6))
         print(f"{k:28s} {r['launches']:4d} {r['avg_ms']:8.3f} {rd:8.3f} {wr:8.3f} {bw:8.1f} "
-              f"{r.get('l2_hit', float('nan')):6.3f}")
+              f"{r.get('l2_hit', float('nan')):6.3f} {r.get('dram_read_share', float('nan')):6.3f}")
 
 
 if __name__ == "__main__":
