@@ -809,183 +809,6 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_prod(SpmvArgs a) {
   block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
 }
 
-// Variant 1: no cross-row-block prefetch (lower VGPR count, higher occupancy).
-template <typename RP, int EPI, bool VEC>
-__global__ __launch_bounds__(kBlock) void spmv_kernel_simple(SpmvArgs a) {
-  using T = EpiTraits<EPI>;
-  constexpr int NP = T::NP;
-  constexpr int NV = T::NV;
-  __shared__ __attribute__((aligned(16))) double s_val[kWindow];
-  __shared__ __attribute__((aligned(16))) int32_t s_col[kWindow];
-  __shared__ int32_t s_rp[kBlock + 1];  // row pointers relative to the block start
-  __shared__ double s_red[(NP > 0 ? NP : 1) * 4];
-
-  const RP* __restrict__ rowptr = static_cast<const RP*>(a.rowptr);
-  const double* __restrict__ val = a.val;
-  const int32_t* __restrict__ col = a.col;
-  const double* __restrict__ x1 = a.x1;
-  const double* __restrict__ x2 = a.x2;
-  const int tid = threadIdx.x;
-
-  double acc[NP > 0 ? NP : 1];
-#pragma unroll
-  for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;
-
-  const int64_t nrb = (a.n + kBlock - 1) / kBlock;
-  for (int64_t rb = blockIdx.x; rb < nrb; rb += gridDim.x) {
-    const int64_t r0 = rb * kBlock;
-    const int nr = (int)min((int64_t)kBlock, a.n - r0);
-    const int64_t bs = (int64_t)rowptr[r0];
-    const int64_t be = (int64_t)rowptr[r0 + nr];
-    if (tid < nr) s_rp[tid + 1] = (int32_t)((int64_t)rowptr[r0 + tid + 1] - bs);
-    if (tid == 0) s_rp[0] = 0;
-    __syncthreads();
-    const bool active = tid < nr;
-    const int rs = active ? s_rp[tid] : 0;
-    const int re = active ? s_rp[tid + 1] : 0;
-    double sum1 = 0.0, sum2 = 0.0;
-    // windows start 4-aligned so every slot is one 16-byte access
-    const int64_t w0 = VEC ? (bs & ~(int64_t)3) : bs;
-    for (int64_t ws = w0; ws < be; ws += kWindow) {
-      {
-        Stage st;
-        stage_load<VEC>(st, val, col, ws, bs, be, tid);
-        stage_commit(st, s_val, s_col, tid);
-      }
-      __syncthreads();
-      if (active) {
-        // this lane's entries inside the window, as window offsets
-        const int64_t off = bs - ws;  // window offset of the block's entry 0
-        const int js = (int)max((int64_t)rs + off, (int64_t)0);
-        const int je = (int)min((int64_t)re + off, (int64_t)kWindow);
-        for (int j = js; j < je; j += kGather) {
-          double v[kGather], p1[kGather], p2[kGather];
-#pragma unroll
-          for (int u = 0; u < kGather; ++u) {
-            const int jj = (j + u < je) ? j + u : js;
-            v[u] = s_val[jj];
-            const int c = s_col[jj];
-            p1[u] = x1[c];
-            if constexpr (NV == 2) p2[u] = x2[c];
-          }
-#pragma unroll
-          for (int u = 0; u < kGather; ++u) {
-            if (j + u < je) {
-              sum1 = sum1 + v[u] * p1[u];
-              if constexpr (NV == 2) sum2 = sum2 + v[u] * p2[u];
-            }
-          }
-        }
-      }
-      __syncthreads();
-    }
-    if (active) {
-      epi_row<EPI>(a, r0 + tid, sum1, sum2, x1, x2, acc);
-    }
-    __syncthreads();  // s_rp is rewritten by the next row block
-  }
-  block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
-}
-
-// Variant 2: wave-independent. Each wave owns 64-row blocks and a private
-// LDS window; staging and the row walk need only wave-local ordering (an
-// s_waitcnt on the LDS counter), never a workgroup barrier, so the four waves
-// of a workgroup stream independently.
-constexpr int kWaveRows = 64;
-constexpr int kWaveWindow = 512;  // entries per wave window (2 slots of 4 per lane)
-constexpr int kWaveSlots = kWaveWindow / (4 * kWaveRows);
-static_assert(kWaveSlots * 4 * kWaveRows == kWaveWindow, "wave window layout");
-
-__device__ __forceinline__ void lds_fence() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
-
-template <typename RP, int EPI, bool VEC>
-__global__ __launch_bounds__(kBlock) void spmv_kernel_wave(SpmvArgs a) {
-  using T = EpiTraits<EPI>;
-  constexpr int NP = T::NP;
-  constexpr int NV = T::NV;
-  constexpr int kWaves = kBlock / 64;
-  __shared__ __attribute__((aligned(16))) double s_val_all[kWaves][kWaveWindow];
-  __shared__ __attribute__((aligned(16))) int32_t s_col_all[kWaves][kWaveWindow];
-  __shared__ double s_red[(NP > 0 ? NP : 1) * 4];
-
-  const RP* __restrict__ rowptr = static_cast<const RP*>(a.rowptr);
-  const double* __restrict__ val = a.val;
-  const int32_t* __restrict__ col = a.col;
-  const double* __restrict__ x1 = a.x1;
-  const double* __restrict__ x2 = a.x2;
-  const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  double* s_val = s_val_all[w];
-  int32_t* s_col = s_col_all[w];
-
-  double acc[NP > 0 ? NP : 1];
-#pragma unroll
-  for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;
-
-  const int64_t nwb = (a.n + kWaveRows - 1) / kWaveRows;
-  const int64_t gw = (int64_t)blockIdx.x * kWaves + w;
-  const int64_t nwaves = (int64_t)gridDim.x * kWaves;
-  for (int64_t wb = gw; wb < nwb; wb += nwaves) {
-    const int64_t r0 = wb * kWaveRows;
-    const int nr = (int)min((int64_t)kWaveRows, a.n - r0);
-    const int64_t bs = (int64_t)rowptr[r0];
-    const int64_t be = (int64_t)rowptr[r0 + nr];
-    const bool active = lane < nr;
-    const int64_t my_end = active ? (int64_t)rowptr[r0 + lane + 1] : be;
-    // row start = previous lane's end (lane 0: block start)
-    const int64_t my_beg = !active ? be : lane == 0 ? bs : (int64_t)rowptr[r0 + lane];
-    const int rs = (int)(my_beg - bs), re = (int)(my_end - bs);
-    double sum1 = 0.0, sum2 = 0.0;
-    const int64_t w0 = VEC ? (bs & ~(int64_t)3) : bs;
-    for (int64_t ws = w0; ws < be; ws += kWaveWindow) {
-      dbl2v lo[kWaveSlots], hi[kWaveSlots];
-      int4v c4[kWaveSlots];
-#pragma unroll
-      for (int q = 0; q < kWaveSlots; ++q) {
-        const int64_t g0 = ws + (int64_t)(lane + q * 64) * 4;
-        if (VEC && g0 >= bs && g0 + 4 <= be) {
-          lo[q] = *reinterpret_cast<const dbl2v*>(val + g0);
-          hi[q] = *reinterpret_cast<const dbl2v*>(val + g0 + 2);
-          c4[q] = *reinterpret_cast<const int4v*>(col + g0);
-        } else {
-          double tv[4];
-          int tc[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int64_t g = g0 + u;
-            const bool ok = g >= bs && g < be;
-            tv[u] = ok ? val[g] : 0.0;
-            tc[u] = ok ? col[g] : 0;
-          }
-          lo[q] = dbl2v{tv[0], tv[1]};
-          hi[q] = dbl2v{tv[2], tv[3]};
-          c4[q] = int4v{tc[0], tc[1], tc[2], tc[3]};
-        }
-      }
-      lds_fence();  // previous window fully read by every lane of the wave
-#pragma unroll
-      for (int q = 0; q < kWaveSlots; ++q) {
-        const int e0 = (lane + q * 64) * 4;
-        *reinterpret_cast<dbl2v*>(&s_val[e0]) = lo[q];
-        *reinterpret_cast<dbl2v*>(&s_val[e0 + 2]) = hi[q];
-        *reinterpret_cast<int4v*>(&s_col[e0]) = c4[q];
-      }
-      lds_fence();  // window visible to every lane of the wave
-      if (active) {
-        const int64_t off = bs - ws;
-        row_window<NV>(s_val, s_col, x1, x2, (int)max((int64_t)rs + off, (int64_t)0),
-                       (int)min((int64_t)re + off, (int64_t)kWaveWindow), sum1, sum2);
-      }
-    }
-    if (active) {
-      epi_row<EPI>(a, r0 + lane, sum1, sum2, x1, x2, acc);
-    }
-  }
-  block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
-}
-
 // Uniform loads through the scalar cache: the row-block boundaries
 // rowptr[r0], rowptr[r0 + nr] are the same for every lane, and the matrix is
 // constant while the kernel runs, so they are read as constant-address-space
@@ -1242,6 +1065,221 @@ void spmv2_launch(const SpmvArgs& a, dim3 grid, dim3 block, hipStream_t s) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Product-then-sum, version 2 (default for long rows). The operations and
+// their order are spmv_kernel_prod's (bitwise scipy), organised like
+// spmv_kernel2 around the in-order completion of vector loads, as a two-stage
+// software pipeline over windows: while the products of window t are formed
+// and its rows summed, the gathers of window t+1 and the loads of window t+2
+// are in flight. Per iteration: wait for the gathers of t (issued one
+// iteration earlier), write its products to LDS; wait for the loads of t+1,
+// issue its gathers; issue the loads of t+2; barrier; sum window t. Gathers
+// and window loads are issued unconditionally (a drained stage re-issues
+// valid addresses) so every path has the same load count after the gathers
+// and the waits stay exact; every gathered column is a real entry's column.
+// ---------------------------------------------------------------------------
+struct PWin {  // one staging window, uniform across the workgroup
+  int64_t ws = 0, bs = 0, be = 0, r0 = 0;
+  int nr = 0, first = 0, last = 0, valid = 0;
+};
+
+template <bool NT>
+__device__ __forceinline__ void pstage_load2(PStage& st, const double* __restrict__ val,
+                                             const int32_t* __restrict__ col, int64_t ws,
+                                             int64_t be, int tid) {
+  const int64_t last = max((be - 1) & ~(int64_t)1, (int64_t)0);
+#pragma unroll
+  for (int q = 0; q < kPSlots; ++q) {
+    const int64_t g0 = min(ws + (int64_t)(tid + q * kBlock) * 2, last);
+    if constexpr (NT)
+      st.v[q] = __builtin_nontemporal_load(reinterpret_cast<const dbl2v*>(val + g0));
+    else
+      st.v[q] = *reinterpret_cast<const dbl2v*>(val + g0);
+    st.c[q] = *reinterpret_cast<const int2v*>(col + g0);
+  }
+}
+
+template <typename RP, int EPI, bool DB, bool NT>
+__global__ __launch_bounds__(kBlock) void spmv_kernel_prod2(SpmvArgs a) {
+  using T = EpiTraits<EPI>;
+  constexpr int NP = T::NP;
+  constexpr int NV = T::NV;
+  constexpr int NB = DB ? 2 : 1;  // product buffers
+  constexpr int NE = 2 * kPSlots;  // entries per lane per window
+  __shared__ __attribute__((aligned(16))) double s_p1[NB][kWindow];
+  __shared__ __attribute__((aligned(16))) double s_p2[NV == 2 ? NB : 1][NV == 2 ? kWindow : 2];
+  __shared__ double s_red[(NP > 0 ? NP : 1) * 4];
+
+  const RP* __restrict__ rowptr = static_cast<const RP*>(a.rowptr);
+  const double* __restrict__ val = a.val;
+  const int32_t* __restrict__ col = a.col;
+  const double* __restrict__ x1 = a.x1;
+  const double* __restrict__ x2 = a.x2;
+  const int tid = threadIdx.x;
+
+  double acc[NP > 0 ? NP : 1];
+#pragma unroll
+  for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;
+
+  const int64_t nrb = (a.n + kBlock - 1) / kBlock;
+  RowSched sched;
+  sched.init(nrb, a.slab, a.slab_sub, true);
+  const int64_t jstep = sched.jstep, jcount = sched.jcount;
+  if (sched.j0 >= jcount) {
+    block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
+    return;
+  }
+  auto block_rows = [&](int64_t b) { return (int)min((int64_t)kBlock, a.n - b * kBlock); };
+  auto wstart = [](int64_t e) { return e & ~(int64_t)1; };
+
+  // Window generator: gj is the schedule index of the block of the newest
+  // window, (bsn, ben) the bounds of the block after it (scalar cache).
+  int64_t gj = sched.j0, bsn = 0, ben = 0;
+  auto fetch_next_bounds = [&]() {
+    if (gj + jstep < jcount) {
+      const int64_t rb = sched.rb(gj + jstep);
+      bsn = (int64_t)load_uniform(rowptr, rb * kBlock);
+      ben = (int64_t)load_uniform(rowptr, rb * kBlock + block_rows(rb));
+    }
+  };
+  PWin w0;
+  {
+    const int64_t rb = sched.rb(gj);
+    w0.r0 = rb * kBlock;
+    w0.nr = block_rows(rb);
+    w0.bs = (int64_t)load_uniform(rowptr, w0.r0);
+    w0.be = (int64_t)load_uniform(rowptr, w0.r0 + w0.nr);
+    w0.ws = wstart(w0.bs);
+    w0.first = 1;
+    w0.last = w0.ws + kWindow >= w0.be;
+    w0.valid = 1;
+  }
+  fetch_next_bounds();
+  auto advance = [&](const PWin& w) {
+    PWin o = w;
+    if (!w.valid) return o;
+    if (!w.last) {
+      o.ws = w.ws + kWindow;
+      o.first = 0;
+      o.last = o.ws + kWindow >= o.be;
+      return o;
+    }
+    if (gj + jstep >= jcount) {
+      o.valid = 0;
+      return o;
+    }
+    gj += jstep;
+    const int64_t rb = sched.rb(gj);
+    o.r0 = rb * kBlock;
+    o.nr = block_rows(rb);
+    o.bs = bsn;
+    o.be = ben;
+    o.ws = wstart(bsn);
+    o.first = 1;
+    o.last = o.ws + kWindow >= o.be;
+    fetch_next_bounds();
+    return o;
+  };
+
+  // stage registers: st = loads of the load-stage window; pv/g1/g2 = values
+  // and gathered x of the gather-stage window; row ranges of the sum-,
+  // gather- and load-stage windows' blocks (rlo_s/_g/_l)
+  PStage st;
+  dbl2v pv[kPSlots];
+  double g1[NE], g2[NV == 2 ? NE : 1];
+  RP rlo_l = 0, rhi_l = 0, rlo_g = 0, rhi_g = 0, rlo_s = 0, rhi_s = 0;
+  EpiIn pin_g, pin_s;
+  double sum1 = 0.0, sum2 = 0.0;
+  {
+    const int64_t ri = min(w0.r0 + tid, a.n - 1);
+    rlo_g = rowptr[ri];
+    rhi_g = rowptr[ri + 1];
+  }
+  pstage_load2<NT>(st, val, col, w0.ws, w0.be, tid);
+  PWin wsum, wg = w0;  // wsum invalid: the pipeline fills first
+  int it = 0;
+  for (;;) {
+    if (!wsum.valid && !wg.valid) break;
+    // (a) products of the sum-stage window (its gathers were issued last round)
+    if constexpr (!DB) __syncthreads();  // the single buffer's last readers are done
+    if (wsum.valid) {
+      double* p1 = s_p1[DB ? (it & 1) : 0];
+#pragma unroll
+      for (int q = 0; q < kPSlots; ++q) {
+        reinterpret_cast<dbl2v*>(p1)[tid + q * kBlock] =
+            dbl2v{pv[q].x * g1[2 * q], pv[q].y * g1[2 * q + 1]};
+        if constexpr (NV == 2) {
+          double* p2 = s_p2[DB ? (it & 1) : 0];
+          reinterpret_cast<dbl2v*>(p2)[tid + q * kBlock] =
+              dbl2v{pv[q].x * g2[2 * q], pv[q].y * g2[2 * q + 1]};
+        }
+      }
+    }
+    // (b) gather stage: the gather-stage window's loads have landed. A slot
+    // holds entries (e, e+1) of a real chunk (pstage_load2's clamp), but the
+    // second entry of the last chunk can lie past the matrix end: columns of
+    // entries at or past the block end are replaced by 0 (a valid x index;
+    // the product lands in a slot no row reads).
+    const int64_t wlast = max((wg.be - 1) & ~(int64_t)1, (int64_t)0);
+#pragma unroll
+    for (int q = 0; q < kPSlots; ++q) {
+      pv[q] = st.v[q];
+      const int64_t e0 = min(wg.ws + (int64_t)(tid + q * kBlock) * 2, wlast);
+      const int c0 = e0 < wg.be ? st.c[q].x : 0;
+      const int c1 = e0 + 1 < wg.be ? st.c[q].y : 0;
+      g1[2 * q] = x1[c0];
+      g1[2 * q + 1] = x1[c1];
+      if constexpr (NV == 2) {
+        g2[2 * q] = x2[c0];
+        g2[2 * q + 1] = x2[c1];
+      }
+    }
+    if (wg.valid && wg.last) pin_g = epi_load<EPI>(a, min(wg.r0 + tid, a.n - 1));
+    // (c) load stage: the window after the gather-stage one (row range first)
+    const PWin wl = advance(wg);
+    if (wl.valid && wl.first) {  // a new block: its row ranges
+      const int64_t ri = min(wl.r0 + tid, a.n - 1);
+      rlo_l = rowptr[ri];
+      rhi_l = rowptr[ri + 1];
+    } else {  // same block as the gather-stage window
+      rlo_l = rlo_g;
+      rhi_l = rhi_g;
+    }
+    const PWin& wld = wl.valid ? wl : wg;  // drained: re-issue valid addresses
+    pstage_load2<NT>(st, val, col, wld.ws, wld.be, tid);
+    // (d) sum the sum-stage window's rows, in stored order
+    __syncthreads();
+    if (wsum.valid) {
+      const double* p1 = s_p1[DB ? (it & 1) : 0];
+      const double* p2 = s_p2[NV == 2 && DB ? (it & 1) : 0];
+      if (wsum.first) {
+        sum1 = 0.0;
+        sum2 = 0.0;
+      }
+      if (tid < wsum.nr) {
+        const int js = (int)max((int64_t)rlo_s - wsum.ws, (int64_t)0);
+        const int je = (int)min((int64_t)rhi_s - wsum.ws, (int64_t)kWindow);
+        for (int j = js; j < je; ++j) {
+          sum1 = sum1 + p1[j];
+          if constexpr (NV == 2) sum2 = sum2 + p2[j];
+        }
+        if (wsum.last) epi_row_in<EPI>(a, wsum.r0 + tid, sum1, sum2, x1, x2, pin_s, acc);
+      }
+    }
+    // rotate the stages
+    wsum = wg;
+    wg = wl;
+    rlo_s = rlo_g;
+    rhi_s = rhi_g;
+    rlo_g = rlo_l;
+    rhi_g = rhi_l;
+    pin_s = pin_g;
+    ++it;
+  }
+  __syncthreads();
+  block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
+}
+
 // The offset-mask row walk (SpmvArgs::mask); false if not applicable.
 template <typename RP, int E, bool VEC>
 bool spmv_masked(const SpmvArgs& a, dim3 grid, dim3 block, hipStream_t s) {
@@ -1260,43 +1298,34 @@ bool spmv_masked(const SpmvArgs& a, dim3 grid, dim3 block, hipStream_t s) {
 template <typename RP, bool VEC, int E>
 void spmv_dispatch_epi(const SpmvArgs& a, int nblocks, hipStream_t s) {
   const dim3 grid(nblocks), block(kBlock);
-  // Row walk v2 with a non-temporal matrix stream (13; +1 % over 10) for short
-  // rows, product-then-sum (8) for long rows. The
-  // KR_SPMV_VARIANT environment variable overrides the choice for A/B runs
-  // (tools/spmv_micro.py): 0 row walk v1, 1 no prefetch, 2 wave-independent, 3 4-deep gathers,
-  // 6 no XCD schedule, 7 non-temporal staging, 9 8-deep gathers. Fused steps
-  // instantiate only the production kernels (row walk, offset masks,
-  // product-then-sum); the A/B variants fall back to the row walk for them.
+  // Short rows: row walk v2 with a non-temporal matrix stream (13). Long rows
+  // (SpmvArgs::long_rows): product-then-sum v2 (14; C3 +5 %). KR_SPMV_VARIANT
+  // overrides for A/B runs: 0 row walk v1, 8 product-then-sum v1, 10 row
+  // walk v2 with plain loads, 12 row walk v2 single-buffered, 15
+  // product-then-sum v2 with plain loads.
   const char* env = getenv("KR_SPMV_VARIANT");
-  int variant = env ? atoi(env) : (a.long_rows ? 8 : 13);
-  if ((variant == 10 || variant == 12 || variant == 13) && a.nnz_total < 4)
-    variant = 0;  // v2 needs 4 entries
+  // Two-vector long-row SpMVs stay on v1: v2's extra gather registers cost a
+  // wave per SIMD there (144 VGPRs) and it measured 7 % slower (C5 dual).
+  int variant = env ? atoi(env) : (a.long_rows ? (EpiTraits<E>::NV == 1 ? 14 : 8) : 13);
+  // the v2 kernels need 16-byte aligned bases and >= 4 entries
+  if (variant >= 10 && (!VEC || a.nnz_total < 4)) variant = a.long_rows ? 8 : 0;
+  if constexpr (VEC) {
+    switch (variant) {
+      case 10: spmv2_launch<RP, E, VEC>(a, grid, block, s); return;
+      case 12: spmv2_launch<RP, E, VEC, false>(a, grid, block, s); return;
+      case 13: spmv2_launch<RP, E, VEC, true, true>(a, grid, block, s); return;
+      case 14:
+        spmv_kernel_prod2<RP, E, EpiTraits<E>::NV == 1, true><<<grid, block, 0, s>>>(a);
+        return;
+      case 15:
+        spmv_kernel_prod2<RP, E, EpiTraits<E>::NV == 1, false><<<grid, block, 0, s>>>(a);
+        return;
+      default: break;
+    }
+  }
   if (variant == 8) {
     spmv_kernel_prod<RP, E, VEC><<<grid, block, 0, s>>>(a);
     return;
-  }
-  if (variant == 10) {
-    spmv2_launch<RP, E, VEC>(a, grid, block, s);
-    return;
-  }
-  if (variant == 12) {  // row walk v2, single-buffered window (A/B)
-    spmv2_launch<RP, E, VEC, false>(a, grid, block, s);
-    return;
-  }
-  if (variant == 13) {  // row walk v2, non-temporal matrix stream (A/B)
-    spmv2_launch<RP, E, VEC, true, true>(a, grid, block, s);
-    return;
-  }
-  if constexpr (!is_step<E>()) {
-    switch (variant) {
-      case 1: spmv_kernel_simple<RP, E, VEC><<<grid, block, 0, s>>>(a); return;
-      case 2: spmv_kernel_wave<RP, E, VEC><<<grid, block, 0, s>>>(a); return;
-      case 3: spmv_kernel<RP, E, VEC, 4><<<grid, block, 0, s>>>(a); return;
-      case 9: spmv_kernel<RP, E, VEC, 8><<<grid, block, 0, s>>>(a); return;
-      case 6: spmv_kernel<RP, E, VEC, kGather, false><<<grid, block, 0, s>>>(a); return;
-      case 7: spmv_kernel<RP, E, VEC, kGather, true, true><<<grid, block, 0, s>>>(a); return;
-      default: break;
-    }
   }
   if (!(a.mask && spmv_masked<RP, E, VEC>(a, grid, block, s)))
     spmv_kernel<RP, E, VEC><<<grid, block, 0, s>>>(a);

@@ -69,11 +69,11 @@ MATRICES = {
 }
 
 
-@pytest.mark.parametrize("variant", ["0", "8", "10"])
+@pytest.mark.parametrize("variant", ["0", "8", "10", "14"])
 @pytest.mark.parametrize("name", list(MATRICES))
 @pytest.mark.parametrize("rp64", [0, 1])
 def test_spmv_bitwise_vs_scipy(torch_dev, monkeypatch, name, rp64, variant):
-    """The SpMV kernels (row walk v1 0 and v2 10, product-then-sum 8) are
+    """The SpMV kernels (row walk v1 0 and v2 10, product-then-sum v1 8 and v2 14) are
     bitwise scipy."""
     monkeypatch.setenv("KR_SPMV_VARIANT", variant)
     A = MATRICES[name]()
