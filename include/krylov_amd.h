@@ -137,6 +137,15 @@ int kr_system_destroy(kr_system* sys);
 int kr_system_adopt_csr(kr_system* sys, int shard, const void* rowptr_dev, int rowptr64,
                         int32_t* col_dev, const double* val_dev);
 
+/* Adopt a DENSE row block already resident on the shard's device: rows
+ * row_begin[s]..row_begin[s+1] of A as a row-major (n_local x n_global)
+ * float64 array with leading dimension ld >= n_global (global columns).
+ * Replaces the reference's np.ndarray branch of MultiGpu.alloc
+ * (v3/gpu/common.py:100-101, v3/gpu/mpi/common.py:124-125), whose product is
+ * a cuBLAS dgemv; here a wave-per-row GEMV with the same fused epilogues as
+ * the SpMV. The caller keeps the buffer alive until kr_system_destroy. */
+int kr_system_adopt_dense(kr_system* sys, int shard, const double* a_dev, int64_t ld);
+
 /* Generate this shard's rows of a synthetic SPD matrix on the device.
  * dim = 2 or 3: 5-/7-point Poisson on an n_side^dim grid, lexicographic
  * order, diagonal 2*dim, off-diagonals -1 (scipy kronsum of tridiag(-1,2,-1)).

@@ -76,6 +76,7 @@ _SIGNATURES = {
     "kr_system_create": [_PP, _I64, _I, _PI, _PI64, _P],
     "kr_system_destroy": [_P],
     "kr_system_adopt_csr": [_P, _I, _P, _I, _P, _P],
+    "kr_system_adopt_dense": [_P, _I, _P, _I64],
     "kr_system_gen_poisson": [_P, _I, _I64],
     "kr_system_gen_banded": [_P, _I, _I64, _U64, _I],
     "kr_system_finalize": [_P],

@@ -422,6 +422,18 @@ void generate(kr_system* sys, int rowptr64_req, int max_row_nnz, Count count, Fi
 
 extern "C" {
 
+int kr_system_adopt_dense(kr_system* sys, int shard, const double* a, int64_t ld) {
+  return guarded([&] {
+    KR_REQUIRE(sys && shard >= 0 && shard < (int)sys->shards.size(), "bad shard");
+    KR_REQUIRE(!sys->finalized, "system already finalized");
+    KR_REQUIRE(ld >= sys->n_global, "leading dimension < n_global");
+    Shard& s = sys->shards[shard];
+    KR_REQUIRE(a || s.n == 0, "NULL dense block");
+    s.dense = a;
+    s.dld = ld;
+  });
+}
+
 int kr_system_gen_poisson(kr_system* sys, int dim, int64_t n_side) {
   return guarded([&] {
     KR_REQUIRE(dim == 2 || dim == 3, "dim must be 2 or 3");

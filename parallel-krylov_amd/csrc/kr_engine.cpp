@@ -209,6 +209,12 @@ void System::finalize() {
   const int nranks = comm ? comm->nranks : 1;
   // 1. column range of every local block
   for (auto& s : shards) {
+    if (s.dense) {  // every row reaches every column
+      s.col_lo = s.n > 0 ? 0 : s.row0;
+      s.col_hi = s.n > 0 ? n_global - 1 : s.row0 + s.n - 1;
+      s.nnz = s.n * n_global;
+      continue;
+    }
     KR_REQUIRE(s.rowptr && s.col && s.val, "matrix of a shard is not set");
     KR_HIP_CHECK(hipSetDevice(s.dev));
     int64_t* d = nullptr;
@@ -280,7 +286,12 @@ void System::finalize() {
     }
     // 4. interior rows (every column owned), computed on global columns
     KR_HIP_CHECK(hipSetDevice(s.dev));
-    {
+    if (s.dense) {  // no interior rows when there are other shards
+      const bool alone = P == 1;
+      s.int_lo = 0;
+      s.int_hi = alone ? s.n : 0;
+      s.reach = n_global;
+    } else {
       int64_t* d = nullptr;
       KR_HIP_CHECK(hipMalloc(&d, 3 * sizeof(int64_t)));
       launch_interior(s.rowptr, s.rowptr64, s.n, s.col, s.row0, s.row0 + s.n - 1, d, s.stream);
@@ -304,15 +315,20 @@ void System::finalize() {
       KR_HIP_CHECK(hipStreamCreateWithFlags(&s.comm_stream, hipStreamNonBlocking));
     if (!s.ev_in) KR_HIP_CHECK(hipEventCreateWithFlags(&s.ev_in, hipEventDisableTiming));
     if (!s.ev_out) KR_HIP_CHECK(hipEventCreateWithFlags(&s.ev_out, hipEventDisableTiming));
-    // 5. rewrite columns to local numbering: local = global - row0 + pad
-    launch_col_shift(s.rowptr, s.rowptr64, s.n, s.col, s.pad - s.row0, s.stream);
-    // 6. offset masks for short-row blocks whose rows use at most 64 distinct
-    // column offsets (stencils, banded): the SpMV then reads a 1-8 byte mask
-    // per row instead of a 4-byte column per entry. KR_MASK=0 disables.
-    build_masks(s);
+    if (!s.dense) {
+      // 5. rewrite columns to local numbering: local = global - row0 + pad
+      launch_col_shift(s.rowptr, s.rowptr64, s.n, s.col, s.pad - s.row0, s.stream);
+      // 6. offset masks for short-row blocks whose rows use at most 64 distinct
+      // column offsets (stencils, banded): the SpMV then reads a 1-8 byte mask
+      // per row instead of a 4-byte column per entry. KR_MASK=0 disables.
+      build_masks(s);
+    }
     // 7. reduction buffers
     s.grid = default_grid(s.n);
-    s.spmv_grid = spmv_grid_for(s.n, s.reach);
+    // dense: one wave per row, 4 rows per workgroup
+    s.spmv_grid = s.dense ? (int)std::max<int64_t>(1, std::min<int64_t>((s.n + 3) / 4,
+                                                                         (int64_t)grid_cap() * 4))
+                          : spmv_grid_for(s.n, s.reach);
     s.pstride = std::max(s.grid, s.spmv_grid);
     s.slot_n.fill(0);
     KR_HIP_CHECK(hipMalloc(&s.partials, sizeof(double) * (size_t)kMaxSlots * s.pstride));
@@ -550,6 +566,13 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
     }
     a.epi_late = epi_late;
     a.nnz_total = s.nnz;
+    if (s.dense) {
+      a.dense = 1;
+      a.val = s.dense + r_begin * s.dld;
+      a.dld = s.dld;
+      a.ncols = n_global;
+      a.xcol0 = s.pad - s.row0;  // local index of global column 0
+    }
     if (step) {
       a.u1 = s.own(st->u1) + r_begin;
       a.u2 = s.own(st->u2) + r_begin;
@@ -567,6 +590,7 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
     // fused step: u1, u2 read and written (+ x read and written)
     const double extra = step ? (step_x ? 48.0 : 32.0) * s.n
                               : (b >= 0 || e >= 0) ? 8.0 * s.n : 0.0;
+    if (s.dense) return 8.0 * s.nnz + nv * 8.0 * (n_global + s.n) + extra;
     return 12.0 * s.nnz + (s.rowptr64 ? 8.0 : 4.0) * (s.n + 1) + nv * 16.0 * s.n + extra;
   };
   // The partial stride is s.pstride for every launch; the full / interior

@@ -60,6 +60,10 @@ struct Shard {
   int32_t* col = nullptr;
   const double* val = nullptr;
   int64_t nnz = 0;
+  // dense row block instead of CSR (kr_system_adopt_dense): n x n_global
+  // row-major, leading dimension dld, global column numbering
+  const double* dense = nullptr;
+  int64_t dld = 0;
   std::vector<void*> owned;
   // halo geometry: vector = [pad | n own rows | halo_hi]; halo_lo rows sit
   // just below the own rows (pad >= halo_lo, pad multiple of 8).

@@ -100,6 +100,10 @@ struct SpmvArgs {
   double c0 = 0, c1 = 0;
   int epi_late = 0;  // 1: load own-row epilogue operands at the row end (A/B, KR_EPI_LATE)
   int64_t nnz_total = -1;  // entries of val/col (-1: unknown; spmv_kernel2 needs >= 4)
+  // Dense row block (gemv_kernel): val is n x ncols row-major with leading
+  // dimension dld; x1 + xcol0 (x2 + xcol0) is the full input vector.
+  int dense = 0;
+  int64_t dld = 0, ncols = 0, xcol0 = 0;
 };
 // Mean row length from which the product-then-sum SpMV is used.
 constexpr double kLongRow = 12.0;

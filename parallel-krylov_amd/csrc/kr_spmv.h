@@ -1280,6 +1280,69 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_prod2(SpmvArgs a) {
   block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
 }
 
+// ---------------------------------------------------------------------------
+// Dense row block (the reference's np.ndarray A branch, v3/gpu/common.py:100-101
+// and v3/gpu/mpi/common.py:124-125, where cupy runs a cuBLAS dgemv). One wave
+// per row: lane l accumulates columns l, l+64, ... in order (8 independent
+// 512-byte loads in flight per lane), then a fixed shuffle tree reduces the
+// 64 partial sums -- deterministic, not sequential: dense parity is within
+// rounding, as the reference's own dgemv order differs from numpy's. The
+// epilogues (products, fused steps) are the SpMV's, applied by lane 0.
+// ---------------------------------------------------------------------------
+template <int EPI>
+__global__ __launch_bounds__(kBlock) void gemv_kernel(SpmvArgs a) {
+  using T = EpiTraits<EPI>;
+  constexpr int NP = T::NP;
+  constexpr int NV = T::NV;
+  constexpr int U = 8;
+  __shared__ double s_red[(NP > 0 ? NP : 1) * 4];
+  double acc[NP > 0 ? NP : 1];
+#pragma unroll
+  for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;
+  const int lane = threadIdx.x & 63;
+  const int64_t waves = (int64_t)gridDim.x * (kBlock / 64);
+  const double* __restrict__ xf1 = a.x1 + a.xcol0;
+  const double* __restrict__ xf2 = NV == 2 ? a.x2 + a.xcol0 : nullptr;
+  const int64_t nc = a.ncols;
+  for (int64_t row = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); row < a.n;
+       row += waves) {
+    const double* __restrict__ ar = a.val + row * a.dld;
+    double s1 = 0.0, s2 = 0.0;
+    int64_t c = lane;
+    for (; c + 64 * (U - 1) < nc; c += 64 * U) {
+      double av[U], p1[U], p2[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        av[u] = __builtin_nontemporal_load(ar + c + 64 * u);
+        p1[u] = xf1[c + 64 * u];
+        if constexpr (NV == 2) p2[u] = xf2[c + 64 * u];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        s1 = s1 + av[u] * p1[u];
+        if constexpr (NV == 2) s2 = s2 + av[u] * p2[u];
+      }
+    }
+    for (; c < nc; c += 64) {
+      const double av = ar[c];
+      s1 = s1 + av * xf1[c];
+      if constexpr (NV == 2) s2 = s2 + av * xf2[c];
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      s1 += __shfl_down(s1, off, 64);
+      if constexpr (NV == 2) s2 += __shfl_down(s2, off, 64);
+    }
+    if (lane == 0) {
+      const double* xo1 = a.x1;  // own-row operands use the halo-extended base
+      const double* xo2 = a.x2;
+      epi_row_in<EPI>(a, row, s1, s2, xo1, xo2, epi_load<EPI>(a, row), acc);
+    }
+  }
+  __syncthreads();
+  block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
+}
+
 // The offset-mask row walk (SpmvArgs::mask); false if not applicable.
 template <typename RP, int E, bool VEC>
 bool spmv_masked(const SpmvArgs& a, dim3 grid, dim3 block, hipStream_t s) {
@@ -1338,6 +1401,10 @@ void spmv_dispatch_epi(const SpmvArgs& a, int nblocks, hipStream_t s) {
 // parallel.
 template <int E>
 void spmv_launch_epi(const SpmvArgs& a, int nblocks, hipStream_t s) {
+  if (a.dense) {
+    gemv_kernel<E><<<nblocks, kBlock, 0, s>>>(a);
+    return;
+  }
   // 16-byte staging needs 16-byte aligned val/col bases
   const bool vec = ((reinterpret_cast<uintptr_t>(a.val) | reinterpret_cast<uintptr_t>(a.col)) &
                     15) == 0;

@@ -49,6 +49,14 @@ def balanced_partition(n: int, parts: int) -> list:
     return out
 
 
+def _is_tensor(v) -> bool:
+    try:
+        import torch
+        return isinstance(v, torch.Tensor)
+    except ImportError:  # pragma: no cover
+        return False
+
+
 def visible_devices() -> list:
     """Shard -> device map for the single-process family.
 
@@ -196,10 +204,31 @@ class KrylovSystem:
         call("kr_system_adopt_csr", self.handle, s, t_rp.data_ptr(), int(rp64),
              t_col.data_ptr(), t_val.data_ptr())
 
+    def adopt_dense(self, s: int, block) -> None:
+        """Upload the dense row block of shard s (its rows x all N columns,
+        a numpy array or tensor): the GEMV path (v3/gpu/common.py:100-101)."""
+        torch = _torch()
+        blk = block if _is_tensor(block) else np.asarray(block)
+        if blk.ndim != 2 or blk.shape[1] != self.n_global:
+            raise ValueError(f"dense block must be (rows, {self.n_global})")
+        if _is_tensor(blk):
+            t = blk.to(device=self.device(s), dtype=torch.float64).contiguous()
+        else:
+            t = torch.from_numpy(np.require(blk, np.float64, ["C", "W"])).to(self.device(s))
+        torch.cuda.synchronize(self.device(s))
+        self._keep.append(t)
+        call("kr_system_adopt_dense", self.handle, s, t.data_ptr(), int(t.shape[1]))
+
     def set_matrix(self, A) -> None:
-        """Distribute a whole matrix (scipy sparse or dense ndarray) over the
-        local shards (in-process family)."""
+        """Distribute a whole matrix over the local shards (in-process
+        family): scipy sparse (any format) as CSR, a dense ndarray/tensor as
+        dense row blocks (GEMV), like the reference's two branches."""
         import scipy.sparse as sp
+        if not sp.issparse(A) and (isinstance(A, np.ndarray) or _is_tensor(A)):
+            for s in range(self.nshards):
+                r0, r1 = self.shard_rows(s)
+                self.adopt_dense(s, A[r0:r1])
+            return
         A = sp.csr_matrix(A) if not sp.isspmatrix_csr(A) else A
         for s in range(self.nshards):
             r0, r1 = self.shard_rows(s)
@@ -374,7 +403,8 @@ def system_from_matrix(A, devices=None) -> KrylovSystem:
     """Single-process system over ``devices`` (default: all visible GPUs)."""
     import scipy.sparse as sp
     devices = visible_devices() if devices is None else list(devices)
-    A = sp.csr_matrix(A) if not sp.isspmatrix_csr(A) else A
+    if sp.issparse(A):
+        A = sp.csr_matrix(A) if not sp.isspmatrix_csr(A) else A
     n = A.shape[0]
     sysm = KrylovSystem(n, balanced_partition(n, len(devices)), devices)
     sysm.set_matrix(A)

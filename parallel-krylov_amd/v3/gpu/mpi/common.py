@@ -114,8 +114,10 @@ def run(method, banner, comm, local_A, b, x=None, tol=1e-05, maxiter=None, k=Non
     comm_h = d.communicator(device)
     sysm = KrylovSystem(N, [row0, row0 + local_n], [device], comm=comm_h)
     try:
-        block = local_A if sp.issparse(local_A) else sp.csr_matrix(np.asarray(local_A))
-        sysm.adopt_csr(0, block)
+        if sp.issparse(local_A):
+            sysm.adopt_csr(0, local_A)
+        else:  # dense row block: GEMV path (v3/gpu/mpi/common.py:124-125)
+            sysm.adopt_dense(0, local_A)
         sysm.finalize()
         b_parts = [torch.from_numpy(np.ascontiguousarray(bh[row0:row0 + local_n])).to(
             torch.device("cuda", device))]

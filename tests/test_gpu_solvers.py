@@ -227,3 +227,83 @@ def test_fused_steps_bitwise_equal_unfused(monkeypatch, shards, method, matrix, 
         if "khistory" in i0:
             np.testing.assert_array_equal(i1["khistory"], i0["khistory"])
         np.testing.assert_array_equal(x1, x0)
+
+
+def _dense_spd(n, seed):
+    """Dense SPD matrix with no zero entry (every entry is used by the GEMV)."""
+    rng = np.random.default_rng(seed)
+    B = rng.uniform(0.5, 1.5, size=(n, n)) / n
+    return B @ B.T + np.diag(rng.uniform(1.0, 2.0, size=n))
+
+
+@pytest.mark.parametrize("shards", ["0", "0,0,0"])
+def test_dense_gemv_matches_numpy(monkeypatch, shards):
+    """Dense A (the reference's np.ndarray branch, v3/gpu/common.py:100-101)
+    runs the GEMV kernel: y = A x within rounding of numpy's dgemv (the order
+    differs: per-lane column sums + a fixed tree), sharded or not."""
+    from parallel_krylov_amd.system import KrylovSystem, balanced_partition, visible_devices
+    monkeypatch.setenv("KRYLOV_AMD_SHARDS", shards)
+    A = _dense_spd(700, 1)
+    n = A.shape[0]
+    devs = visible_devices()
+    sysm = KrylovSystem(n, balanced_partition(n, len(devs)), devs)
+    sysm.set_matrix(A)
+    sysm.finalize()
+    x = np.random.default_rng(2).standard_normal(n)
+    y = sysm.gather(sysm.spmv(sysm.split(x))).cpu().numpy()
+    ref = A @ x
+    assert np.max(np.abs(y - ref)) <= 1e-13 * np.max(np.abs(A) @ np.abs(x))
+    sysm.close()
+
+
+@pytest.mark.parametrize("method,k", [("cg", None), ("mrr", None), ("kskipcg", 2),
+                                      ("kskipmrr", 3), ("adaptivekskipmrr", 4)])
+def test_dense_solvers_match_oracle(method, k):
+    """All five solvers on a dense A through the drop-in API, against the
+    oracle (v3/cpu on the same dense ndarray). Dense products differ from
+    numpy's in order only, so the histories agree to rounding: same
+    iteration count, residuals within 1e-9 relative while above 1e-8 (1e-6
+    for the k-skip methods, whose recurrences amplify rounding)."""
+    from oracle import v3cpu
+    A = _dense_spd(500, 3)
+    b = np.random.default_rng(4).standard_normal(A.shape[0])
+    kw = dict(tol=1e-10, maxiter=300)
+    if k is not None:
+        kw["k"] = k
+    with contextlib.redirect_stdout(io.StringIO()):
+        x, info = _solver(method)(A, b, **kw)
+    x_ref, info_ref = v3cpu.METHODS[method](A, b, **kw)
+    np.testing.assert_array_equal(info["nosl"], info_ref["nosl"])
+    res, gres = info["residual"], info_ref["residual"]
+    big = gres > 1e-8
+    # k-skip recurrences amplify rounding differences (SURVEY.md 8c envelope)
+    rtol = 1e-9 if k is None else 1e-6
+    assert np.all(np.abs(res[big] - gres[big]) <= rtol * gres[big])
+    assert res[-1] < kw["tol"]
+    xh = x.cpu().numpy()
+    assert np.linalg.norm(xh - x_ref) <= 1e-8 * np.linalg.norm(x_ref)
+
+
+def test_dense_mpi_single_rank(dist_single):
+    """The MPI family with a dense local_A block (v3/gpu/mpi/common.py:124-125)."""
+    from oracle import v3cpu
+    A = _dense_spd(300, 5)
+    b = np.random.default_rng(6).standard_normal(A.shape[0])
+    with contextlib.redirect_stdout(io.StringIO()):
+        x, info = _solver("kskipmrr", "gpu.mpi")(None, A, b, tol=1e-10, k=2)
+    x_ref, info_ref = v3cpu.kskipmrr(A, b, tol=1e-10, k=2)
+    np.testing.assert_array_equal(info["nosl"], info_ref["nosl"])
+    assert np.linalg.norm(x.cpu().numpy() - x_ref) <= 1e-8 * np.linalg.norm(x_ref)
+
+
+@pytest.mark.parametrize("shards", ["0", "0,0"])
+def test_dense_fused_steps_bitwise_equal_unfused(monkeypatch, shards):
+    """The fused k-skip steps in the GEMV epilogue == separate vector steps."""
+    A = _dense_spd(400, 7)
+    b = np.random.default_rng(8).standard_normal(A.shape[0])
+    base = {"KRYLOV_AMD_SHARDS": shards}
+    kw = dict(tol=1e-10, maxiter=200, k=3)
+    x0, i0 = _run_env(monkeypatch, {**base, "KR_FUSE": "0"}, "kskipmrr", A, b, **kw)
+    x1, i1 = _run_env(monkeypatch, {**base, "KR_FUSE": "1"}, "kskipmrr", A, b, **kw)
+    np.testing.assert_array_equal(i1["residual"], i0["residual"])
+    np.testing.assert_array_equal(x1, x0)
