@@ -626,6 +626,7 @@ int kr_solve_history(kr_system* sys, double* residual, int64_t* nosl, int64_t* k
 int kr_solve_kernel_stats(kr_system* sys, kr_kernel_stat* stats, int cap, int* count) {
   return guarded([&] {
     KR_REQUIRE(sys && count, "NULL argument");
+    sys->harvest_profile();  // events still pending (harvested lazily, see reduce)
     int c = 0;
     if (!sys->shards.empty()) {
       for (auto& kv : sys->shards[0].stats) {
