@@ -201,7 +201,8 @@ typedef struct {
   int k;           /* k-skip depth (ignored by CG/MrR) */
   double tol;      /* relative residual tolerance */
   int64_t maxiter; /* <= 0: n_global (reference default, v3/gpu/common.py:35) */
-  int profile;     /* != 0: per-kernel HIP-event timing */
+  int profile;     /* N > 0: per-kernel HIP-event timing on every N-th outer
+                     iteration (1 = all; events cost ~10 us per kernel) */
 } kr_solve_params;
 
 typedef struct {

@@ -561,6 +561,9 @@ int kr_solve_begin(kr_system* sys, const kr_solve_params* params, const double* 
     sys->session.reset();
     for (auto& s : sys->shards) s.stats.clear();
     sys->profile = params->profile != 0;
+    sys->profile_every = params->profile > 0 ? params->profile : 1;
+    sys->prof_tick = 0;
+    sys->prof_active = true;
     sys->session = make_session(sys, *params);
     sys->session->begin(b, x0);
   });
@@ -571,7 +574,11 @@ int kr_solve_step(kr_system* sys, int64_t max_outer, int* done) {
     KR_REQUIRE(sys, "NULL system");
     if (!sys->session) throw Failure(KR_ERR_STATE, "kr_solve_begin was not called");
     Session& ss = *sys->session;
-    for (int64_t c = 0; c < max_outer && !ss.done; ++c) ss.step_once();
+    for (int64_t c = 0; c < max_outer && !ss.done; ++c) {
+      // profile = N: per-kernel events on every N-th outer iteration only
+      sys->prof_active = (sys->prof_tick++ % sys->profile_every) == 0;
+      ss.step_once();
+    }
     if (done) *done = ss.done ? 1 : 0;
   });
 }

@@ -377,7 +377,8 @@ void System::alloc_vectors(int count) {
 
 void System::prof_begin(Shard& s, const char* name, hipEvent_t& t0) {
   (void)name;
-  if (!profile) return;
+  t0 = nullptr;
+  if (!profile || !prof_active) return;
   if (s.event_pool.empty()) {
     hipEvent_t e;
     KR_HIP_CHECK(hipEventCreate(&e));
@@ -389,7 +390,7 @@ void System::prof_begin(Shard& s, const char* name, hipEvent_t& t0) {
 }
 
 void System::prof_end(Shard& s, const char* name, hipEvent_t t0, double bytes) {
-  if (!profile) return;
+  if (!profile || !t0) return;
   if (s.event_pool.empty()) {
     hipEvent_t e;
     KR_HIP_CHECK(hipEventCreate(&e));

@@ -126,6 +126,9 @@ struct System {
   int first_global = 0;             // global index of shards[0]
   bool finalized = false;
   bool profile = false;
+  int profile_every = 1;            // events on every profile_every-th outer iteration
+  int64_t prof_tick = 0;
+  bool prof_active = true;
   bool overlap = true;              // split SpMV: interior rows || halo exchange
   bool fuse_steps = true;           // k-skip steps fused into the SpMV epilogue
   int epi_late = 0;                 // SpmvArgs::epi_late (A/B knob)

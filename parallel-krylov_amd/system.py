@@ -320,7 +320,7 @@ class KrylovSystem:
             raise ValueError(f"unknown method {method!r}")
         prm = _lib.SolveParams(method=_lib.KR_METHOD[method], k=int(k or 0), tol=float(tol),
                                maxiter=-1 if maxiter is None else int(maxiter),
-                               profile=1 if profile else 0)
+                               profile=int(profile) if profile else 0)
         for s in range(self.nshards):
             torch.cuda.synchronize(self.device(s))
         b_arr = ptr_array([t.data_ptr() for t in b_parts])
@@ -338,7 +338,7 @@ class KrylovSystem:
             self.finalize()
         prm = _lib.SolveParams(method=_lib.KR_METHOD[method], k=int(k or 0), tol=float(tol),
                                maxiter=-1 if maxiter is None else int(maxiter),
-                               profile=1 if profile else 0)
+                               profile=int(profile) if profile else 0)
         for s in range(self.nshards):
             torch.cuda.synchronize(self.device(s))
         b_arr = ptr_array([t.data_ptr() for t in b_parts])
