@@ -71,6 +71,7 @@ const char* epi_name(SpmvEpi e) {
     case EPI_STEP_MRR_X2: return "spmv_step_mrr_x2";
     case EPI_STEP_MRR_X: return "spmv_step_mrr_x";
     case EPI_STEP_KCG: return "spmv_step_kcg";
+    case EPI_STEP_MRR_FIRST2: return "spmv_step_mrr_first2";
   }
   return "spmv?";
 }
@@ -356,6 +357,16 @@ void System::finalize() {
     // row-block start (KR_EPI_LATE=0): late measured 1-3 % faster on C4.
     const char* el = getenv("KR_EPI_LATE");
     epi_late = el ? atoi(el) != 0 : 1;
+    // Steps 0 and 1 in one SpMV: row walk v2 only (short rows, 16-byte
+    // aligned CSR with >= 4 entries, no dense shard, no forced v1 kernel).
+    const char* ff = getenv("KR_FUSE_FIRST");
+    const char* sv = getenv("KR_SPMV_VARIANT");
+    bool v2 = !sv || atoi(sv) == 10 || atoi(sv) == 12 || atoi(sv) == 13;
+    for (auto& s : shards)
+      if (s.dense || s.nnz < 4 ||
+          ((reinterpret_cast<uintptr_t>(s.val) | reinterpret_cast<uintptr_t>(s.col)) & 15))
+        v2 = false;
+    fuse_first = fuse_steps && !long_rows && v2 && !(ff && atoi(ff) == 0);
   }
   finalized = true;
 }
@@ -420,7 +431,7 @@ void System::harvest_profile() {
   }
 }
 
-void System::halo(int id1, int id2) {
+void System::halo(int id1, int id2, int id3) {
   if (comm) {
     Shard& s = shards[0];
     if (s.recv.empty() && s.send.empty()) return;
@@ -429,7 +440,7 @@ void System::halo(int id1, int id2) {
     double bytes = 0;
     KR_HIP_CHECK(hipSetDevice(s.dev));
     KR_NCCL_CHECK(ncclGroupStart());
-    for (int id : {id1, id2}) {
+    for (int id : {id1, id2, id3}) {
       if (id < 0) continue;
       for (auto& p : s.send) {
         KR_NCCL_CHECK(ncclSend(s.vec[id] + s.local_index(p.g0), (size_t)p.count, ncclFloat64,
@@ -456,7 +467,7 @@ void System::halo(int id1, int id2) {
     for (auto& p : s.recv) {
       Shard& t = shards[p.peer];
       KR_HIP_CHECK(hipStreamWaitEvent(s.stream, t.ev_a, 0));
-      for (int id : {id1, id2}) {
+      for (int id : {id1, id2, id3}) {
         if (id < 0) continue;
         double* dst = s.vec[id] + s.local_index(p.g0);
         const double* src = t.vec[id] + t.local_index(p.g0);
@@ -477,13 +488,13 @@ void System::halo(int id1, int id2) {
   }
 }
 
-void System::halo_async(int id1, int id2) {
+void System::halo_async(int id1, int id2, int id3) {
   if (comm) {
     Shard& s = shards[0];
     KR_HIP_CHECK(hipSetDevice(s.dev));
     KR_HIP_CHECK(hipStreamWaitEvent(s.comm_stream, s.ev_in, 0));
     KR_NCCL_CHECK(ncclGroupStart());
-    for (int id : {id1, id2}) {
+    for (int id : {id1, id2, id3}) {
       if (id < 0) continue;
       for (auto& p : s.send)
         KR_NCCL_CHECK(ncclSend(s.vec[id] + s.local_index(p.g0), (size_t)p.count, ncclFloat64,
@@ -501,7 +512,7 @@ void System::halo_async(int id1, int id2) {
     for (auto& p : s.recv) {
       Shard& t = shards[p.peer];
       KR_HIP_CHECK(hipStreamWaitEvent(s.comm_stream, t.ev_in, 0));
-      for (int id : {id1, id2}) {
+      for (int id : {id1, id2, id3}) {
         if (id < 0) continue;
         double* dst = s.vec[id] + s.local_index(p.g0);
         const double* src = t.vec[id] + t.local_index(p.g0);
@@ -520,12 +531,17 @@ void System::halo_async(int id1, int id2) {
 void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int b,
                   int slot0, const StepOps* st) {
   const bool dual = (epi == EPI_DUAL_NONE || epi == EPI_DUAL_MRR || epi == EPI_DUAL_KCG);
+  const bool virt = epi == EPI_STEP_MRR_FIRST2;
   const bool step = (epi == EPI_STEP_MRR_NOX || epi == EPI_STEP_MRR_X2 ||
-                     epi == EPI_STEP_MRR_X || epi == EPI_STEP_KCG);
+                     epi == EPI_STEP_MRR_X || epi == EPI_STEP_KCG || virt);
   KR_REQUIRE(!step || (st && st->u1 >= 0 && st->u2 >= 0 && out1 != in1),
              "fused step: operands missing or output aliases the input");
-  const bool step_x = (epi == EPI_STEP_MRR_X2 || epi == EPI_STEP_MRR_X);
+  const bool step_x = (epi == EPI_STEP_MRR_X2 || epi == EPI_STEP_MRR_X || virt);
   KR_REQUIRE(!step_x || (st->us >= 0 && st->ud >= 0), "fused step: x operands missing");
+  KR_REQUIRE(!virt || (in2 >= 0 && st->x3 >= 0 && st->u1 != in2 && st->u1 != st->x3),
+             "fused first step: y0/Ar1 missing or y written over a gathered input");
+  const int hx2 = (dual || virt) ? in2 : -1;  // vectors whose halo the SpMV reads
+  const int hx3 = virt ? st->x3 : -1;
   KR_REQUIRE(slot0 + spmv_products(epi) <= kMaxSlots, "reduction slots exhausted");
   const bool exchange =
       comm ? !(shards[0].recv.empty() && shards[0].send.empty()) : shards.size() > 1;
@@ -547,7 +563,7 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
     a.val = s.val;
     a.n = rows;
     a.x1 = s.vec[in1];
-    a.x2 = dual ? s.vec[in2] : nullptr;
+    a.x2 = (dual || virt) ? s.vec[in2] : nullptr;
     a.xoff = s.pad + r_begin;
     a.y1 = s.own(out1) + r_begin;
     a.y2 = dual ? s.own(out2) + r_begin : nullptr;
@@ -583,14 +599,22 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
       }
       a.c0 = st->c0;
       a.c1 = st->c1;
+      if (virt) {
+        a.x3 = s.vec[st->x3];
+        a.c2 = st->c2;
+        a.c3 = st->c3;
+      }
     }
     return a;
   };
   auto bytes_of = [&](Shard& s) {
     const double nv = dual ? 2.0 : 1.0;
     // fused step: u1, u2 read and written (+ x read and written)
-    const double extra = step ? (step_x ? 48.0 : 32.0) * s.n
-                              : (b >= 0 || e >= 0) ? 8.0 * s.n : 0.0;
+    // fused first step: inputs r0, y0, Ar1 (3 x 8N, one counted below as
+    // x), z and x read, y z r x written
+    const double extra = virt ? 64.0 * s.n
+                         : step ? (step_x ? 48.0 : 32.0) * s.n
+                                : (b >= 0 || e >= 0) ? 8.0 * s.n : 0.0;
     if (s.dense) return 8.0 * s.nnz + nv * 8.0 * (n_global + s.n) + extra;
     return 12.0 * s.nnz + (s.rowptr64 ? 8.0 : 4.0) * (s.n + 1) + nv * 16.0 * s.n + extra;
   };
@@ -610,7 +634,7 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
   };
 
   if (!split) {
-    halo(in1, dual ? in2 : -1);
+    halo(in1, hx2, hx3);
     for (auto& s : shards) {
       KR_HIP_CHECK(hipSetDevice(s.dev));
       hipEvent_t t0 = nullptr;
@@ -627,7 +651,7 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
     prof_begin(s, nm, t0s[li]);
     KR_HIP_CHECK(hipEventRecord(s.ev_in, s.stream));
   }
-  halo_async(in1, dual ? in2 : -1);
+  halo_async(in1, hx2, hx3);
   for (auto& s : shards) {  // interior rows: all blocks write their partials
     KR_HIP_CHECK(hipSetDevice(s.dev));
     launch_full(s, s.int_lo, s.int_hi - s.int_lo);
@@ -853,29 +877,33 @@ class KskipMrrSession : public Base {
   // vector ids: fixed ones, then Ar[0..k0+1], Ay[0..k0]. Ar[0] (r) lives in
   // one of two buffers, r0 / r_alt: a fused step SpMV reads r from one and
   // writes the next r into the other (other rows still gather the old r).
-  enum { XA, XB, B, Z, RALT, FIXED };
+  // Ay[0] (y) likewise alternates between y0 / y_alt when steps 0 and 1 run
+  // in one SpMV (EPI_STEP_MRR_FIRST2 gathers y0 and writes the new y).
+  enum { XA, XB, B, Z, RALT, YALT, FIXED };
   int k0 = 0;
   bool adaptive = false;
   int cur = XA, pre = XB;  // current x buffer / adaptive snapshot buffer
   int xsrc = XA;           // source of the next x update
   int r0 = FIXED, r_alt = RALT;
+  int y0 = FIXED, y_alt = YALT;
   double pre_residual = 0;
   int AR(int j) const { return FIXED + j; }
   int AY(int j) const { return FIXED + (k0 + 2) + j; }
   static constexpr int kHead = 5;
   int gram_slots(int kk) const { return kHead + 7 * kk; }
 
-  void head() { sys->spmv(EPI_HEAD_MRR, r0, -1, AR(1), -1, AY(0), -1, 0); }
+  void head() { sys->spmv(EPI_HEAD_MRR, r0, -1, AR(1), -1, y0, -1, 0); }
   void chain(int kk) {
     for (int m = 0; m < kk; ++m)
-      sys->spmv(EPI_DUAL_MRR, AR(m + 1), AY(m), AR(m + 2), AY(m + 1), -1, -1, kHead + 7 * m);
+      sys->spmv(EPI_DUAL_MRR, AR(m + 1), m == 0 ? y0 : AY(m), AR(m + 2), AY(m + 1), -1, -1,
+                kHead + 7 * m);
   }
   // Initial / restart MrR step (v3/cpu/kskipmrr.py:26-31).
   void mrr_first(int x_from) {
     sys->spmv(EPI_XY, r0, -1, AR(1), -1, -1, -1, 0);
     const auto g = sys->reduce(3);
     const double zeta = g[1] / g[2];
-    sys->ew(EW_MRR_FIRST, 0, zeta, {AY(0), AR(1), Z, r0, x_from, cur}, 0);
+    sys->ew(EW_MRR_FIRST, 0, zeta, {y0, AR(1), Z, r0, x_from, cur}, 0);
     xsrc = cur;
   }
   // x -= z is deferred pairwise: step j stores z and leaves x (kind 0), step
@@ -894,6 +922,8 @@ class KskipMrrSession : public Base {
     sys->alloc_vectors(FIXED + (k0 + 2) + (k0 + 1));
     r0 = AR(0);
     r_alt = RALT;
+    y0 = AY(0);
+    y_alt = YALT;
     load_bx(B, XA, b, x0);
     if (adaptive) sys->copy_own(XB, XA);  // pre_x guard = x0
     sys->spmv(EPI_BMINUS, XA, -1, r0, -1, -1, B, 0);
@@ -971,19 +1001,40 @@ class KskipMrrSession : public Base {
     auto ew_step = [&](int j) {
       const int kind = step_kind(j);
       if (kind == 0) {
-        sys->ew(EW_MRR_NOX, eta[j], zeta[j], {AY(0), AR(1), Z, r0, -1, -1}, 0);
+        sys->ew(EW_MRR_NOX, eta[j], zeta[j], {y0, AR(1), Z, r0, -1, -1}, 0);
       } else {
         sys->ew(kind == 1 ? EW_MRR_X2 : EW_MRR, eta[j], zeta[j],
-                {AY(0), AR(1), Z, r0, xsrc, cur}, 0);
+                {y0, AR(1), Z, r0, xsrc, cur}, 0);
         xsrc = cur;
       }
     };
-    ew_step(0);
-    for (int j = 1; j <= k; ++j) {
+    int j1 = 1;
+    if (sys->fuse_steps && sys->fuse_first && k >= 1) {
+      // steps 0 (kind 0) and 1 (kind 1) in one SpMV: r1 is formed at every
+      // gathered column from r0, y0, Ar1; new y and r go to the other buffers
+      StepOps st;
+      st.u1 = y_alt;
+      st.u2 = Z;
+      st.us = xsrc;
+      st.ud = cur;
+      st.c0 = eta[0];
+      st.c1 = zeta[0];
+      st.x3 = AR(1);
+      st.c2 = eta[1];
+      st.c3 = zeta[1];
+      sys->spmv(EPI_STEP_MRR_FIRST2, r0, y0, r_alt, -1, -1, -1, 0, &st);
+      xsrc = cur;
+      std::swap(r0, r_alt);
+      std::swap(y0, y_alt);
+      j1 = 2;
+    } else {
+      ew_step(0);
+    }
+    for (int j = j1; j <= k; ++j) {
       if (sys->fuse_steps) {
         const int kind = step_kind(j);
         StepOps st;
-        st.u1 = AY(0);
+        st.u1 = y0;
         st.u2 = Z;
         if (kind != 0) {
           st.us = xsrc;

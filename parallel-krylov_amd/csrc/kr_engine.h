@@ -111,6 +111,8 @@ class Session;
 struct StepOps {
   int u1 = -1, u2 = -1, us = -1, ud = -1;
   double c0 = 0, c1 = 0;
+  int x3 = -1;          // EPI_STEP_MRR_FIRST2: Ar1 (gathered with r0 = in1, y0 = in2)
+  double c2 = 0, c3 = 0;
 };
 
 // Exchange plan of global shard `me`: the rows it receives from / sends to
@@ -131,6 +133,7 @@ struct System {
   bool prof_active = true;
   bool overlap = true;              // split SpMV: interior rows || halo exchange
   bool fuse_steps = true;           // k-skip steps fused into the SpMV epilogue
+  bool fuse_first = true;           // k-skip MrR steps 0+1 in one SpMV (EPI_STEP_MRR_FIRST2)
   int epi_late = 0;                 // SpmvArgs::epi_late (A/B knob)
   std::unique_ptr<Session> session;
 
@@ -141,10 +144,10 @@ struct System {
   void alloc_vectors(int count);
   // Halo exchange of up to two vectors (ids), all shards.
   void build_masks(Shard& s);
-  void halo(int id1, int id2 = -1);
+  void halo(int id1, int id2 = -1, int id3 = -1);
   // The same exchange on the shards' comm streams, ordered after ev_in and
   // signalling ev_out (overlapped path).
-  void halo_async(int id1, int id2);
+  void halo_async(int id1, int id2, int id3 = -1);
   void spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int b, int slot0,
             const StepOps* st = nullptr);
   void ew(EwOp op, double c0, double c1, std::array<int, 6> ids, int slot0);

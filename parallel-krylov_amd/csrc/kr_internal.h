@@ -63,6 +63,12 @@ enum SpmvEpi : int {
   EPI_STEP_MRR_X2,   //   ... and ud = (us - u2_old) - u2_new (deferred x -= z, two steps)
   EPI_STEP_MRR_X,    //   ... and ud = us - u2_new
   EPI_STEP_KCG,      // t=Ax; u1+=c0*x; u2-=c0*t; y1=u2+c1*x                 (u1=x u2=Ar0, x=Ap0)
+  // Steps 0 AND 1 of a k-skip MrR outer iteration in one SpMV: the input
+  // r1 = r0 - (c0*y0 + c1*Ar1) is formed at every gathered column from x1=r0,
+  // x2=y0, x3=Ar1 (exactly as the step-0 vector kernel rounds it), then step 1
+  // (c2, c3) runs in the epilogue: u1 (y) and y1 (r) are written to buffers
+  // other than x2 / x1, which other rows still gather. Row walk v2 only.
+  EPI_STEP_MRR_FIRST2,
 };
 int spmv_products(SpmvEpi epi);
 
@@ -98,6 +104,8 @@ struct SpmvArgs {
   const double* us = nullptr;
   double* ud = nullptr;
   double c0 = 0, c1 = 0;
+  const double* x3 = nullptr;  // EPI_STEP_MRR_FIRST2: Ar1 (halo-extended)
+  double c2 = 0, c3 = 0;       // EPI_STEP_MRR_FIRST2: step-1 scalars (eta1, zeta1)
   int epi_late = 0;  // 1: load own-row epilogue operands at the row end (A/B, KR_EPI_LATE)
   int64_t nnz_total = -1;  // entries of val/col (-1: unknown; spmv_kernel2 needs >= 4)
   // Dense row block (gemv_kernel): val is n x ncols row-major with leading

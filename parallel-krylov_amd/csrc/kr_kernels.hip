@@ -33,6 +33,7 @@ extern template void spmv_launch_epi<EPI_STEP_MRR_NOX>(const SpmvArgs&, int, hip
 extern template void spmv_launch_epi<EPI_STEP_MRR_X2>(const SpmvArgs&, int, hipStream_t);
 extern template void spmv_launch_epi<EPI_STEP_MRR_X>(const SpmvArgs&, int, hipStream_t);
 extern template void spmv_launch_epi<EPI_STEP_KCG>(const SpmvArgs&, int, hipStream_t);
+extern template void spmv_launch_epi<EPI_STEP_MRR_FIRST2>(const SpmvArgs&, int, hipStream_t);
 
 namespace {
 
@@ -548,7 +549,8 @@ int spmv_products(SpmvEpi epi) {
     case EPI_STEP_MRR_NOX:
     case EPI_STEP_MRR_X2:
     case EPI_STEP_MRR_X:
-    case EPI_STEP_KCG: return 0;
+    case EPI_STEP_KCG:
+    case EPI_STEP_MRR_FIRST2: return 0;
   }
   return 0;
 }
@@ -576,6 +578,7 @@ void launch_spmv_grid(SpmvEpi epi, const SpmvArgs& a, int nblocks, hipStream_t s
     KR_CASE(EPI_STEP_MRR_X2)
     KR_CASE(EPI_STEP_MRR_X)
     KR_CASE(EPI_STEP_KCG)
+    KR_CASE(EPI_STEP_MRR_FIRST2)
 #undef KR_CASE
     default:
       throw Failure(KR_ERR_INVALID, "unknown SpMV epilogue");

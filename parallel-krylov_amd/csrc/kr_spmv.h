@@ -114,10 +114,26 @@ template <>
 struct EpiTraits<EPI_STEP_MRR_X> : EpiStepTraits {};
 template <>
 struct EpiTraits<EPI_STEP_KCG> : EpiStepTraits {};
+template <>
+struct EpiTraits<EPI_STEP_MRR_FIRST2> : EpiStepTraits {};
 template <int EPI>
 constexpr bool is_step() {
   return EPI == EPI_STEP_MRR_NOX || EPI == EPI_STEP_MRR_X2 || EPI == EPI_STEP_MRR_X ||
-         EPI == EPI_STEP_KCG;
+         EPI == EPI_STEP_KCG || EPI == EPI_STEP_MRR_FIRST2;
+}
+// The SpMV input is virtual: r1 = r0 - (c0*y0 + c1*Ar1) at every column.
+template <int EPI>
+constexpr bool is_virtual() {
+  return EPI == EPI_STEP_MRR_FIRST2;
+}
+// r1 at one column, rounded exactly like ew_kernel<EW_MRR_NOX>'s step 0:
+// y1 = fl(fl(c0*y0) + fl(c1*ar1)), r1 = fl(r0 - y1).
+__device__ __forceinline__ double virtual_r1(double c0, double c1, double r0, double y0,
+                                             double ar1) {
+  const double t1 = c0 * y0;
+  const double t2 = c1 * ar1;
+  const double y = t1 + t2;
+  return r0 - y;
 }
 
 // Products of one row. x/x2: inputs at the row, y/y2: results, e: extra.
@@ -189,7 +205,13 @@ __device__ __forceinline__ EpiIn epi_load(const SpmvArgs& a, int64_t row) {
   if constexpr (is_step<EPI>()) {
     in.u1 = a.u1[row];
     in.u2 = a.u2[row];
-    if constexpr (EPI == EPI_STEP_MRR_X2 || EPI == EPI_STEP_MRR_X) in.us = a.us[row];
+    if constexpr (EPI == EPI_STEP_MRR_X2 || EPI == EPI_STEP_MRR_X ||
+                  EPI == EPI_STEP_MRR_FIRST2)
+      in.us = a.us[row];
+    if constexpr (EPI == EPI_STEP_MRR_FIRST2) {
+      in.x2 = a.x2[a.xoff + row];  // y0
+      in.e = a.x3[a.xoff + row];   // Ar1
+    }
   } else if constexpr (EPI == EPI_BMINUS) {
     in.e = a.b[row];
   } else if constexpr (T::kE) {
@@ -206,7 +228,28 @@ __device__ __forceinline__ void epi_row_in(const SpmvArgs& a, int64_t row, doubl
                                                              ? EpiTraits<EPI>::NP
                                                              : 1]) {
   using T = EpiTraits<EPI>;
-  if constexpr (is_step<EPI>()) {
+  if constexpr (EPI == EPI_STEP_MRR_FIRST2) {
+    // step 0 at the own row (c0 = eta0, c1 = zeta0; x = r0, x2 = y0, e = Ar1,
+    // u2 = z0), then step 1 (c2 = eta1, c3 = zeta1) with sum1 = (A r1)[row]
+    const double t1 = a.c0 * in.x2;
+    const double t2 = a.c1 * in.e;
+    const double y1 = t1 + t2;
+    const double t3 = a.c0 * in.u2;
+    const double t4 = a.c1 * in.x;
+    const double z1 = t3 - t4;
+    const double r1 = in.x - y1;
+    const double s1 = a.c2 * y1;
+    const double s2 = a.c3 * sum1;
+    const double y2 = s1 + s2;
+    const double s3 = a.c2 * z1;
+    const double s4 = a.c3 * r1;
+    const double z2 = s3 - s4;
+    const double xm = in.us - z1;  // x -= z of step 0, deferred
+    a.ud[row] = xm - z2;
+    a.u1[row] = y2;
+    a.u2[row] = z2;
+    a.y1[row] = r1 - y2;  // Ar0 of step 2
+  } else if constexpr (is_step<EPI>()) {
     const double xv = in.x;
     if constexpr (EPI == EPI_STEP_KCG) {  // x = Ap0, sum1 = Ap1; u1 = x, u2 = Ar0
       const double a0 = a.c0 * xv;
@@ -408,6 +451,42 @@ __device__ __forceinline__ void row_window(const double* s_val, const int32_t* s
         if constexpr (NV == 2) sum2 = sum2 + v[u] * p2[u];
       }
     }
+  }
+}
+
+// Further gather batches of a row whose input is virtual (is_virtual):
+// x(c) = r1 at column c from r0 = x1, y0 = x2, Ar1 = x3 (SpmvArgs), summed in
+// stored order. Columns from the LDS column window or the offset masks.
+template <int GATHER, typename W>
+__device__ __forceinline__ void row_window_virtual(const double* s_val, const int32_t* s_col,
+                                                   const int32_t* s_M, int64_t xrow,
+                                                   const SpmvArgs& a, int js, int je, W& mrem,
+                                                   double& sum1) {
+  for (int j = js; j < je; j += GATHER) {
+    double v[GATHER], p1[GATHER], p2[GATHER], p3[GATHER];
+#pragma unroll
+    for (int u = 0; u < GATHER; ++u) {
+      const bool ok = j + u < je;
+      const int jj = ok ? j + u : js;
+      v[u] = s_val[jj];
+      int64_t c;
+      if (s_col) {
+        c = s_col[jj];
+      } else {
+        c = xrow;
+        if (ok) {
+          c += s_M[sizeof(W) == 8 ? __builtin_ctzll((unsigned long long)mrem)
+                                  : __builtin_ctz((unsigned)mrem)];
+          mrem &= mrem - 1;
+        }
+      }
+      p1[u] = a.x1[c];
+      p2[u] = a.x2[c];
+      p3[u] = a.x3[c];
+    }
+#pragma unroll
+    for (int u = 0; u < GATHER; ++u)
+      if (j + u < je) sum1 = sum1 + v[u] * virtual_r1(a.c0, a.c1, p1[u], p2[u], p3[u]);
   }
 }
 
@@ -868,6 +947,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
   using T = EpiTraits<EPI>;
   constexpr int NP = T::NP;
   constexpr int NV = T::NV;
+  constexpr bool VIRT = is_virtual<EPI>();
   constexpr int G = kGather;
   constexpr bool COLS = MW == 0;  // else: offset masks, no column stream
   using MT = typename MaskType<(MW > 0 ? MW : 64)>::type;
@@ -964,7 +1044,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
     const int64_t xrow = a.xoff + r0 + tid;
 
     // (1) first gather batch of this window
-    double v[G], p1[G], p2[G];
+    double v[G], p1[G], p2[G], p3[VIRT ? G : 1];
 #pragma unroll
     for (int u = 0; u < G; ++u) {
       const bool ok = js + u < je;
@@ -981,7 +1061,8 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
         }
       }
       p1[u] = x1[c];
-      if constexpr (NV == 2) p2[u] = x2[c];
+      if constexpr (NV == 2 || VIRT) p2[u] = x2[c];
+      if constexpr (VIRT) p3[u] = a.x3[c];
     }
 
     // (2) the next window's loads: they stay in flight while this one is summed
@@ -1011,15 +1092,25 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
 #pragma unroll
     for (int u = 0; u < G; ++u) {
       if (js + u < je) {
-        sum1 = sum1 + v[u] * p1[u];
-        if constexpr (NV == 2) sum2 = sum2 + v[u] * p2[u];
+        if constexpr (VIRT) {
+          sum1 = sum1 + v[u] * virtual_r1(a.c0, a.c1, p1[u], p2[u], p3[u]);
+        } else {
+          sum1 = sum1 + v[u] * p1[u];
+          if constexpr (NV == 2) sum2 = sum2 + v[u] * p2[u];
+        }
       }
     }
     if (je - js > G) {
-      if constexpr (COLS)
+      if constexpr (VIRT) {
+        if constexpr (COLS)
+          row_window_virtual<G>(sv, sc, nullptr, 0, a, js + G, je, mrem, sum1);
+        else
+          row_window_virtual<G>(sv, nullptr, s_M, xrow, a, js + G, je, mrem, sum1);
+      } else if constexpr (COLS) {
         row_window<NV, G>(sv, sc, x1, x2, js + G, je, sum1, sum2);
-      else
+      } else {
         row_window_mask<NV, G>(sv, s_M, x1, x2, xrow, js + G, je, mrem, sum1, sum2);
+      }
     }
     buf ^= 1;
     if constexpr (!DB) __syncthreads();  // the single buffer is rewritten next
@@ -1372,26 +1463,33 @@ void spmv_dispatch_epi(const SpmvArgs& a, int nblocks, hipStream_t s) {
   int variant = env ? atoi(env) : (a.long_rows ? (EpiTraits<E>::NV == 1 ? 14 : 8) : 13);
   // the v2 kernels need 16-byte aligned bases and >= 4 entries
   if (variant >= 10 && (!VEC || a.nnz_total < 4)) variant = a.long_rows ? 8 : 0;
-  if constexpr (VEC) {
-    switch (variant) {
-      case 10: spmv2_launch<RP, E, VEC>(a, grid, block, s); return;
-      case 12: spmv2_launch<RP, E, VEC, false>(a, grid, block, s); return;
-      case 13: spmv2_launch<RP, E, VEC, true, true>(a, grid, block, s); return;
-      case 14:
-        spmv_kernel_prod2<RP, E, EpiTraits<E>::NV == 1, true><<<grid, block, 0, s>>>(a);
-        return;
-      case 15:
-        spmv_kernel_prod2<RP, E, EpiTraits<E>::NV == 1, false><<<grid, block, 0, s>>>(a);
-        return;
-      default: break;
-    }
-  }
-  if (variant == 8) {
-    spmv_kernel_prod<RP, E, VEC><<<grid, block, 0, s>>>(a);
+  if constexpr (is_virtual<E>()) {  // implemented by the row walk v2 only
+    if (!VEC || a.nnz_total < 4 || a.dense)
+      throw Failure(KR_ERR_INVALID, "fused first step needs the row walk v2");
+    spmv2_launch<RP, E, VEC, true, true>(a, grid, block, s);
     return;
+  } else {
+    if constexpr (VEC) {
+      switch (variant) {
+        case 10: spmv2_launch<RP, E, VEC>(a, grid, block, s); return;
+        case 12: spmv2_launch<RP, E, VEC, false>(a, grid, block, s); return;
+        case 13: spmv2_launch<RP, E, VEC, true, true>(a, grid, block, s); return;
+        case 14:
+          spmv_kernel_prod2<RP, E, EpiTraits<E>::NV == 1, true><<<grid, block, 0, s>>>(a);
+          return;
+        case 15:
+          spmv_kernel_prod2<RP, E, EpiTraits<E>::NV == 1, false><<<grid, block, 0, s>>>(a);
+          return;
+        default: break;
+      }
+    }
+    if (variant == 8) {
+      spmv_kernel_prod<RP, E, VEC><<<grid, block, 0, s>>>(a);
+      return;
+    }
+    if (!(a.mask && spmv_masked<RP, E, VEC>(a, grid, block, s)))
+      spmv_kernel<RP, E, VEC><<<grid, block, 0, s>>>(a);
   }
-  if (!(a.mask && spmv_masked<RP, E, VEC>(a, grid, block, s)))
-    spmv_kernel<RP, E, VEC><<<grid, block, 0, s>>>(a);
 }
 
 }  // namespace
@@ -1402,7 +1500,10 @@ void spmv_dispatch_epi(const SpmvArgs& a, int nblocks, hipStream_t s) {
 template <int E>
 void spmv_launch_epi(const SpmvArgs& a, int nblocks, hipStream_t s) {
   if (a.dense) {
-    gemv_kernel<E><<<nblocks, kBlock, 0, s>>>(a);
+    if constexpr (is_virtual<E>())
+      throw Failure(KR_ERR_INVALID, "fused first step has no dense kernel");
+    else
+      gemv_kernel<E><<<nblocks, kBlock, 0, s>>>(a);
     return;
   }
   // 16-byte staging needs 16-byte aligned val/col bases
