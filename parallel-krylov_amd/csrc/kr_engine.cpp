@@ -300,8 +300,10 @@ void System::finalize() {
       KR_HIP_CHECK(hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, s.stream));
       KR_HIP_CHECK(hipStreamSynchronize(s.stream));
       KR_HIP_CHECK(hipFree(d));
-      s.int_lo = h[0];
-      s.int_hi = h[1];
+      // Interior rows, shrunk to whole row blocks so that the two boundary
+      // ranges are whole blocks too and run as ONE launch (SpmvArgs::rb_gap).
+      s.int_lo = std::min<int64_t>((h[0] + kBlock - 1) / kBlock * kBlock, s.n);
+      s.int_hi = std::max<int64_t>(h[1] / kBlock * kBlock, s.int_lo);
       s.reach = h[2];
       // Slab schedule (A/B only, KR_SLAB=S row blocks per plane): keeps x
       // rows one reach apart (3-D stencils) closer in time; measured 5-15 %
@@ -509,6 +511,10 @@ void System::halo_async(int id1, int id2, int id3) {
   }
   for (auto& s : shards) {
     KR_HIP_CHECK(hipSetDevice(s.dev));
+    // The copies overwrite s's halo rows: s's own earlier kernels (the
+    // previous SpMV's boundary rows read the same halo when consecutive SpMVs
+    // share an input vector) must be done first, not only the peer's.
+    KR_HIP_CHECK(hipStreamWaitEvent(s.comm_stream, s.ev_in, 0));
     for (auto& p : s.recv) {
       Shard& t = shards[p.peer];
       KR_HIP_CHECK(hipStreamWaitEvent(s.comm_stream, t.ev_in, 0));
@@ -619,15 +625,9 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
     return 12.0 * s.nnz + (s.rowptr64 ? 8.0 : 4.0) * (s.n + 1) + nv * 16.0 * s.n + extra;
   };
   // The partial stride is s.pstride for every launch; the full / interior
-  // launch writes s.spmv_grid partials per product, a boundary launch with
-  // fewer blocks adds into the first entries.
+  // launch writes s.spmv_grid partials per product, the boundary launch (fewer
+  // blocks) adds into the first entries.
   const int np = spmv_products(epi);
-  auto launch_part = [&](Shard& s, int64_t r_begin, int64_t rows, int acc) {
-    if (rows <= 0) return;
-    SpmvArgs a = args_for(s, r_begin, rows, s.pstride, acc);
-    const int g = (int)std::min<int64_t>(s.spmv_grid, (rows + kBlock - 1) / kBlock);
-    launch_spmv_grid(epi, a, g, s.stream);
-  };
   auto launch_full = [&](Shard& s, int64_t r_begin, int64_t rows) {
     launch_spmv_grid(epi, args_for(s, r_begin, rows, s.pstride, 0), s.spmv_grid, s.stream);
     for (int p = 0; p < np; ++p) s.slot_n[slot0 + p] = s.spmv_grid;
@@ -665,8 +665,17 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
       // own halo copied, and every reader done with this shard's rows
       for (auto& t : shards) KR_HIP_CHECK(hipStreamWaitEvent(s.stream, t.ev_out, 0));
     }
-    launch_part(s, 0, s.int_lo, 1);
-    launch_part(s, s.int_hi, s.n - s.int_hi, 1);
+    // both boundary ranges in one launch: row blocks [0, int_lo/B) and
+    // [int_hi/B, end) (interior bounds are whole blocks, see finalize)
+    const int64_t nb_lo = s.int_lo / kBlock, nb_gap = (s.int_hi - s.int_lo) / kBlock;
+    const int64_t nb_all = (s.n + kBlock - 1) / kBlock;
+    if (nb_all - nb_gap > 0) {
+      SpmvArgs ab = args_for(s, 0, s.n, s.pstride, 1);
+      ab.rb_gap_at = nb_lo;
+      ab.rb_gap = nb_gap;
+      const int g = (int)std::min<int64_t>(s.spmv_grid, nb_all - nb_gap);
+      launch_spmv_grid(epi, ab, g, s.stream);
+    }
     prof_end(s, nm, t0s[li], bytes_of(s));
   }
 }

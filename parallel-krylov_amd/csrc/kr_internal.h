@@ -112,6 +112,9 @@ struct SpmvArgs {
   // dimension dld; x1 + xcol0 (x2 + xcol0) is the full input vector.
   int dense = 0;
   int64_t dld = 0, ncols = 0, xcol0 = 0;
+  // Row-block gap (boundary launch of a split SpMV): the launch covers the
+  // row blocks [0, rb_gap_at) and [rb_gap_at + rb_gap, ceil(n / kBlock)).
+  int64_t rb_gap_at = 0, rb_gap = 0;
 };
 // Mean row length from which the product-then-sum SpMV is used.
 constexpr double kLongRow = 12.0;

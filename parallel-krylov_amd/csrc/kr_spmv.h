@@ -513,6 +513,7 @@ __device__ __forceinline__ void row_window_virtual(const double* s_val, const in
 // changes speed: every row block is visited exactly once.
 struct RowSched {
   int64_t j0, jstep, jcount, base = 0, off = 0, w = 0, S = 0, sub = 0, full = 0, rem = 0;
+  int64_t gap_at = 0, gap = 0;  // SpmvArgs::rb_gap_at / rb_gap (virtual -> physical)
   int nc = 0;
   // row blocks of sub-slab c (width wc, all planes; the last plane is partial)
   __device__ int64_t chunk_count(int c, int64_t wc) const {
@@ -545,7 +546,7 @@ struct RowSched {
       jcount = nrb;
     }
   }
-  __device__ int64_t rb(int64_t v) const {
+  __device__ int64_t rb_virtual(int64_t v) const {
     if (!w) return base + v;
     // sub-slab after sub-slab; inside one, plane after plane
     for (int c = 0; c < nc; ++c) {
@@ -555,6 +556,10 @@ struct RowSched {
       v -= cnt;
     }
     return -1;  // unreachable: v < jcount
+  }
+  __device__ int64_t rb(int64_t v) const {
+    const int64_t r = rb_virtual(v);
+    return r < gap_at ? r : r + gap;
   }
 };
 
@@ -588,9 +593,11 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
 #pragma unroll
   for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;
 
-  const int64_t nrb = (a.n + kBlock - 1) / kBlock;
+  const int64_t nrb = (a.n + kBlock - 1) / kBlock - a.rb_gap;
   RowSched sched;
   sched.init(nrb, a.slab, a.slab_sub, XCD);
+  sched.gap_at = a.rb_gap_at;
+  sched.gap = a.rb_gap;
   int64_t j = sched.j0;
   const int64_t jstep = sched.jstep, jcount = sched.jcount;
   auto rb_of = [&](int64_t v) { return sched.rb(v); };
@@ -784,9 +791,11 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_prod(SpmvArgs a) {
 #pragma unroll
   for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;
 
-  const int64_t nrb = (a.n + kBlock - 1) / kBlock;
+  const int64_t nrb = (a.n + kBlock - 1) / kBlock - a.rb_gap;
   RowSched sched;  // as spmv_kernel
   sched.init(nrb, a.slab, a.slab_sub, true);
+  sched.gap_at = a.rb_gap_at;
+  sched.gap = a.rb_gap;
   int64_t j = sched.j0;
   const int64_t jstep = sched.jstep, jcount = sched.jcount;
   auto rb_of = [&](int64_t v) { return sched.rb(v); };
@@ -975,9 +984,11 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
 #pragma unroll
   for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;
 
-  const int64_t nrb = (a.n + kBlock - 1) / kBlock;
+  const int64_t nrb = (a.n + kBlock - 1) / kBlock - a.rb_gap;
   RowSched sched;
   sched.init(nrb, a.slab, a.slab_sub, true);
+  sched.gap_at = a.rb_gap_at;
+  sched.gap = a.rb_gap;
   int64_t j = sched.j0;
   const int64_t jstep = sched.jstep, jcount = sched.jcount;
   if (j >= jcount) {
@@ -1212,9 +1223,11 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_prod2(SpmvArgs a) {
 #pragma unroll
   for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;
 
-  const int64_t nrb = (a.n + kBlock - 1) / kBlock;
+  const int64_t nrb = (a.n + kBlock - 1) / kBlock - a.rb_gap;
   RowSched sched;
   sched.init(nrb, a.slab, a.slab_sub, true);
+  sched.gap_at = a.rb_gap_at;
+  sched.gap = a.rb_gap;
   const int64_t jstep = sched.jstep, jcount = sched.jcount;
   if (sched.j0 >= jcount) {
     block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
