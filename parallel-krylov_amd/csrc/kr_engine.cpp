@@ -170,8 +170,19 @@ System::~System() {
 void System::build_masks(Shard& s) {
   const char* env = getenv("KR_MASK");
   if (env && atoi(env) == 0) return;
-  if (s.n == 0 || (double)s.nnz >= kLongRow * (double)s.n) return;
-  if ((reinterpret_cast<uintptr_t>(s.val) | reinterpret_cast<uintptr_t>(s.col)) & 15) return;
+  // Diagonal-offset values for long rows (mean >= kLongRow nnz/row: banded
+  // C3 +23 %, C5 +35 % over the product-then-sum kernel). Short rows keep the
+  // LDS-staged row walk with masks, which measured equal or up to 5 % faster
+  // on 512^3 Poisson (C2 256^3: DIA +3 %). KR_DIA=0 never, KR_DIA=2 always.
+  if (s.n == 0) return;
+  const char* de = getenv("KR_DIA");
+  const int dia_mode = de ? atoi(de) : 1;
+  const bool long_rows = (double)s.nnz >= kLongRow * (double)s.n;
+  const bool dia_on = dia_mode == 2 || (dia_mode == 1 && long_rows);
+  if (!dia_on && long_rows) return;
+  if (!dia_on &&
+      ((reinterpret_cast<uintptr_t>(s.val) | reinterpret_cast<uintptr_t>(s.col)) & 15))
+    return;
   unsigned long long* table = nullptr;
   KR_HIP_CHECK(hipMalloc(&table, kOffTableBytes + 16));
   int* flags = reinterpret_cast<int*>(reinterpret_cast<char*>(table) + kOffTableBytes);
@@ -197,6 +208,17 @@ void System::build_masks(Shard& s) {
   s.owned.push_back(mask);
   KR_HIP_CHECK(hipMemcpyAsync(dM, M.data(), nm * sizeof(int32_t), hipMemcpyHostToDevice, s.stream));
   launch_masks(s.rowptr, s.rowptr64, s.n, s.col, s.pad, dM, nm, mw, mask, s.stream);
+  if (dia_on) {
+    const int64_t ld = (s.n + 63) / 64 * 64;
+    double* dia = nullptr;
+    if (hipMalloc(&dia, sizeof(double) * (size_t)nm * ld) != hipSuccess)
+      throw Failure(KR_ERR_NOMEM, "diagonal-offset values: allocation failed");
+    s.owned.push_back(dia);
+    KR_HIP_CHECK(hipMemsetAsync(dia, 0, sizeof(double) * (size_t)nm * ld, s.stream));
+    launch_dia_fill(s.rowptr, s.rowptr64, s.n, s.col, s.val, s.pad, dM, nm, dia, ld, s.stream);
+    s.dia = dia;
+    s.dia_ld = ld;
+  }
   KR_HIP_CHECK(hipStreamSynchronize(s.stream));
   s.mask = mask;
   s.moff = dM;
@@ -351,9 +373,9 @@ void System::finalize() {
     // Fusion pays for the short-row (row-walk) kernel: C4 +6 %. With the
     // product-then-sum kernel (long rows) the fused SpMV costs more than the
     // separate vector pass (C5: +0.9 ms vs +0.5 ms), so long rows keep it.
-    bool long_rows = false;
+    bool long_rows = false;  // long rows on the product-then-sum kernel (no DIA)
     for (auto& s : shards)
-      if (s.n > 0 && (double)s.nnz >= kLongRow * (double)s.n) long_rows = true;
+      if (s.n > 0 && !s.dia && (double)s.nnz >= kLongRow * (double)s.n) long_rows = true;
     fuse_steps = fz ? atoi(fz) != 0 : !long_rows;
     // Own-row epilogue operands loaded at the row end (default) or at the
     // row-block start (KR_EPI_LATE=0): late measured 1-3 % faster on C4.
@@ -363,11 +385,13 @@ void System::finalize() {
     // aligned CSR with >= 4 entries, no dense shard, no forced v1 kernel).
     const char* ff = getenv("KR_FUSE_FIRST");
     const char* sv = getenv("KR_SPMV_VARIANT");
-    bool v2 = !sv || atoi(sv) == 10 || atoi(sv) == 12 || atoi(sv) == 13;
-    for (auto& s : shards)
-      if (s.dense || s.nnz < 4 ||
+    bool v2 = true;  // every shard on the DIA kernel or the row walk v2
+    for (auto& s : shards) {
+      if (s.dia) continue;
+      if (s.dense || s.nnz < 4 || (sv && atoi(sv) != 10 && atoi(sv) != 12 && atoi(sv) != 13) ||
           ((reinterpret_cast<uintptr_t>(s.val) | reinterpret_cast<uintptr_t>(s.col)) & 15))
         v2 = false;
+    }
     fuse_first = fuse_steps && !long_rows && v2 && !(ff && atoi(ff) == 0);
   }
   finalized = true;
@@ -586,6 +610,10 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
       a.moff = s.moff;
       a.nm = s.nm;
       a.mw = s.mw;
+      if (s.dia) {
+        a.dia = s.dia + r_begin;
+        a.dia_ld = s.dia_ld;
+      }
     }
     a.epi_late = epi_late;
     a.nnz_total = s.nnz;

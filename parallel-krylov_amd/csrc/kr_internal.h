@@ -98,6 +98,11 @@ struct SpmvArgs {
   const int32_t* moff = nullptr;
   int nm = 0;
   int mw = 0;
+  // Diagonal-offset values (optional, with the masks): entry of row i at
+  // offset moff[b] is dia[b * dia_ld + i] (row-block launches offset dia by
+  // their first row). The SpMV then needs neither LDS staging nor rowptr.
+  const double* dia = nullptr;
+  int64_t dia_ld = 0;
   // Fused-step operands (EPI_STEP_*), own rows: in/out u1, u2, x source/dest.
   double* u1 = nullptr;
   double* u2 = nullptr;
@@ -208,6 +213,11 @@ void launch_interior(const void* rowptr, int rowptr64, int64_t n, const int32_t*
 // (key offset + 2^32, 0 empty); flags: 1 = a row not strictly increasing,
 // 2 = more than 256 offsets.
 constexpr int kMaxMaskBits = 64;
+// Diagonal-offset values from a masked CSR block (values of row i at offset
+// M[b] land in dia[b * ld + i]; absent entries stay 0).
+void launch_dia_fill(const void* rowptr, int rowptr64, int64_t n, const int32_t* col,
+                     const double* val, int64_t base, const int32_t* M, int nm, double* dia,
+                     int64_t ld, hipStream_t s);
 constexpr size_t kOffTableBytes = 256 * sizeof(unsigned long long);
 void launch_offsets(const void* rowptr, int rowptr64, int64_t n, const int32_t* col,
                     int64_t base, unsigned long long* table, int* flags, hipStream_t s);

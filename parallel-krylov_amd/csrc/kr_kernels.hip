@@ -10,6 +10,7 @@
 // run to run, but they are not OpenBLAS's order.
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -520,6 +521,24 @@ __global__ void mask_kernel(const RP* rowptr, int64_t n, const int32_t* col, int
 }
 
 template <typename RP>
+__global__ void dia_fill_kernel(const RP* rowptr, int64_t n, const int32_t* col,
+                                const double* val, int64_t base, const int32_t* M, int nm,
+                                double* dia, int64_t ld) {
+  __shared__ int32_t sM[64];
+  if ((int)threadIdx.x < nm) sM[threadIdx.x] = M[threadIdx.x];
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t j = (int64_t)rowptr[i]; j < (int64_t)rowptr[i + 1]; ++j) {
+      const int64_t off = (int64_t)col[j] - (base + i);
+      int b = 0;
+      while (b < nm - 1 && sM[b] != off) ++b;
+      dia[(int64_t)b * ld + i] = val[j];
+    }
+  }
+}
+
+template <typename RP>
 __global__ void col_shift_kernel(const RP* rowptr, int64_t n, int32_t* col, int64_t delta) {
   const int64_t base = (int64_t)rowptr[0];
   const int64_t nnz = (int64_t)rowptr[n] - base;
@@ -786,6 +805,20 @@ void launch_masks(const void* rowptr, int rowptr64, int64_t n, const int32_t* co
   else if (mw == 16) masks_typed<uint16_t>(rowptr, rowptr64, n, col, base, M, nm, mask, s);
   else if (mw == 32) masks_typed<uint32_t>(rowptr, rowptr64, n, col, base, M, nm, mask, s);
   else masks_typed<uint64_t>(rowptr, rowptr64, n, col, base, M, nm, mask, s);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_dia_fill(const void* rowptr, int rowptr64, int64_t n, const int32_t* col,
+                     const double* val, int64_t base, const int32_t* M, int nm, double* dia,
+                     int64_t ld, hipStream_t s) {
+  if (n <= 0) return;
+  const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 65535);
+  if (rowptr64)
+    dia_fill_kernel<int64_t><<<g, 256, 0, s>>>(static_cast<const int64_t*>(rowptr), n, col, val,
+                                               base, M, nm, dia, ld);
+  else
+    dia_fill_kernel<int32_t><<<g, 256, 0, s>>>(static_cast<const int32_t*>(rowptr), n, col, val,
+                                               base, M, nm, dia, ld);
   KR_HIP_CHECK(hipGetLastError());
 }
 

@@ -1185,13 +1185,20 @@ struct PWin {  // one staging window, uniform across the workgroup
   int nr = 0, first = 0, last = 0, valid = 0;
 };
 
-template <bool NT>
-__device__ __forceinline__ void pstage_load2(PStage& st, const double* __restrict__ val,
+// PS slots of 2 entries per lane: a window of PS * 2 * kBlock entries.
+template <int PS>
+struct PStageN {
+  dbl2v v[PS];
+  int2v c[PS];
+};
+
+template <bool NT, int PS>
+__device__ __forceinline__ void pstage_load2(PStageN<PS>& st, const double* __restrict__ val,
                                              const int32_t* __restrict__ col, int64_t ws,
                                              int64_t be, int tid) {
   const int64_t last = max((be - 1) & ~(int64_t)1, (int64_t)0);
 #pragma unroll
-  for (int q = 0; q < kPSlots; ++q) {
+  for (int q = 0; q < PS; ++q) {
     const int64_t g0 = min(ws + (int64_t)(tid + q * kBlock) * 2, last);
     if constexpr (NT)
       st.v[q] = __builtin_nontemporal_load(reinterpret_cast<const dbl2v*>(val + g0));
@@ -1201,15 +1208,19 @@ __device__ __forceinline__ void pstage_load2(PStage& st, const double* __restric
   }
 }
 
-template <typename RP, int EPI, bool DB, bool NT>
+// PS slots per lane (window PS * 512 entries): 4 for one vector; 2 for two
+// vectors, whose doubled gather and product registers would otherwise cost a
+// wave per SIMD (144 VGPRs at 4 slots).
+template <typename RP, int EPI, bool DB, bool NT, int PS>
 __global__ __launch_bounds__(kBlock) void spmv_kernel_prod2(SpmvArgs a) {
   using T = EpiTraits<EPI>;
   constexpr int NP = T::NP;
   constexpr int NV = T::NV;
   constexpr int NB = DB ? 2 : 1;  // product buffers
-  constexpr int NE = 2 * kPSlots;  // entries per lane per window
-  __shared__ __attribute__((aligned(16))) double s_p1[NB][kWindow];
-  __shared__ __attribute__((aligned(16))) double s_p2[NV == 2 ? NB : 1][NV == 2 ? kWindow : 2];
+  constexpr int NE = 2 * PS;      // entries per lane per window
+  constexpr int KW = PS * 2 * kBlock;  // window entries
+  __shared__ __attribute__((aligned(16))) double s_p1[NB][KW];
+  __shared__ __attribute__((aligned(16))) double s_p2[NV == 2 ? NB : 1][NV == 2 ? KW : 2];
   __shared__ double s_red[(NP > 0 ? NP : 1) * 4];
 
   const RP* __restrict__ rowptr = static_cast<const RP*>(a.rowptr);
@@ -1255,7 +1266,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_prod2(SpmvArgs a) {
     w0.be = (int64_t)load_uniform(rowptr, w0.r0 + w0.nr);
     w0.ws = wstart(w0.bs);
     w0.first = 1;
-    w0.last = w0.ws + kWindow >= w0.be;
+    w0.last = w0.ws + KW >= w0.be;
     w0.valid = 1;
   }
   fetch_next_bounds();
@@ -1263,9 +1274,9 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_prod2(SpmvArgs a) {
     PWin o = w;
     if (!w.valid) return o;
     if (!w.last) {
-      o.ws = w.ws + kWindow;
+      o.ws = w.ws + KW;
       o.first = 0;
-      o.last = o.ws + kWindow >= o.be;
+      o.last = o.ws + KW >= o.be;
       return o;
     }
     if (gj + jstep >= jcount) {
@@ -1280,7 +1291,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_prod2(SpmvArgs a) {
     o.be = ben;
     o.ws = wstart(bsn);
     o.first = 1;
-    o.last = o.ws + kWindow >= o.be;
+    o.last = o.ws + KW >= o.be;
     fetch_next_bounds();
     return o;
   };
@@ -1288,8 +1299,8 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_prod2(SpmvArgs a) {
   // stage registers: st = loads of the load-stage window; pv/g1/g2 = values
   // and gathered x of the gather-stage window; row ranges of the sum-,
   // gather- and load-stage windows' blocks (rlo_s/_g/_l)
-  PStage st;
-  dbl2v pv[kPSlots];
+  PStageN<PS> st;
+  dbl2v pv[PS];
   double g1[NE], g2[NV == 2 ? NE : 1];
   RP rlo_l = 0, rhi_l = 0, rlo_g = 0, rhi_g = 0, rlo_s = 0, rhi_s = 0;
   EpiIn pin_g, pin_s;
@@ -1299,7 +1310,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_prod2(SpmvArgs a) {
     rlo_g = rowptr[ri];
     rhi_g = rowptr[ri + 1];
   }
-  pstage_load2<NT>(st, val, col, w0.ws, w0.be, tid);
+  pstage_load2<NT, PS>(st, val, col, w0.ws, w0.be, tid);
   PWin wsum, wg = w0;  // wsum invalid: the pipeline fills first
   int it = 0;
   for (;;) {
@@ -1309,7 +1320,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_prod2(SpmvArgs a) {
     if (wsum.valid) {
       double* p1 = s_p1[DB ? (it & 1) : 0];
 #pragma unroll
-      for (int q = 0; q < kPSlots; ++q) {
+      for (int q = 0; q < PS; ++q) {
         reinterpret_cast<dbl2v*>(p1)[tid + q * kBlock] =
             dbl2v{pv[q].x * g1[2 * q], pv[q].y * g1[2 * q + 1]};
         if constexpr (NV == 2) {
@@ -1326,7 +1337,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_prod2(SpmvArgs a) {
     // the product lands in a slot no row reads).
     const int64_t wlast = max((wg.be - 1) & ~(int64_t)1, (int64_t)0);
 #pragma unroll
-    for (int q = 0; q < kPSlots; ++q) {
+    for (int q = 0; q < PS; ++q) {
       pv[q] = st.v[q];
       const int64_t e0 = min(wg.ws + (int64_t)(tid + q * kBlock) * 2, wlast);
       const int c0 = e0 < wg.be ? st.c[q].x : 0;
@@ -1350,7 +1361,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_prod2(SpmvArgs a) {
       rhi_l = rhi_g;
     }
     const PWin& wld = wl.valid ? wl : wg;  // drained: re-issue valid addresses
-    pstage_load2<NT>(st, val, col, wld.ws, wld.be, tid);
+    pstage_load2<NT, PS>(st, val, col, wld.ws, wld.be, tid);
     // (d) sum the sum-stage window's rows, in stored order
     __syncthreads();
     if (wsum.valid) {
@@ -1362,7 +1373,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_prod2(SpmvArgs a) {
       }
       if (tid < wsum.nr) {
         const int js = (int)max((int64_t)rlo_s - wsum.ws, (int64_t)0);
-        const int je = (int)min((int64_t)rhi_s - wsum.ws, (int64_t)kWindow);
+        const int je = (int)min((int64_t)rhi_s - wsum.ws, (int64_t)KW);
         for (int j = js; j < je; ++j) {
           sum1 = sum1 + p1[j];
           if constexpr (NV == 2) sum2 = sum2 + p2[j];
@@ -1382,6 +1393,119 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_prod2(SpmvArgs a) {
   }
   __syncthreads();
   block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
+}
+
+// ---------------------------------------------------------------------------
+// Diagonal-offset SpMV (default where offset masks exist: stencils, banded).
+// The values are stored offset-major (SpmvArgs::dia): for one offset, the
+// entries of consecutive rows are contiguous, and so are the x entries they
+// multiply (x[row + M[b]]). One lane per row, rows summed in stored order
+// (increasing offset = increasing column, as in CSR) from 0.0: bitwise scipy.
+// No LDS staging, no row pointers, no barrier: every load is a coalesced
+// 512-byte wave access, and latency is hidden by occupancy (8 waves/SIMD).
+// Loads are unconditional (absent entries read a valid slot and x[row]) and
+// absent entries are skipped by a select, so the sum is exactly the CSR one.
+// ---------------------------------------------------------------------------
+template <int EPI, int MW, int CH>  // CH: offsets per load batch
+__global__ __launch_bounds__(kBlock) void spmv_dia_kernel(SpmvArgs a) {
+  using T = EpiTraits<EPI>;
+  constexpr int NP = T::NP;
+  constexpr int NV = T::NV;
+  constexpr bool VIRT = is_virtual<EPI>();
+  using MT = typename MaskType<MW>::type;
+  using W = typename std::conditional<(MW > 32), uint64_t, uint32_t>::type;
+  __shared__ double s_red[(NP > 0 ? NP : 1) * 4];
+  const MT* __restrict__ mask = static_cast<const MT*>(a.mask);
+  const double* __restrict__ dia = a.dia;
+  const double* __restrict__ x1 = a.x1;
+  const double* __restrict__ x2 = a.x2;
+  const int tid = threadIdx.x;
+  const int nm = a.nm;
+  double acc[NP > 0 ? NP : 1];
+#pragma unroll
+  for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;
+
+  const int64_t nrb = (a.n + kBlock - 1) / kBlock - a.rb_gap;
+  RowSched sched;
+  sched.init(nrb, a.slab, a.slab_sub, true);
+  sched.gap_at = a.rb_gap_at;
+  sched.gap = a.rb_gap;
+  for (int64_t j = sched.j0; j < sched.jcount; j += sched.jstep) {
+    const int64_t row = sched.rb(j) * kBlock + tid;
+    const bool active = row < a.n;
+    const int64_t rr = active ? row : a.n - 1;  // loads stay in bounds
+    const W m = active ? (W)mask[rr] : (W)0;
+    const EpiIn pin = epi_load<EPI>(a, rr);
+    const int64_t xrow = a.xoff + rr;
+    double sum1 = 0.0, sum2 = 0.0;
+    for (int k0 = 0; k0 < nm; k0 += CH) {
+      double v[CH], p1[CH], p2[CH], p3[VIRT ? CH : 1];
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        const int k = min(k0 + u, nm - 1);
+        const bool ok = k0 + u < nm && ((m >> k) & 1);
+        const int64_t c = ok ? xrow + load_uniform(a.moff, k) : xrow;
+        v[u] = __builtin_nontemporal_load(dia + (int64_t)k * a.dia_ld + rr);
+        p1[u] = x1[c];
+        if constexpr (NV == 2 || VIRT) p2[u] = x2[c];
+        if constexpr (VIRT) p3[u] = a.x3[c];
+      }
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        const bool ok = k0 + u < nm && ((m >> min(k0 + u, nm - 1)) & 1);
+        if constexpr (VIRT) {
+          const double t = sum1 + v[u] * virtual_r1(a.c0, a.c1, p1[u], p2[u], p3[u]);
+          sum1 = ok ? t : sum1;
+        } else {
+          const double t1 = sum1 + v[u] * p1[u];
+          sum1 = ok ? t1 : sum1;
+          if constexpr (NV == 2) {
+            const double t2 = sum2 + v[u] * p2[u];
+            sum2 = ok ? t2 : sum2;
+          }
+        }
+      }
+    }
+    if (active) epi_row_in<EPI>(a, row, sum1, sum2, x1, x2, pin, acc);
+  }
+  __syncthreads();
+  block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
+}
+
+template <int E, int CH>
+void spmv_dia_launch_ch(const SpmvArgs& a, int nblocks, hipStream_t s) {
+  switch (a.mw) {
+    case 8: spmv_dia_kernel<E, 8, CH><<<nblocks, kBlock, 0, s>>>(a); return;
+    case 16: spmv_dia_kernel<E, 16, CH><<<nblocks, kBlock, 0, s>>>(a); return;
+    case 32: spmv_dia_kernel<E, 32, CH><<<nblocks, kBlock, 0, s>>>(a); return;
+    default: spmv_dia_kernel<E, 64, CH><<<nblocks, kBlock, 0, s>>>(a); return;
+  }
+}
+
+template <int E>
+void spmv_dia_launch(const SpmvArgs& a, int nblocks, hipStream_t s) {
+  const char* env = getenv("KR_DIA_CH");  // A/B: 4 or 8 offsets per load batch
+  const int ch = env ? atoi(env) : 8;
+  if (ch == 4)
+    spmv_dia_launch_ch<E, 4>(a, nblocks, s);
+  else
+    spmv_dia_launch_ch<E, 8>(a, nblocks, s);
+}
+
+// Which kernel serves a masked shard: the diagonal-offset kernel, except for
+// short-row multi-vector SpMVs (dual, fused first step), where the row walk
+// v2 measured faster (512^3 dual 2.77 vs 2.82 ms, first step 3.93 vs 4.20 ms).
+// KR_DIA_ALL=1 routes those to the diagonal-offset kernel too (A/B).
+template <int E>
+bool use_dia(const SpmvArgs& a) {
+  if (!a.dia) return false;
+  constexpr bool multi = EpiTraits<E>::NV == 2 || is_virtual<E>();
+  if (!multi || a.long_rows) return true;
+  const bool vec = ((reinterpret_cast<uintptr_t>(a.val) | reinterpret_cast<uintptr_t>(a.col)) &
+                    15) == 0;
+  if (!vec || a.nnz_total < 4) return true;
+  const char* env = getenv("KR_DIA_ALL");
+  return env && atoi(env) == 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -1487,11 +1611,16 @@ void spmv_dispatch_epi(const SpmvArgs& a, int nblocks, hipStream_t s) {
         case 10: spmv2_launch<RP, E, VEC>(a, grid, block, s); return;
         case 12: spmv2_launch<RP, E, VEC, false>(a, grid, block, s); return;
         case 13: spmv2_launch<RP, E, VEC, true, true>(a, grid, block, s); return;
-        case 14:
-          spmv_kernel_prod2<RP, E, EpiTraits<E>::NV == 1, true><<<grid, block, 0, s>>>(a);
+        case 14:  // one vector: 4 slots, double-buffered; two: 2 slots
+          spmv_kernel_prod2<RP, E, true, true, EpiTraits<E>::NV == 1 ? 4 : 2>
+              <<<grid, block, 0, s>>>(a);
           return;
         case 15:
-          spmv_kernel_prod2<RP, E, EpiTraits<E>::NV == 1, false><<<grid, block, 0, s>>>(a);
+          spmv_kernel_prod2<RP, E, true, false, EpiTraits<E>::NV == 1 ? 4 : 2>
+              <<<grid, block, 0, s>>>(a);
+          return;
+        case 16:  // A/B: two vectors with 4 slots, single-buffered (144 VGPRs)
+          spmv_kernel_prod2<RP, E, EpiTraits<E>::NV == 1, true, 4><<<grid, block, 0, s>>>(a);
           return;
         default: break;
       }
@@ -1512,6 +1641,10 @@ void spmv_dispatch_epi(const SpmvArgs& a, int nblocks, hipStream_t s) {
 // parallel.
 template <int E>
 void spmv_launch_epi(const SpmvArgs& a, int nblocks, hipStream_t s) {
+  if (use_dia<E>(a)) {
+    spmv_dia_launch<E>(a, nblocks, s);
+    return;
+  }
   if (a.dense) {
     if constexpr (is_virtual<E>())
       throw Failure(KR_ERR_INVALID, "fused first step has no dense kernel");

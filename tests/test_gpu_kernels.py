@@ -296,18 +296,27 @@ MASKED = {
     "offsets64": (lambda: _offset_matrix(6000, np.arange(-32, 32) * 3 + 1, 8, 3), 64),
     "offsets65": (lambda: _offset_matrix(6000, np.arange(-32, 33) * 3, 8, 4), 0),
     "unsorted": (lambda: _offset_matrix(3000, np.arange(-3, 4), 4, 5, sort=False), 0),
-    "long_rows": (lambda: golden_matrix(["banded", 3001, 13, 64, 0]), 0),
+    # long rows: masks (and the diagonal-offset values) only with KR_DIA on
+    "long_rows": (lambda: golden_matrix(["banded", 3001, 13, 64, 0]), 32),
+    "long_rows_63": (lambda: golden_matrix(["banded", 2000, 31, 256, 0]), 64),
 }
 
 
+@pytest.mark.parametrize("dia", ["2", "1", "0"])
 @pytest.mark.parametrize("shards", [1, 3])
 @pytest.mark.parametrize("name", list(MASKED))
-def test_offset_mask_layout_spmv_bitwise(torch_dev, monkeypatch, name, shards):
-    """Short-row matrices with <= 64 distinct column offsets use the offset-
-    mask layout (no column stream); the SpMV stays bitwise scipy's, with
-    KR_MASK=0 (plain columns) as the control."""
+def test_offset_mask_layout_spmv_bitwise(torch_dev, monkeypatch, name, shards, dia):
+    """Matrices with <= 64 distinct column offsets (stencils, banded) use the
+    offset-mask layout: the diagonal-offset SpMV (long rows by default,
+    KR_DIA=1; every masked shard with KR_DIA=2) or the short-row row walk
+    without a column stream (short rows; KR_DIA=0 for every shard).
+    The SpMV stays bitwise scipy's, with KR_MASK=0 (plain columns) as the
+    control."""
     from parallel_krylov_amd.system import KrylovSystem, balanced_partition
     builder, bits = MASKED[name]
+    if dia == "0" and name.startswith("long_rows"):
+        bits = 0
+    monkeypatch.setenv("KR_DIA", dia)
     A = builder()
     n = A.shape[0]
     x = np.random.default_rng(9).standard_normal(n)
