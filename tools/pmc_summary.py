@@ -18,7 +18,7 @@ import sys
 # Names follow kr_internal.h's SpmvEpi / EwOp enums (and kr_engine's epi_name/ew_name).
 EPI = ["spmv", "spmv_bminus", "spmv_xy", "spmv_head_mrr", "spmv_head_kcg", "spmv_mrr_loop",
        "spmv2", "spmv2_gram_mrr", "spmv2_gram_kcg", "spmv_step_mrr_nox", "spmv_step_mrr_x2",
-       "spmv_step_mrr_x", "spmv_step_kcg"]
+       "spmv_step_mrr_x", "spmv_step_kcg", "spmv_step_mrr_first2"]
 EW = ["dot", "update_mrr_first", "update_mrr", "update_cg", "update_cg_p", "update_kcg",
       "mrr_s", "copy", "update_mrr_nox", "update_mrr_x2"]
 
@@ -27,6 +27,9 @@ def short(name):
     m = re.search(r"spmv_kernel\w*<(\w+), (\d+), (\w+)", name)
     if m:
         return EPI[int(m.group(2))] + ("" if m.group(1) == "int" else "_rp64")
+    m = re.search(r"(spmv_dia|gemv)_kernel<(\d+)\b", name)
+    if m:
+        return EPI[int(m.group(2))] + ("_dia" if m.group(1) == "spmv_dia" else "_dense")
     m = re.search(r"ew_kernel<(\d+), (\w+)", name)
     if m:
         return EW[int(m.group(1))] + ("" if m.group(2) == "true" else "_scalar")
