@@ -77,6 +77,29 @@ int kr_dot_f64(const double* u_dev, const double* v_dev, int64_t n, double* out_
 int kr_multidot_f64(const double* const* u_ptrs_host, const double* const* v_ptrs_host,
                     int count, int64_t n, double* out_dev, void* stream);
 
+/* *out_dev = ||u||_2 = sqrt(<u, u>) (same reduction as kr_dot_f64).
+ * Replaces cupy.linalg.norm, e.g. v3/gpu/kskipmrr.py:26,42 and v3/gpu/common.py:33. */
+int kr_norm2_f64(const double* u_dev, int64_t n, double* out_dev, void* stream);
+
+/* k-skip MrR Gram coefficients (v3/gpu/kskipmrr.py:53-61) of the basis rows
+ * Ar[0..k+1] and Ay[0..k], row m at ar_dev + m*ld (ld >= n):
+ *   out[0 .. 2k+3)            alpha[j] = <Ar[j/2], Ar[j/2 + j%2]>
+ *   out[2k+3 .. 4k+5)         beta[j]  = <Ay[j/2], Ar[j/2 + j%2]>, beta[0] = 0
+ *   out[4k+5 .. 6k+6)         delta[j] = <Ay[j/2], Ay[j/2 + j%2]>
+ * i.e. the 6k+5 dots plus beta[0], laid out as the alpha/beta/delta arrays
+ * kr_kskipmrr_recurrence takes. The solver engine fuses these products into
+ * the basis SpMVs instead; this entry point serves callers with their own basis. */
+int kr_gram_kskipmrr_f64(const double* ar_dev, const double* ay_dev, int k, int64_t n,
+                         int64_t ld, double* out_dev, void* stream);
+
+/* k-skip CG Gram coefficients (v3/gpu/kskipcg.py:44-52) of Ar[0..k], Ap[0..k+1]:
+ *   out[0 .. 2k+1)            a[j] = <Ar[j/2], Ar[j/2 + j%2]>
+ *   out[2k+1 .. 4k+5)         f[j] = <Ap[j/2], Ap[j/2 + j%2]>, f[2k+3] = 0
+ *                             (the reference dots with the never-computed Ap[k+2])
+ *   out[4k+5 .. 6k+7)         c[j] = <Ar[j/2], Ap[j/2 + j%2]>                     */
+int kr_gram_kskipcg_f64(const double* ar_dev, const double* ap_dev, int k, int64_t n,
+                        int64_t ld, double* out_dev, void* stream);
+
 /* Fused k-skip MrR / MrR vector step (v3/gpu/kskipmrr.py:67-71):
  *   y = eta*y + zeta*ar1 ; z = eta*z - zeta*r ; r -= y ; x -= z
  * rounded exactly like the numpy statements (no FMA). first != 0 selects the
@@ -114,6 +137,21 @@ typedef struct kr_comm kr_comm;
 int kr_comm_unique_id(uint8_t* id_out /* KR_UNIQUE_ID_BYTES */);
 int kr_comm_init(kr_comm** comm, const uint8_t* id, int nranks, int rank, int device);
 int kr_comm_destroy(kr_comm* comm);
+
+/* In-place sum over the ranks of buf_dev[0..count) (ncclAllReduce). Replaces
+ * the Allgather + host sum of the reference's distributed dots
+ * (v3/gpu/mpi/common.py:163). The solver engine all-gathers the per-rank
+ * partials instead and sums them in rank order (deterministic histories). */
+int kr_allreduce_sum_f64(kr_comm* comm, double* buf_dev, int64_t count, void* stream);
+
+/* Halo exchange of one halo-extended vector x_dev: pieces are (peer, first
+ * element of x_dev, count) triples, nsend sent and nrecv received in one RCCL
+ * group (ncclSend/ncclRecv). The element offsets are local: global row g of a
+ * kr_halo_plan piece lives at g - row0 + pad in the System layout. Replaces
+ * the full-vector broadcast + gather of MultiGpu.dot (v3/gpu/common.py:115-122,
+ * v3/gpu/mpi/common.py:154-163). */
+int kr_halo_exchange_f64(kr_comm* comm, double* x_dev, const int64_t* recv, int nrecv,
+                         const int64_t* send, int nsend, void* stream);
 
 /* ------------------------------------------------------------------------
  * Distributed system: A and every vector row-partitioned into contiguous

@@ -65,6 +65,9 @@ _SIGNATURES = {
     "kr_spmv2_csr_f64": [_P, _I, _P, _P, _I64, _P, _P, _P, _P, _P],
     "kr_dot_f64": [_P, _P, _I64, _P, _P],
     "kr_multidot_f64": [_PP, _PP, _I, _I64, _P, _P],
+    "kr_norm2_f64": [_P, _I64, _P, _P],
+    "kr_gram_kskipmrr_f64": [_P, _P, _I, _I64, _I64, _P, _P],
+    "kr_gram_kskipcg_f64": [_P, _P, _I, _I64, _I64, _P, _P],
     "kr_update_mrr_f64": [_D, _D, _I, _P, _P, _P, _P, _P, _I64, _P],
     "kr_update_cg_f64": [_D, _P, _P, _P, _P, _I64, _P],
     "kr_kskipmrr_recurrence": [_I, _PD, _PD, _PD, _PD, _PD],
@@ -73,6 +76,8 @@ _SIGNATURES = {
     "kr_comm_unique_id": [_P],
     "kr_comm_init": [_PP, _P, _I, _I, _I],
     "kr_comm_destroy": [_P],
+    "kr_allreduce_sum_f64": [_P, _P, _I64, _P],
+    "kr_halo_exchange_f64": [_P, _P, _PI64, _I, _PI64, _I, _P],
     "kr_system_create": [_PP, _I64, _I, _PI, _PI64, _P],
     "kr_system_destroy": [_P],
     "kr_system_adopt_csr": [_P, _I, _P, _I, _P, _P],

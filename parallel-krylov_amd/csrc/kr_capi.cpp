@@ -173,6 +173,88 @@ int kr_multidot_f64(const double* const* u_ptrs, const double* const* v_ptrs, in
   });
 }
 
+int kr_norm2_f64(const double* u, int64_t n, double* out, void* stream) {
+  return guarded([&] {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int rc = kr_dot_f64(u, u, n, out, stream);
+    if (rc != 0) throw Failure(rc, g_last_error);
+    launch_sqrt(out, s);
+  });
+}
+
+namespace {
+// Gram pairs (u row, v row, output index) in ranges of <= 64, one multidot each.
+struct GramPair {
+  const double* u;
+  const double* v;
+  int out;
+};
+
+void gram_run(const std::vector<GramPair>& pairs, int64_t n, double* out, hipStream_t s) {
+  for (size_t base = 0; base < pairs.size(); base += 64) {
+    const int count = (int)std::min<size_t>(64, pairs.size() - base);
+    MultiDotArgs a{};
+    for (int i = 0; i < count; ++i) {
+      a.u[i] = pairs[base + i].u;
+      a.v[i] = pairs[base + i].v;
+    }
+    a.count = count;
+    a.n = n;
+    a.grid = default_grid(n);
+    a.partials = primitive_scratch((size_t)count * a.grid);
+    // Finalize into a contiguous staging range, then scatter: the outputs of
+    // one range are consecutive by construction (pairs are listed in order).
+    launch_multidot(a, s);
+    launch_finalize(a.partials, a.grid, count, out + pairs[base].out, s);
+  }
+}
+}  // namespace
+
+int kr_gram_kskipmrr_f64(const double* ar, const double* ay, int k, int64_t n, int64_t ld,
+                         double* out, void* stream) {
+  return guarded([&] {
+    KR_REQUIRE(k >= 0 && n >= 0 && ld >= n && out, "bad arguments");
+    KR_REQUIRE(n == 0 || (ar && ay), "NULL operand");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int na = 2 * k + 3, nb = 2 * k + 2;
+    std::vector<GramPair> pairs;
+    for (int j = 0; j < na; ++j)  // alpha[j] = <Ar[j/2], Ar[j/2 + j%2]>
+      pairs.push_back({ar + (j / 2) * ld, ar + (j / 2 + j % 2) * ld, j});
+    for (int j = 1; j < nb; ++j)  // beta[j] = <Ay[j/2], Ar[j/2 + j%2]>, beta[0] = 0
+      pairs.push_back({ay + (j / 2) * ld, ar + (j / 2 + j % 2) * ld, na + j});
+    for (int j = 0; j < 2 * k + 1; ++j)  // delta[j] = <Ay[j/2], Ay[j/2 + j%2]>
+      pairs.push_back({ay + (j / 2) * ld, ay + (j / 2 + j % 2) * ld, na + nb + j});
+    KR_HIP_CHECK(hipMemsetAsync(out + na, 0, sizeof(double), s));
+    // alpha (contiguous), then beta[1..] + delta (contiguous from na + 1).
+    std::vector<GramPair> first(pairs.begin(), pairs.begin() + na);
+    std::vector<GramPair> rest(pairs.begin() + na, pairs.end());
+    gram_run(first, n, out, s);
+    gram_run(rest, n, out, s);
+  });
+}
+
+int kr_gram_kskipcg_f64(const double* ar, const double* ap, int k, int64_t n, int64_t ld,
+                        double* out, void* stream) {
+  return guarded([&] {
+    KR_REQUIRE(k >= 0 && n >= 0 && ld >= n && out, "bad arguments");
+    KR_REQUIRE(n == 0 || (ar && ap), "NULL operand");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int na = 2 * k + 1, nf = 2 * k + 4, nc = 2 * k + 2;
+    std::vector<GramPair> pairs;
+    for (int j = 0; j < na; ++j)  // a[j] = <Ar[j/2], Ar[j/2 + j%2]>
+      pairs.push_back({ar + (j / 2) * ld, ar + (j / 2 + j % 2) * ld, j});
+    for (int j = 0; j < nf - 1; ++j)  // f[j] = <Ap[j/2], Ap[j/2 + j%2]>; f[2k+3] = 0
+      pairs.push_back({ap + (j / 2) * ld, ap + (j / 2 + j % 2) * ld, na + j});
+    for (int j = 0; j < nc; ++j)  // c[j] = <Ar[j/2], Ap[j/2 + j%2]>
+      pairs.push_back({ar + (j / 2) * ld, ap + (j / 2 + j % 2) * ld, na + nf + j});
+    KR_HIP_CHECK(hipMemsetAsync(out + na + nf - 1, 0, sizeof(double), s));
+    std::vector<GramPair> first(pairs.begin(), pairs.begin() + na + nf - 1);
+    std::vector<GramPair> rest(pairs.begin() + na + nf - 1, pairs.end());
+    gram_run(first, n, out, s);
+    gram_run(rest, n, out, s);
+  });
+}
+
 int kr_update_mrr_f64(double eta, double zeta, int first, double* y, const double* ar1,
                       double* z, double* r, double* x, int64_t n, void* stream) {
   return guarded([&] {
@@ -287,6 +369,45 @@ int kr_comm_destroy(kr_comm* comm) {
     if (!comm) return;
     if (comm->nccl) ncclCommDestroy(comm->nccl);
     delete comm;
+  });
+}
+
+int kr_allreduce_sum_f64(kr_comm* comm, double* buf, int64_t count, void* stream) {
+  return guarded([&] {
+    KR_REQUIRE(comm && count >= 0, "bad arguments");
+    if (count == 0) return;
+    KR_REQUIRE(buf, "NULL operand");
+    if (comm->nranks == 1 || !comm->nccl) return;  // one rank: the sum is the buffer
+    KR_NCCL_CHECK(ncclAllReduce(buf, buf, (size_t)count, ncclDouble, ncclSum, comm->nccl,
+                                static_cast<hipStream_t>(stream)));
+  });
+}
+
+int kr_halo_exchange_f64(kr_comm* comm, double* x, const int64_t* recv, int nrecv,
+                         const int64_t* send, int nsend, void* stream) {
+  return guarded([&] {
+    KR_REQUIRE(comm && nrecv >= 0 && nsend >= 0, "bad arguments");
+    KR_REQUIRE((nrecv == 0 || recv) && (nsend == 0 || send), "NULL piece list");
+    if (nrecv + nsend == 0) return;
+    KR_REQUIRE(x, "NULL operand");
+    KR_REQUIRE(comm->nccl, "communicator has no RCCL handle");
+    for (int q = 0; q < nrecv; ++q)
+      KR_REQUIRE(recv[3 * q] >= 0 && recv[3 * q] < comm->nranks && recv[3 * q + 1] >= 0 &&
+                     recv[3 * q + 2] >= 0,
+                 "bad receive piece");
+    for (int q = 0; q < nsend; ++q)
+      KR_REQUIRE(send[3 * q] >= 0 && send[3 * q] < comm->nranks && send[3 * q + 1] >= 0 &&
+                     send[3 * q + 2] >= 0,
+                 "bad send piece");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    KR_NCCL_CHECK(ncclGroupStart());
+    for (int q = 0; q < nsend; ++q)
+      KR_NCCL_CHECK(ncclSend(x + send[3 * q + 1], (size_t)send[3 * q + 2], ncclDouble,
+                             (int)send[3 * q], comm->nccl, s));
+    for (int q = 0; q < nrecv; ++q)
+      KR_NCCL_CHECK(ncclRecv(x + recv[3 * q + 1], (size_t)recv[3 * q + 2], ncclDouble,
+                             (int)recv[3 * q], comm->nccl, s));
+    KR_NCCL_CHECK(ncclGroupEnd());
   });
 }
 

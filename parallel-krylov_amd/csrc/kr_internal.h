@@ -165,6 +165,7 @@ constexpr int kFinalizeSlots = 128;
 struct SlotCounts {
   int n[kFinalizeSlots];
 };
+void launch_sqrt(double* p, hipStream_t s);  // p[0] = sqrt(p[0]) (cupy.linalg.norm)
 void launch_finalize_counts(const double* partials, int stride, const SlotCounts& counts,
                             int nslots, double* out, hipStream_t s);
 

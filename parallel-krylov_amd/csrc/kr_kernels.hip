@@ -646,6 +646,15 @@ void launch_finalize(const double* partials, int grid, int nslots, double* out,
   KR_HIP_CHECK(hipGetLastError());
 }
 
+__global__ void sqrt_kernel(double* p) {
+  if (threadIdx.x == 0) p[0] = sqrt(p[0]);
+}
+
+void launch_sqrt(double* p, hipStream_t s) {
+  sqrt_kernel<<<1, 64, 0, s>>>(p);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
 void launch_finalize_counts(const double* partials, int stride, const SlotCounts& counts,
                             int nslots, double* out, hipStream_t s) {
   if (nslots <= 0) return;

@@ -148,6 +148,102 @@ def test_multidot_matches_dot(torch_dev):
         assert abs(out[q].item() - exact) <= 1e-12 * np.abs(Vh[i] * Vh[j]).sum()
 
 
+def test_norm2(torch_dev):
+    import torch
+    n = 123457
+    u = np.random.default_rng(5).standard_normal(n)
+    out = torch.zeros(1, dtype=torch.float64, device=torch_dev)
+    ut = _t(u, torch_dev)
+    _sync()
+    assert _lib().kr_norm2_f64(ut.data_ptr(), n, out.data_ptr(), None) == 0
+    _sync()
+    assert abs(out.item() - math.sqrt(math.fsum(u * u))) <= 1e-13 * out.item()
+
+
+def _gram_ref(rows_u, rows_v, m):
+    """out[j] = <U[j//2], V[j//2 + j%2]> for j < m (the reference's Gram loops)."""
+    return [math.fsum(rows_u[j // 2] * rows_v[j // 2 + j % 2]) for j in range(m)]
+
+
+@pytest.mark.parametrize("k", [0, 1, 4, 12])
+def test_gram_kskipmrr_matches_reference_loops(torch_dev, k):
+    """kr_gram_kskipmrr_f64 = the alpha/beta/delta loops of
+    v3/gpu/kskipmrr.py:53-61 (k=12: 77 dots, more than one multidot range),
+    on strided basis rows (ld > n)."""
+    import torch
+    n, ld = 20011, 20011 + 5
+    rng = np.random.default_rng(k)
+    Ar = rng.standard_normal((k + 2, ld))
+    Ay = rng.standard_normal((k + 1, ld))
+    out = torch.full((6 * k + 6,), np.nan, dtype=torch.float64, device=torch_dev)
+    art, ayt = _t(Ar, torch_dev), _t(Ay, torch_dev)
+    _sync()
+    assert _lib().kr_gram_kskipmrr_f64(art.data_ptr(), ayt.data_ptr(), k, n, ld,
+                                       out.data_ptr(), None) == 0
+    _sync()
+    o = out.cpu().numpy()
+    Arn, Ayn = Ar[:, :n], Ay[:, :n]
+    alpha = _gram_ref(Arn, Arn, 2 * k + 3)
+    beta = [0.0] + _gram_ref(Ayn, Arn, 2 * k + 2)[1:]
+    delta = _gram_ref(Ayn, Ayn, 2 * k + 1)
+    ref = np.array(alpha + beta + delta)
+    assert o[2 * k + 3] == 0.0
+    np.testing.assert_allclose(o, ref, rtol=0, atol=1e-12 * n)
+
+
+@pytest.mark.parametrize("k", [0, 3, 10])
+def test_gram_kskipcg_matches_reference_loops(torch_dev, k):
+    """kr_gram_kskipcg_f64 = the a/f/c loops of v3/gpu/kskipcg.py:44-52, with
+    f[2k+3] = 0 (the reference dots Ap[k+1] with the never-computed Ap[k+2])."""
+    import torch
+    n, ld = 9001, 9001
+    rng = np.random.default_rng(100 + k)
+    Ar = rng.standard_normal((k + 1, ld))
+    Ap = rng.standard_normal((k + 2, ld))
+    out = torch.full((6 * k + 7,), np.nan, dtype=torch.float64, device=torch_dev)
+    art, apt = _t(Ar, torch_dev), _t(Ap, torch_dev)
+    _sync()
+    assert _lib().kr_gram_kskipcg_f64(art.data_ptr(), apt.data_ptr(), k, n, ld,
+                                      out.data_ptr(), None) == 0
+    _sync()
+    o = out.cpu().numpy()
+    Ap0 = np.vstack([Ap, np.zeros((1, ld))])
+    a = _gram_ref(Ar, Ar, 2 * k + 1)
+    f = _gram_ref(Ap0, Ap0, 2 * k + 4)
+    c = _gram_ref(Ar, Ap0, 2 * k + 2)
+    np.testing.assert_allclose(o, np.array(a + f + c), rtol=0, atol=1e-12 * n)
+    assert o[2 * k + 1 + 2 * k + 3] == 0.0
+
+
+def test_comm_single_rank_allreduce_and_halo(torch_dev):
+    """The RCCL primitives on a one-rank communicator: the all-reduce leaves
+    the buffer as is; a halo exchange with pieces to and from rank 0 itself
+    copies the sent rows to the received positions (ncclSend/ncclRecv to self)."""
+    import torch
+    from parallel_krylov_amd.system import Communicator
+    comm = Communicator(0, 1, torch_dev.index or 0, lambda data: data)
+    lib = _lib()
+    buf = _t(np.arange(7, dtype=np.float64), torch_dev)
+    _sync()
+    assert lib.kr_allreduce_sum_f64(comm.handle, buf.data_ptr(), 7, None) == 0
+    _sync()
+    np.testing.assert_array_equal(buf.cpu().numpy(), np.arange(7.0))
+    x = np.random.default_rng(9).standard_normal(5000)
+    xt = _t(x, torch_dev)
+    send = (ctypes.c_int64 * 6)(0, 100, 300, 0, 2000, 17)
+    recv = (ctypes.c_int64 * 6)(0, 4000, 300, 0, 4500, 17)
+    _sync()
+    assert lib.kr_halo_exchange_f64(comm.handle, xt.data_ptr(), recv, 2, send, 2, None) == 0
+    _sync()
+    ref = x.copy()
+    ref[4000:4300] = x[100:400]
+    ref[4500:4517] = x[2000:2017]
+    np.testing.assert_array_equal(xt.cpu().numpy(), ref)
+    bad = (ctypes.c_int64 * 3)(1, 0, 1)  # peer 1 of a one-rank communicator
+    assert lib.kr_halo_exchange_f64(comm.handle, xt.data_ptr(), bad, 1, None, 0, None) < 0
+    comm.close()
+
+
 @pytest.mark.parametrize("n,offset", [(1, 0), (4097, 0), (4097, 1), (300000, 0)])
 @pytest.mark.parametrize("first", [0, 1])
 def test_update_mrr_bitwise(torch_dev, n, offset, first):
