@@ -698,6 +698,7 @@ int kr_solve_step(kr_system* sys, int64_t max_outer, int* done) {
     for (int64_t c = 0; c < max_outer && !ss.done; ++c) {
       // profile = N: per-kernel events on every N-th outer iteration only
       sys->prof_active = (sys->prof_tick++ % sys->profile_every) == 0;
+      ss.hint = max_outer - c;
       ss.step_once();
     }
     if (done) *done = ss.done ? 1 : 0;

@@ -153,6 +153,8 @@ System::~System() {
     if (s.slots) (void)hipFree(s.slots);
     if (s.gather) (void)hipFree(s.gather);
     if (s.host) (void)hipHostFree(s.host);
+    if (s.st) (void)hipFree(s.st);
+    if (s.hst) (void)hipHostFree(s.hst);
     for (auto& p : s.pending) {
       (void)hipEventDestroy(p.t0);
       (void)hipEventDestroy(p.t1);
@@ -623,6 +625,7 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
       }
     }
     a.epi_late = epi_late;
+    a.stop = dev_stop;
     a.nnz_total = s.nnz;
     if (s.dense) {
       a.dense = 1;
@@ -736,6 +739,97 @@ void System::ew(EwOp op, double c0, double c1, std::array<int, 6> ids, int slot0
   }
 }
 
+bool System::device_scalars() const {
+  const char* env = getenv("KR_DEVICE_SCALARS");  // 0: one host sync per reduction (A/B)
+  if (env && atoi(env) == 0) return false;
+  return shards.size() == 1 && !comm;
+}
+
+void System::scalar_state_init(double gamma) {
+  Shard& s = shards[0];
+  KR_HIP_CHECK(hipSetDevice(s.dev));
+  if (!s.st) {
+    KR_HIP_CHECK(hipMalloc(&s.st, sizeof(double) * kScalarState));
+    KR_HIP_CHECK(hipHostMalloc(&s.hst, sizeof(double) * kScalarState, 0));
+  }
+  KR_HIP_CHECK(hipStreamSynchronize(s.stream));  // hst is free
+  for (int q = 0; q < kScalarState; ++q) s.hst[q] = 0.0;
+  s.hst[ST_GAMMA] = gamma;
+  KR_HIP_CHECK(hipMemcpyAsync(s.st, s.hst, sizeof(double) * kScalarState,
+                              hipMemcpyHostToDevice, s.stream));
+}
+
+void System::ew_dev(EwOp op, int coef, std::array<int, 6> ids, int slot0) {
+  KR_REQUIRE(slot0 + ew_products(op) <= kMaxSlots, "reduction slots exhausted");
+  Shard& s = shards[0];
+  EwArgs a;
+  for (int q = 0; q < 6; ++q) a.p[q] = ids[q] >= 0 ? s.own(ids[q]) : nullptr;
+  a.n = s.n;
+  a.partials = s.partials + (size_t)slot0 * s.pstride;
+  a.grid = s.grid;
+  a.stride = s.pstride;
+  a.cdev = s.st + coef;
+  a.stop = dev_stop;
+  for (int p = 0; p < ew_products(op); ++p) s.slot_n[slot0 + p] = s.grid;
+  hipEvent_t t0 = nullptr;
+  const char* nm = ew_name(op);
+  prof_begin(s, nm, t0);
+  launch_ew(op, a, s.stream);
+  prof_end(s, nm, t0, 8.0 * ew_vectors(op) * s.n);
+}
+
+void System::scalar(ScalarOp op, int need, int64_t it, int h, double thr, int check) {
+  Shard& s = shards[0];
+  ScalarArgs a;
+  a.op = op;
+  a.need = need;
+  a.partials = s.partials;
+  a.stride = s.pstride;
+  for (int q = 0; q < 5; ++q) a.cnt[q] = s.slot_n[q];
+  a.st = s.st;
+  a.it = it;
+  a.h = h;
+  a.check = check;
+  a.thr = thr;
+  hipEvent_t t0 = nullptr;
+  prof_begin(s, "scalar", t0);
+  launch_scalar(a, s.stream);
+  prof_end(s, "scalar", t0, 8.0 * s.pstride * __builtin_popcount(need));
+}
+
+void System::scalar_state_read() {
+  Shard& s = shards[0];
+  KR_HIP_CHECK(hipMemcpyAsync(s.hst, s.st, sizeof(double) * kScalarState,
+                              hipMemcpyDeviceToHost, s.stream));
+  KR_HIP_CHECK(hipStreamSynchronize(s.stream));
+  size_t pend = s.pending.size();
+  if (pend > 512) harvest_profile();
+}
+
+// conv(g) = sqrt(g)/||b|| < tol, the reference's test on a squared norm g,
+// is monotone in g >= 0 (sqrt and division by ||b|| > 0 are correctly rounded,
+// hence monotone), so it equals 0 <= g < thr for the smallest non-negative
+// double thr with !conv(thr): found by bisection over the bit patterns with
+// the host's own arithmetic. The device test is then bitwise the host's.
+double conv_threshold(double bnorm, double tol) {
+  auto conv = [&](double g) { return std::sqrt(g) / bnorm < tol; };
+  auto dbl = [](uint64_t b) {
+    double d;
+    std::memcpy(&d, &b, 8);
+    return d;
+  };
+  if (!conv(0.0)) return 0.0;
+  uint64_t lo = 0, hi = 0x7FF0000000000000ull;  // conv(+0) true; conv(+inf) false
+  while (hi - lo > 1) {
+    const uint64_t mid = lo + (hi - lo) / 2;
+    if (conv(dbl(mid)))
+      lo = mid;
+    else
+      hi = mid;
+  }
+  return dbl(hi);
+}
+
 void System::copy_own(int dst, int src) {
   for (auto& s : shards) {
     KR_HIP_CHECK(hipSetDevice(s.dev));
@@ -815,11 +909,59 @@ class Base : public Session {
   void start_timer() { t_start = now_seconds(); }
 };
 
+// Device-resident scalar batches (CG, MrR on one shard): up to
+// kScalarBatch iterations are enqueued at once; the scalars live in Shard::st
+// and the convergence test runs on the device (scalar_kernel), which then
+// stops every later kernel of the batch. The host syncs once per batch and
+// replays the bookkeeping from the recorded norms, checking that the device
+// stopped exactly where its own test says (conv_threshold makes the two tests
+// bitwise the same). KR_DEVICE_SCALARS=0 restores one sync per reduction.
+int scalar_batch() {
+  const char* env = getenv("KR_SCALAR_BATCH");
+  const int b = env ? atoi(env) : 32;
+  return std::max(1, std::min(b, kScalarBatch));
+}
+
 // --------------------------------------------------------------------- CG
 // v3/gpu/cg.py:8-51 (oracle v3/cpu/cg.py:7-48)
 class CgSession : public Base {
   enum { X, B, R, P, V, NV };
   double gamma = 0;
+  bool dev = false;
+  double thr = 0;
+  std::vector<double> q;  // gamma of the iterations of the current batch
+  size_t qpos = 0;
+
+  // Iterations i .. i+m-1 on the device; q[j] = gamma at the top of i+j+1.
+  void run_batch() {
+    const int64_t m = std::min<int64_t>({(int64_t)scalar_batch(), std::max<int64_t>(hint, 1),
+                                         prm.maxiter - i});
+    sys->dev_stop = sys->shards[0].st + ST_STOP;
+    for (int64_t j = 0; j < m; ++j) {
+      if (j > 0) sys->prof_active = (sys->prof_tick++ % sys->profile_every) == 0;
+      sys->spmv(EPI_XY, P, -1, V, -1, -1, -1, 0);              // v = A p ; sigma
+      sys->scalar(SC_CG_ALPHA, 1 << 1, i + j, (int)j, thr);     // alpha = gamma / sigma
+      sys->ew_dev(EW_CG, ST_C0, {X, P, R, V, -1, -1}, 0);       // x += a p ; r -= a v
+      sys->scalar(SC_CG_BETA, 1 << 0, i + j, (int)j, thr);      // beta, gamma, test
+      sys->ew_dev(EW_CG_P, ST_C2, {P, R, -1, -1, -1, -1}, 0);  // p = r + b p
+    }
+    sys->dev_stop = nullptr;
+    sys->scalar_state_read();
+    const double* h = sys->shards[0].hst;
+    q.assign(h + ST_HIST, h + ST_HIST + m);
+    qpos = 0;
+    int64_t stop_at = -1;
+    for (int64_t j = 0; j < m; ++j)
+      if (i + j + 1 < prm.maxiter && rel(q[j]) < prm.tol) {
+        stop_at = i + j + 1;
+        q.resize(j + 1);
+        break;
+      }
+    const bool dstop = h[ST_STOP] != 0.0;
+    if (stop_at >= 0 ? !(dstop && (int64_t)h[ST_STOP_AT] == stop_at)
+                     : (dstop && (int64_t)h[ST_STOP_AT] < prm.maxiter))
+      throw Failure(KR_ERR_INVALID, "device/host convergence test disagree (CG)");
+  }
 
  public:
   void begin(const double* const* b, const double* const* x0) override {
@@ -828,6 +970,11 @@ class CgSession : public Base {
     sys->spmv(EPI_BMINUS, X, -1, R, -1, -1, B, 0);  // r = b - A x
     gamma = sys->reduce(1)[0];                      // gamma = <r,r>
     sys->copy_own(P, R);                            // p = r.copy()
+    dev = sys->device_scalars();
+    if (dev) {
+      thr = conv_threshold(bnorm, prm.tol);
+      sys->scalar_state_init(gamma);
+    }
     i = 0;
     index = 0;
     set_nosl(0, 0);
@@ -845,14 +992,19 @@ class CgSession : public Base {
       converged = true;
       return done = true;
     }
-    sys->spmv(EPI_XY, P, -1, V, -1, -1, -1, 0);  // v = A p ; sigma = <p,v>
-    const double sigma = sys->reduce(3)[1];
-    const double alpha = gamma / sigma;
-    sys->ew(EW_CG, alpha, 0, {X, P, R, V, -1, -1}, 0);  // x += a p ; r -= a v
-    const double gnew = sys->reduce(1)[0];
-    const double beta = gnew / gamma;
-    gamma = gnew;
-    sys->ew(EW_CG_P, beta, 0, {P, R, -1, -1, -1, -1}, 0);  // p = r + b p
+    if (dev) {
+      if (qpos >= q.size()) run_batch();
+      gamma = q[qpos++];
+    } else {
+      sys->spmv(EPI_XY, P, -1, V, -1, -1, -1, 0);  // v = A p ; sigma = <p,v>
+      const double sigma = sys->reduce(3)[1];
+      const double alpha = gamma / sigma;
+      sys->ew(EW_CG, alpha, 0, {X, P, R, V, -1, -1}, 0);  // x += a p ; r -= a v
+      const double gnew = sys->reduce(1)[0];
+      const double beta = gnew / gamma;
+      gamma = gnew;
+      sys->ew(EW_CG_P, beta, 0, {P, R, -1, -1, -1, -1}, 0);  // p = r + b p
+    }
     i += 1;
     set_nosl(i, i);
     index = i;
@@ -866,6 +1018,40 @@ class CgSession : public Base {
 // v3/gpu/mrr.py:8-65 (oracle v3/cpu/mrr.py:7-61)
 class MrrSession : public Base {
   enum { X, B, R, Y, Z, AR, NV };
+  bool dev = false;
+  double thr = 0;
+  std::vector<double> q;  // <r,r> at the top of the iterations of the batch
+  size_t qpos = 0;
+
+  // Iterations i .. i+m-1 on the device; q[j] = <r,r> at the top of i+j.
+  void run_batch() {
+    const int64_t m = std::min<int64_t>({(int64_t)scalar_batch(), std::max<int64_t>(hint, 1),
+                                         prm.maxiter - i});
+    sys->dev_stop = sys->shards[0].st + ST_STOP;
+    for (int64_t j = 0; j < m; ++j) {
+      if (j > 0) sys->prof_active = (sys->prof_tick++ % sys->profile_every) == 0;
+      sys->spmv(EPI_MRR_LOOP, R, -1, AR, -1, Y, -1, 0);            // Ar = A r ; <r,r> mu nu
+      sys->scalar(SC_MRR_GAMMA, 0x7, i + j, (int)j, thr);          // test ; gamma = nu / mu
+      sys->ew_dev(EW_MRR_S, ST_C0, {AR, Y, R, -1, -1, -1}, 3);     // s ; <r,s> <s,s>
+      sys->scalar(SC_MRR_ZETA, 0x18, i + j, (int)j, thr);          // zeta, eta
+      sys->ew_dev(EW_MRR, ST_C2, {Y, AR, Z, R, X, X}, 0);
+    }
+    sys->dev_stop = nullptr;
+    sys->scalar_state_read();
+    const double* h = sys->shards[0].hst;
+    q.assign(h + ST_HIST, h + ST_HIST + m);
+    qpos = 0;
+    int64_t stop_at = -1;
+    for (int64_t j = 0; j < m; ++j)
+      if (rel(q[j]) < prm.tol) {
+        stop_at = i + j;
+        q.resize(j + 1);
+        break;
+      }
+    const bool dstop = h[ST_STOP] != 0.0;
+    if (stop_at >= 0 ? !(dstop && (int64_t)h[ST_STOP_AT] == stop_at) : dstop)
+      throw Failure(KR_ERR_INVALID, "device/host convergence test disagree (MrR)");
+  }
 
  public:
   void begin(const double* const* b, const double* const* x0) override {
@@ -883,6 +1069,11 @@ class MrrSession : public Base {
     i = 1;
     index = 1;
     set_entry(1, 0.0);
+    dev = sys->device_scalars();
+    if (dev) {
+      thr = conv_threshold(bnorm, prm.tol);
+      sys->scalar_state_init(0.0);
+    }
   }
   bool step_once() override {
     if (i >= prm.maxiter) {
@@ -891,20 +1082,30 @@ class MrrSession : public Base {
       index = i;
       return done = true;
     }
-    sys->spmv(EPI_MRR_LOOP, R, -1, AR, -1, Y, -1, 0);  // Ar = A r ; <r,r> mu nu
-    const auto g = sys->reduce(3);
-    set_entry(i, rel(g[0]));
-    index = i;
-    if (residual[i] < prm.tol) {
-      converged = true;
-      return done = true;
+    if (dev) {
+      if (qpos >= q.size()) run_batch();
+      set_entry(i, rel(q[qpos++]));
+      index = i;
+      if (residual[i] < prm.tol) {
+        converged = true;
+        return done = true;
+      }
+    } else {
+      sys->spmv(EPI_MRR_LOOP, R, -1, AR, -1, Y, -1, 0);  // Ar = A r ; <r,r> mu nu
+      const auto g = sys->reduce(3);
+      set_entry(i, rel(g[0]));
+      index = i;
+      if (residual[i] < prm.tol) {
+        converged = true;
+        return done = true;
+      }
+      const double gamma = g[2] / g[1];  // nu / mu
+      sys->ew(EW_MRR_S, gamma, 0, {AR, Y, R, -1, -1, -1}, 0);
+      const auto h = sys->reduce(2);
+      const double zeta = h[0] / h[1];
+      const double eta = (-zeta) * gamma;
+      sys->ew(EW_MRR, eta, zeta, {Y, AR, Z, R, X, X}, 0);
     }
-    const double gamma = g[2] / g[1];  // nu / mu
-    sys->ew(EW_MRR_S, gamma, 0, {AR, Y, R, -1, -1, -1}, 0);
-    const auto h = sys->reduce(2);
-    const double zeta = h[0] / h[1];
-    const double eta = (-zeta) * gamma;
-    sys->ew(EW_MRR, eta, zeta, {Y, AR, Z, R, X, X}, 0);
     i += 1;
     set_nosl(i, i);
     index = i;

@@ -90,6 +90,8 @@ struct Shard {
   double* slots = nullptr;      // [kMaxSlots]
   double* gather = nullptr;     // [nranks][kMaxSlots] (RCCL)
   double* host = nullptr;       // pinned [nranks][kMaxSlots]
+  double* st = nullptr;         // device-resident CG/MrR scalars [kScalarState]
+  double* hst = nullptr;        // pinned copy of st
   // vectors, each ld doubles, zero-initialised
   std::vector<double*> vec;
   hipEvent_t ev_a = nullptr, ev_b = nullptr;
@@ -153,6 +155,16 @@ struct System {
   void spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int b, int slot0,
             const StepOps* st = nullptr);
   void ew(EwOp op, double c0, double c1, std::array<int, 6> ids, int slot0);
+  // Device-resident scalars (single shard, no communicator): the vector
+  // kernel takes c0, c1 from st[coef], st[coef + 1]; scalar() runs one
+  // scalar_kernel step over the reductions in slots `need`. While dev_stop is
+  // set, every SpMV / vector kernel skips itself once the test has fired.
+  bool device_scalars() const;
+  void scalar_state_init(double gamma);
+  void ew_dev(EwOp op, int coef, std::array<int, 6> ids, int slot0);
+  void scalar(ScalarOp op, int need, int64_t it, int h, double thr, int check = 1);
+  void scalar_state_read();  // st -> hst, synchronises the stream
+  const double* dev_stop = nullptr;
   // Device->host of the summed slots [0, nslots): the one host sync point.
   std::vector<double> reduce(int nslots);
   void copy_own(int dst, int src);
@@ -182,6 +194,7 @@ class Session {
   std::vector<int64_t> nosl, khist;
   bool track_k = false;
   double t_start = 0, t_end = 0;
+  int64_t hint = 1;  // iterations kr_solve_step still wants (device-scalar batches)
 
   void set_entry(int64_t idx, double res) {
     if ((int64_t)residual.size() <= idx) residual.resize(idx + 1, 0.0);

@@ -110,6 +110,7 @@ struct SpmvArgs {
   double* ud = nullptr;
   double c0 = 0, c1 = 0;
   const double* x3 = nullptr;  // EPI_STEP_MRR_FIRST2: Ar1 (halo-extended)
+  const double* stop = nullptr;  // skip the launch when *stop != 0 (EwArgs::stop)
   double c2 = 0, c3 = 0;       // EPI_STEP_MRR_FIRST2: step-1 scalars (eta1, zeta1)
   int epi_late = 0;  // 1: load own-row epilogue operands at the row end (A/B, KR_EPI_LATE)
   int64_t nnz_total = -1;  // entries of val/col (-1: unknown; spmv_kernel2 needs >= 4)
@@ -151,8 +152,38 @@ struct EwArgs {
   double* partials = nullptr;
   int grid = 0;                    // workgroups launched
   int stride = 0;                  // partial stride per slot (0: grid)
+  const double* cdev = nullptr;    // device-resident c0, c1 (cdev[0], cdev[1]) if set
+  const double* stop = nullptr;    // skip the launch when *stop != 0 (converged)
 };
 void launch_ew(EwOp op, const EwArgs& a, hipStream_t s);
+
+// Device-resident CG / MrR scalars (scalar_kernel). State layout:
+enum ScalarState : int {
+  ST_GAMMA = 0,    // CG gamma = <r,r> / MrR gamma = nu/mu
+  ST_C0 = 1,       // coefficients of the next vector kernels (EwArgs::cdev)
+  ST_C1 = 2,
+  ST_C2 = 3,
+  ST_C3 = 4,
+  ST_STOP = 5,     // 1.0 once the convergence test fired
+  ST_STOP_AT = 6,  // iteration at whose top it fired
+  ST_HIST = 8,     // ring of reduced norms, one per iteration of a batch
+};
+constexpr int kScalarBatch = 64;  // iterations per host sync (ring size)
+constexpr int kScalarState = ST_HIST + kScalarBatch;
+enum ScalarOp : int { SC_CG_ALPHA = 0, SC_CG_BETA, SC_MRR_GAMMA, SC_MRR_ZETA };
+struct ScalarArgs {
+  int op = 0;
+  int need = 0;                    // bit q: reduce slot q
+  const double* partials = nullptr;
+  int stride = 0;
+  int cnt[5] = {};
+  double* st = nullptr;
+  int64_t it = 0;                  // iteration number (ST_STOP_AT)
+  int h = 0;                       // ST_HIST index
+  int check = 1;                   // 0: no convergence test
+  double thr = 0;                  // converged <=> 0 <= g < thr
+};
+void launch_scalar(const ScalarArgs& a, hipStream_t s);
 
 // Sum partials[slot*grid .. +grid) for slots [0, nslots) into out[slot],
 // in a fixed order (deterministic).

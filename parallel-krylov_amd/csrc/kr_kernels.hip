@@ -155,6 +155,11 @@ __global__ __launch_bounds__(kBlock) void ew_kernel(EwArgs a) {
   using T = EwTraits<OP>;
   constexpr int NP = T::NP;
   __shared__ double s_red[(NP > 0 ? NP : 1) * 4];
+  // Device-resident scalars (CG/MrR without a host sync): stop once the
+  // convergence test fired; coefficients from the scalar kernel's output.
+  if (a.stop && *a.stop != 0.0) return;
+  const double c0 = a.cdev ? a.cdev[0] : a.c0;
+  const double c1 = a.cdev ? a.cdev[1] : a.c1;
   double acc[NP > 0 ? NP : 1];
 #pragma unroll
   for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;
@@ -185,8 +190,8 @@ __global__ __launch_bounds__(kBlock) void ew_kernel(EwArgs a) {
       for (int u = 0; u < U; ++u) {
         const int64_t q = q0 + u * stride;
         if (q >= npairs) break;
-        ew_elem<OP>(a.c0, a.c1, va[u], acc);
-        ew_elem<OP>(a.c0, a.c1, vb[u], acc);
+        ew_elem<OP>(c0, c1, va[u], acc);
+        ew_elem<OP>(c0, c1, vb[u], acc);
 #pragma unroll
         for (int k = 0; k < 6; ++k)
           if (T::W & (1 << k)) {
@@ -205,7 +210,7 @@ __global__ __launch_bounds__(kBlock) void ew_kernel(EwArgs a) {
       double v[6];
 #pragma unroll
       for (int k = 0; k < 6; ++k) v[k] = (T::R & (1 << k)) ? a.p[k][i] : 0.0;
-      ew_elem<OP>(a.c0, a.c1, v, acc);
+      ew_elem<OP>(c0, c1, v, acc);
 #pragma unroll
       for (int k = 0; k < 6; ++k)
         if (T::W & (1 << k)) a.p[k][i] = v[k];
@@ -215,7 +220,7 @@ __global__ __launch_bounds__(kBlock) void ew_kernel(EwArgs a) {
       double v[6];
 #pragma unroll
       for (int k = 0; k < 6; ++k) v[k] = (T::R & (1 << k)) ? a.p[k][i] : 0.0;
-      ew_elem<OP>(a.c0, a.c1, v, acc);
+      ew_elem<OP>(c0, c1, v, acc);
 #pragma unroll
       for (int k = 0; k < 6; ++k)
         if (T::W & (1 << k)) a.p[k][i] = v[k];
@@ -266,26 +271,93 @@ __global__ __launch_bounds__(kBlock) void finalize_kernel(const double* __restri
   }
 }
 
+// Sum of the `cnt` partials of one slot in the fixed order of the finalize
+// kernels (lane-strided, shuffle tree, then waves 0..3). Called by the whole
+// workgroup; every thread gets the result.
+__device__ double block_slot_sum(const double* __restrict__ part, int cnt, double* s_red) {
+  double t = 0.0;
+  for (int i = threadIdx.x; i < cnt; i += kBlock) t += part[i];
+  for (int off = 32; off > 0; off >>= 1) t += __shfl_down(t, off, 64);
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = t;
+  __syncthreads();
+  double r = s_red[0];
+  r = r + s_red[1];
+  r = r + s_red[2];
+  r = r + s_red[3];
+  __syncthreads();  // s_red may be reused by the caller
+  return r;
+}
+
 // As finalize_kernel, with a per-slot partial count (same fixed order).
 __global__ __launch_bounds__(kBlock) void finalize_counts_kernel(const double* __restrict__ part,
                                                                  int stride, SlotCounts c,
                                                                  double* __restrict__ out) {
   __shared__ double s_red[4];
   const int slot = blockIdx.x;
-  const int cnt = c.n[slot];
-  double t = 0.0;
-  for (int i = threadIdx.x; i < cnt; i += kBlock) t += part[(int64_t)slot * stride + i];
-  for (int off = 32; off > 0; off >>= 1) t += __shfl_down(t, off, 64);
-  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = t;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double r = s_red[0];
-    r = r + s_red[1];
-    r = r + s_red[2];
-    r = r + s_red[3];
-    out[slot] = r;
+  const double r = block_slot_sum(part + (int64_t)slot * stride, c.n[slot], s_red);
+  if (threadIdx.x == 0) out[slot] = r;
+}
+
+// ---------------------------------------------------------------------------
+// Device-resident CG / MrR scalars (one workgroup): the reductions of one
+// sync point, summed exactly like finalize_counts + the host's shard sum
+// (0.0 + total), then the scalar statements of the reference, then the
+// convergence test `sqrt(g)/||b|| < tol` as the equivalent `0 <= g < thr`
+// (thr precomputed on the host, see conv_threshold). State in st[ST_*].
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void scalar_kernel(ScalarArgs a) {
+  __shared__ double s_red[4];
+  double* st = a.st;
+  if (st[ST_STOP] != 0.0) return;
+  double v[5];
+#pragma unroll
+  for (int q = 0; q < 5; ++q)
+    v[q] = (a.need >> q) & 1
+               ? 0.0 + block_slot_sum(a.partials + (int64_t)q * a.stride, a.cnt[q], s_red)
+               : 0.0;
+  if (threadIdx.x != 0) return;
+  auto converged = [&](double g) {
+    return a.check && g >= 0.0 && g < a.thr;
+  };
+  switch (a.op) {
+    case SC_CG_ALPHA:  // alpha = gamma / sigma  (v3/gpu/cg.py:33)
+      st[ST_C0] = st[ST_GAMMA] / v[1];
+      st[ST_C1] = 0.0;
+      break;
+    case SC_CG_BETA: {  // beta = gnew / gamma; gamma = gnew  (v3/gpu/cg.py:36-38)
+      const double gnew = v[0];
+      st[ST_HIST + a.h] = gnew;
+      st[ST_C2] = gnew / st[ST_GAMMA];
+      st[ST_C3] = 0.0;
+      st[ST_GAMMA] = gnew;
+      if (converged(gnew)) {  // the test at the top of the next iteration
+        st[ST_STOP_AT] = (double)(a.it + 1);
+        st[ST_STOP] = 1.0;
+      }
+      break;
+    }
+    case SC_MRR_GAMMA: {  // <r,r>, mu, nu -> test; gamma = nu / mu  (v3/gpu/mrr.py:40-46)
+      st[ST_HIST + a.h] = v[0];
+      if (converged(v[0])) {
+        st[ST_STOP_AT] = (double)a.it;
+        st[ST_STOP] = 1.0;
+        break;
+      }
+      st[ST_GAMMA] = v[2] / v[1];
+      st[ST_C0] = st[ST_GAMMA];
+      st[ST_C1] = 0.0;
+      break;
+    }
+    case SC_MRR_ZETA: {  // zeta = <r,s>/<s,s>; eta = -zeta * gamma  (v3/gpu/mrr.py:47-49)
+      const double zeta = v[3] / v[4];
+      st[ST_C2] = (-zeta) * st[ST_GAMMA];
+      st[ST_C3] = zeta;
+      break;
+    }
   }
 }
+
+
 
 // ---------------------------------------------------------------------------
 // Multi-dot (test/composition primitive), up to 16 products per launch.
@@ -652,6 +724,11 @@ __global__ void sqrt_kernel(double* p) {
 
 void launch_sqrt(double* p, hipStream_t s) {
   sqrt_kernel<<<1, 64, 0, s>>>(p);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_scalar(const ScalarArgs& a, hipStream_t s) {
+  scalar_kernel<<<1, kBlock, 0, s>>>(a);
   KR_HIP_CHECK(hipGetLastError());
 }
 

@@ -566,6 +566,7 @@ struct RowSched {
 template <typename RP, int EPI, bool VEC, int GATHER = kGather, bool XCD = true, bool NT = false,
           int MW = 0>
 __global__ __launch_bounds__(kBlock) void spmv_kernel(SpmvArgs a) {
+  if (a.stop && *a.stop != 0.0) return;  // converged (device-resident scalars)
   using T = EpiTraits<EPI>;
   constexpr int NP = T::NP;
   constexpr int NV = T::NV;
@@ -772,6 +773,7 @@ __device__ __forceinline__ void pstage_products(const PStage& st, const double* 
 
 template <typename RP, int EPI, bool VEC>
 __global__ __launch_bounds__(kBlock) void spmv_kernel_prod(SpmvArgs a) {
+  if (a.stop && *a.stop != 0.0) return;  // converged (device-resident scalars)
   using T = EpiTraits<EPI>;
   constexpr int NP = T::NP;
   constexpr int NV = T::NV;
@@ -953,6 +955,7 @@ __device__ __forceinline__ void stage_load2(Stage& st, const double* __restrict_
 // exchange of row pointers).
 template <typename RP, int EPI, bool VEC, int MW, bool DB = true, bool NT = false>
 __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
+  if (a.stop && *a.stop != 0.0) return;  // converged (device-resident scalars)
   using T = EpiTraits<EPI>;
   constexpr int NP = T::NP;
   constexpr int NV = T::NV;
@@ -1213,6 +1216,7 @@ __device__ __forceinline__ void pstage_load2(PStageN<PS>& st, const double* __re
 // wave per SIMD (144 VGPRs at 4 slots).
 template <typename RP, int EPI, bool DB, bool NT, int PS>
 __global__ __launch_bounds__(kBlock) void spmv_kernel_prod2(SpmvArgs a) {
+  if (a.stop && *a.stop != 0.0) return;  // converged (device-resident scalars)
   using T = EpiTraits<EPI>;
   constexpr int NP = T::NP;
   constexpr int NV = T::NV;
@@ -1408,6 +1412,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_prod2(SpmvArgs a) {
 // ---------------------------------------------------------------------------
 template <int EPI, int MW, int CH>  // CH: offsets per load batch
 __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(SpmvArgs a) {
+  if (a.stop && *a.stop != 0.0) return;  // converged (device-resident scalars)
   using T = EpiTraits<EPI>;
   constexpr int NP = T::NP;
   constexpr int NV = T::NV;
@@ -1519,6 +1524,7 @@ bool use_dia(const SpmvArgs& a) {
 // ---------------------------------------------------------------------------
 template <int EPI>
 __global__ __launch_bounds__(kBlock) void gemv_kernel(SpmvArgs a) {
+  if (a.stop && *a.stop != 0.0) return;  // converged (device-resident scalars)
   using T = EpiTraits<EPI>;
   constexpr int NP = T::NP;
   constexpr int NV = T::NV;
