@@ -211,15 +211,23 @@ void System::build_masks(Shard& s) {
   KR_HIP_CHECK(hipMemcpyAsync(dM, M.data(), nm * sizeof(int32_t), hipMemcpyHostToDevice, s.stream));
   launch_masks(s.rowptr, s.rowptr64, s.n, s.col, s.pad, dM, nm, mw, mask, s.stream);
   if (dia_on) {
-    const int64_t ld = (s.n + 63) / 64 * 64;
+    // Row-block-major (default): one contiguous nm x 256 chunk per row block,
+    // so a workgroup reads one sequential stream. Offset-major (KR_DIA_LAYOUT=0,
+    // A/B): nm streams, one per offset, n rows apart.
+    const char* dl = getenv("KR_DIA_LAYOUT");
+    const bool blocked = !(dl && atoi(dl) == 0);
+    const int64_t nb = (s.n + kDiaRows - 1) / kDiaRows;
+    const int64_t ld = nb * kDiaRows;
     double* dia = nullptr;
     if (hipMalloc(&dia, sizeof(double) * (size_t)nm * ld) != hipSuccess)
       throw Failure(KR_ERR_NOMEM, "diagonal-offset values: allocation failed");
     s.owned.push_back(dia);
+    s.dia_bs = blocked ? (int64_t)nm * kDiaRows : kDiaRows;
+    s.dia_ks = blocked ? kDiaRows : ld;
     KR_HIP_CHECK(hipMemsetAsync(dia, 0, sizeof(double) * (size_t)nm * ld, s.stream));
-    launch_dia_fill(s.rowptr, s.rowptr64, s.n, s.col, s.val, s.pad, dM, nm, dia, ld, s.stream);
+    launch_dia_fill(s.rowptr, s.rowptr64, s.n, s.col, s.val, s.pad, dM, nm, dia, s.dia_bs,
+                    s.dia_ks, s.stream);
     s.dia = dia;
-    s.dia_ld = ld;
   }
   KR_HIP_CHECK(hipStreamSynchronize(s.stream));
   s.mask = mask;
@@ -620,8 +628,10 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
       a.nm = s.nm;
       a.mw = s.mw;
       if (s.dia) {
-        a.dia = s.dia + r_begin;
-        a.dia_ld = s.dia_ld;
+        KR_REQUIRE(r_begin % kDiaRows == 0, "DIA launch must start on a row block");
+        a.dia = s.dia + (r_begin / kDiaRows) * s.dia_bs;
+        a.dia_bs = s.dia_bs;
+        a.dia_ks = s.dia_ks;
       }
     }
     a.epi_late = epi_late;

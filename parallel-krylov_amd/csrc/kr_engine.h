@@ -76,7 +76,7 @@ struct Shard {
   int64_t slab_sub = 0;             // sub-slab width (row blocks)
   void* mask = nullptr;             // offset masks (SpmvArgs::mask), owned
   double* dia = nullptr;            // diagonal-offset values (SpmvArgs::dia), owned
-  int64_t dia_ld = 0;
+  int64_t dia_bs = 0, dia_ks = 0;  // SpmvArgs::dia_bs / dia_ks
   int32_t* moff = nullptr;
   int nm = 0, mw = 0;
   hipStream_t comm_stream = nullptr;  // halo exchange, overlapped with interior rows

@@ -99,10 +99,12 @@ struct SpmvArgs {
   int nm = 0;
   int mw = 0;
   // Diagonal-offset values (optional, with the masks): entry of row i at
-  // offset moff[b] is dia[b * dia_ld + i] (row-block launches offset dia by
-  // their first row). The SpMV then needs neither LDS staging nor rowptr.
+  // offset moff[b] is dia[(i / 256) * dia_bs + b * dia_ks + i % 256]
+  // (row-block launches offset dia by their first row block). Offset-major:
+  // dia_bs = 256, dia_ks = ld; row-block-major (default): dia_bs = 256 * nm,
+  // dia_ks = 256. The SpMV then needs neither LDS staging nor rowptr.
   const double* dia = nullptr;
-  int64_t dia_ld = 0;
+  int64_t dia_bs = 0, dia_ks = 0;
   // Fused-step operands (EPI_STEP_*), own rows: in/out u1, u2, x source/dest.
   double* u1 = nullptr;
   double* u2 = nullptr;
@@ -247,9 +249,10 @@ void launch_interior(const void* rowptr, int rowptr64, int64_t n, const int32_t*
 constexpr int kMaxMaskBits = 64;
 // Diagonal-offset values from a masked CSR block (values of row i at offset
 // M[b] land in dia[b * ld + i]; absent entries stay 0).
+constexpr int kDiaRows = 256;  // rows per DIA row block (== kBlock)
 void launch_dia_fill(const void* rowptr, int rowptr64, int64_t n, const int32_t* col,
                      const double* val, int64_t base, const int32_t* M, int nm, double* dia,
-                     int64_t ld, hipStream_t s);
+                     int64_t bs, int64_t ks, hipStream_t s);
 constexpr size_t kOffTableBytes = 256 * sizeof(unsigned long long);
 void launch_offsets(const void* rowptr, int rowptr64, int64_t n, const int32_t* col,
                     int64_t base, unsigned long long* table, int* flags, hipStream_t s);

@@ -595,17 +595,18 @@ __global__ void mask_kernel(const RP* rowptr, int64_t n, const int32_t* col, int
 template <typename RP>
 __global__ void dia_fill_kernel(const RP* rowptr, int64_t n, const int32_t* col,
                                 const double* val, int64_t base, const int32_t* M, int nm,
-                                double* dia, int64_t ld) {
+                                double* dia, int64_t bs, int64_t ks) {
   __shared__ int32_t sM[64];
   if ((int)threadIdx.x < nm) sM[threadIdx.x] = M[threadIdx.x];
   __syncthreads();
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
+    double* di = dia + (i / kDiaRows) * bs + (i % kDiaRows);
     for (int64_t j = (int64_t)rowptr[i]; j < (int64_t)rowptr[i + 1]; ++j) {
       const int64_t off = (int64_t)col[j] - (base + i);
       int b = 0;
       while (b < nm - 1 && sM[b] != off) ++b;
-      dia[(int64_t)b * ld + i] = val[j];
+      di[(int64_t)b * ks] = val[j];
     }
   }
 }
@@ -896,15 +897,15 @@ void launch_masks(const void* rowptr, int rowptr64, int64_t n, const int32_t* co
 
 void launch_dia_fill(const void* rowptr, int rowptr64, int64_t n, const int32_t* col,
                      const double* val, int64_t base, const int32_t* M, int nm, double* dia,
-                     int64_t ld, hipStream_t s) {
+                     int64_t bs, int64_t ks, hipStream_t s) {
   if (n <= 0) return;
   const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 65535);
   if (rowptr64)
     dia_fill_kernel<int64_t><<<g, 256, 0, s>>>(static_cast<const int64_t*>(rowptr), n, col, val,
-                                               base, M, nm, dia, ld);
+                                               base, M, nm, dia, bs, ks);
   else
     dia_fill_kernel<int32_t><<<g, 256, 0, s>>>(static_cast<const int32_t*>(rowptr), n, col, val,
-                                               base, M, nm, dia, ld);
+                                               base, M, nm, dia, bs, ks);
   KR_HIP_CHECK(hipGetLastError());
 }
 

@@ -1400,10 +1400,11 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_prod2(SpmvArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Diagonal-offset SpMV (default where offset masks exist: stencils, banded).
-// The values are stored offset-major (SpmvArgs::dia): for one offset, the
-// entries of consecutive rows are contiguous, and so are the x entries they
-// multiply (x[row + M[b]]). One lane per row, rows summed in stored order
+// Diagonal-offset SpMV (long rows with offset masks: banded, 27-point).
+// The values are stored per row block of 256 rows, offset by offset
+// (SpmvArgs::dia): for one offset, the entries of the block's consecutive
+// rows are contiguous, and so are the x entries they multiply (x[row + M[b]]);
+// a workgroup streams one contiguous nm x 2 KiB chunk. One lane per row, rows summed in stored order
 // (increasing offset = increasing column, as in CSR) from 0.0: bitwise scipy.
 // No LDS staging, no row pointers, no barrier: every load is a coalesced
 // 512-byte wave access, and latency is hidden by occupancy (8 waves/SIMD).
@@ -1442,6 +1443,7 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(SpmvArgs a) {
     const W m = active ? (W)mask[rr] : (W)0;
     const EpiIn pin = epi_load<EPI>(a, rr);
     const int64_t xrow = a.xoff + rr;
+    const double* dia_row = dia + (rr / kDiaRows) * a.dia_bs + (rr % kDiaRows);
     double sum1 = 0.0, sum2 = 0.0;
     for (int k0 = 0; k0 < nm; k0 += CH) {
       double v[CH], p1[CH], p2[CH], p3[VIRT ? CH : 1];
@@ -1450,7 +1452,7 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(SpmvArgs a) {
         const int k = min(k0 + u, nm - 1);
         const bool ok = k0 + u < nm && ((m >> k) & 1);
         const int64_t c = ok ? xrow + load_uniform(a.moff, k) : xrow;
-        v[u] = __builtin_nontemporal_load(dia + (int64_t)k * a.dia_ld + rr);
+        v[u] = __builtin_nontemporal_load(dia_row + (int64_t)k * a.dia_ks);
         p1[u] = x1[c];
         if constexpr (NV == 2 || VIRT) p2[u] = x2[c];
         if constexpr (VIRT) p3[u] = a.x3[c];

@@ -398,18 +398,22 @@ MASKED = {
 }
 
 
-@pytest.mark.parametrize("dia", ["2", "1", "0"])
+@pytest.mark.parametrize("dia", ["2", "2/offset-major", "1", "0"])
 @pytest.mark.parametrize("shards", [1, 3])
 @pytest.mark.parametrize("name", list(MASKED))
 def test_offset_mask_layout_spmv_bitwise(torch_dev, monkeypatch, name, shards, dia):
     """Matrices with <= 64 distinct column offsets (stencils, banded) use the
     offset-mask layout: the diagonal-offset SpMV (long rows by default,
-    KR_DIA=1; every masked shard with KR_DIA=2) or the short-row row walk
-    without a column stream (short rows; KR_DIA=0 for every shard).
+    KR_DIA=1; every masked shard with KR_DIA=2; values row-block-major, or
+    offset-major with KR_DIA_LAYOUT=0) or the short-row row walk without a
+    column stream (short rows; KR_DIA=0 for every shard).
     The SpMV stays bitwise scipy's, with KR_MASK=0 (plain columns) as the
     control."""
     from parallel_krylov_amd.system import KrylovSystem, balanced_partition
     builder, bits = MASKED[name]
+    if dia.endswith("offset-major"):
+        monkeypatch.setenv("KR_DIA_LAYOUT", "0")
+        dia = dia.split("/")[0]
     if dia == "0" and name.startswith("long_rows"):
         bits = 0
     monkeypatch.setenv("KR_DIA", dia)
