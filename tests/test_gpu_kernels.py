@@ -382,6 +382,12 @@ def _offset_matrix(n, offsets, per_row, seed, sort=True):
     return A
 
 
+def _nearly_symmetric(A):
+    A = A.tocsr(copy=True)
+    A[1000, 1001] = A[1000, 1001] * (1 + 2 ** -40)
+    return A
+
+
 MASKED = {
     # name: (builder, expected mask bits)
     "poisson2d_40": (lambda: golden_matrix(["poisson", 40, 2]), 8),
@@ -392,6 +398,8 @@ MASKED = {
     "offsets64": (lambda: _offset_matrix(6000, np.arange(-32, 32) * 3 + 1, 8, 3), 64),
     "offsets65": (lambda: _offset_matrix(6000, np.arange(-32, 33) * 3, 8, 4), 0),
     "unsorted": (lambda: _offset_matrix(3000, np.arange(-3, 4), 4, 5, sort=False), 0),
+    # structurally symmetric, one value off its mirror
+    "nearly_symmetric": (lambda: _nearly_symmetric(golden_matrix(["poisson", 14, 3])), 8),
     # long rows: masks (and the diagonal-offset values) only with KR_DIA on
     "long_rows": (lambda: golden_matrix(["banded", 3001, 13, 64, 0]), 32),
     "long_rows_63": (lambda: golden_matrix(["banded", 2000, 31, 256, 0]), 64),
