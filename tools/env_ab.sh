@@ -5,6 +5,9 @@
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 args=${@:---steps 10 --warmup 2 --no-cpu-baseline}
+# The first bench on a fresh box runs a few % slow (clocks / page-in): one
+# untimed run first, so the first setting is not penalised.
+timeout -k 10 600 python bench.py $args --no-profile > gpurun_out/envab_warm.log 2>&1 || exit $?
 for set in ${SETTINGS:-base}; do
   tag=${set//[^A-Za-z0-9]/_}
   if [ "$set" = base ]; then
