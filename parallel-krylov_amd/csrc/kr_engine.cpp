@@ -228,6 +228,14 @@ void System::build_masks(Shard& s) {
     launch_dia_fill(s.rowptr, s.rowptr64, s.n, s.col, s.val, s.pad, dM, nm, dia, s.dia_bs,
                     s.dia_ks, s.stream);
     s.dia = dia;
+    // x window in LDS for narrow bands (<= 2048 rows beyond the block:
+    // C3 W=64, C5 W=256); KR_DIA_XL=0 gathers from global memory (A/B).
+    const char* xl = getenv("KR_DIA_XL");
+    const int64_t band = (int64_t)M[nm - 1] - M[0];
+    if (!(xl && atoi(xl) == 0) && band <= 2048) {
+      s.dia_wlo = M[0];
+      s.dia_wlen = (int)(kBlock + band);
+    }
   }
   KR_HIP_CHECK(hipStreamSynchronize(s.stream));
   s.mask = mask;
@@ -632,6 +640,9 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
         a.dia = s.dia + (r_begin / kDiaRows) * s.dia_bs;
         a.dia_bs = s.dia_bs;
         a.dia_ks = s.dia_ks;
+        a.dia_wlo = s.dia_wlo;
+        a.dia_wlen = s.dia_wlen;
+        a.xlen = s.ld;
       }
     }
     a.epi_late = epi_late;

@@ -77,6 +77,7 @@ struct Shard {
   void* mask = nullptr;             // offset masks (SpmvArgs::mask), owned
   double* dia = nullptr;            // diagonal-offset values (SpmvArgs::dia), owned
   int64_t dia_bs = 0, dia_ks = 0;  // SpmvArgs::dia_bs / dia_ks
+  int dia_wlo = 0, dia_wlen = 0;   // SpmvArgs::dia_wlo / dia_wlen
   int32_t* moff = nullptr;
   int nm = 0, mw = 0;
   hipStream_t comm_stream = nullptr;  // halo exchange, overlapped with interior rows

@@ -105,6 +105,11 @@ struct SpmvArgs {
   // dia_ks = 256. The SpMV then needs neither LDS staging nor rowptr.
   const double* dia = nullptr;
   int64_t dia_bs = 0, dia_ks = 0;
+  // x window in LDS (narrow bands): rows row0 + dia_wlo .. + dia_wlen - 1 of
+  // each row block (dia_wlen = 0: gathers from global memory); xlen = the
+  // doubles of the halo-extended vectors (window loads clamp to it).
+  int dia_wlo = 0, dia_wlen = 0;
+  int64_t xlen = 0;
   // Fused-step operands (EPI_STEP_*), own rows: in/out u1, u2, x source/dest.
   double* u1 = nullptr;
   double* u2 = nullptr;

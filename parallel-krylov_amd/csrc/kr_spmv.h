@@ -1411,7 +1411,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_prod2(SpmvArgs a) {
 // Loads are unconditional (absent entries read a valid slot and x[row]) and
 // absent entries are skipped by a select, so the sum is exactly the CSR one.
 // ---------------------------------------------------------------------------
-template <int EPI, int MW, int CH>  // CH: offsets per load batch
+template <int EPI, int MW, int CH, bool XL>  // CH: offsets per load batch; XL: x window in LDS
 __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(SpmvArgs a) {
   if (a.stop && *a.stop != 0.0) return;  // converged (device-resident scalars)
   using T = EpiTraits<EPI>;
@@ -1436,13 +1436,31 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(SpmvArgs a) {
   sched.init(nrb, a.slab, a.slab_sub, true);
   sched.gap_at = a.rb_gap_at;
   sched.gap = a.rb_gap;
+  // XL (narrow bands): the x rows the row block reaches, [row0 + M[0],
+  // row0 + 255 + M[nm-1]], are staged in LDS with coalesced loads and the
+  // gathers read LDS: the vector-memory pipe then only carries the value
+  // stream (the kernel is bound by that pipe's issue, SQ_WAIT_INST_ANY).
+  extern __shared__ double s_xw[];
+  const int wlen = a.dia_wlen;
   for (int64_t j = sched.j0; j < sched.jcount; j += sched.jstep) {
-    const int64_t row = sched.rb(j) * kBlock + tid;
+    const int64_t rb0 = sched.rb(j) * kBlock;
+    const int64_t row = rb0 + tid;
     const bool active = row < a.n;
     const int64_t rr = active ? row : a.n - 1;  // loads stay in bounds
     const W m = active ? (W)mask[rr] : (W)0;
     const EpiIn pin = epi_load<EPI>(a, rr);
     const int64_t xrow = a.xoff + rr;
+    if constexpr (XL) {
+      const int64_t wbase = a.xoff + rb0 + a.dia_wlo;
+      __syncthreads();  // the previous row block is done with the window
+      for (int t = tid; t < wlen; t += kBlock) {
+        const int64_t xi = min(max(wbase + t, (int64_t)0), a.xlen - 1);
+        s_xw[t] = x1[xi];
+        if constexpr (NV == 2) s_xw[wlen + t] = x2[xi];
+      }
+      __syncthreads();
+    }
+    const int lx = (int)(rr - rb0) - a.dia_wlo;  // own row in the window
     const double* dia_row = dia + (rr / kDiaRows) * a.dia_bs + (rr % kDiaRows);
     double sum1 = 0.0, sum2 = 0.0;
     for (int k0 = 0; k0 < nm; k0 += CH) {
@@ -1451,11 +1469,17 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(SpmvArgs a) {
       for (int u = 0; u < CH; ++u) {
         const int k = min(k0 + u, nm - 1);
         const bool ok = k0 + u < nm && ((m >> k) & 1);
-        const int64_t c = ok ? xrow + load_uniform(a.moff, k) : xrow;
         v[u] = __builtin_nontemporal_load(dia_row + (int64_t)k * a.dia_ks);
-        p1[u] = x1[c];
-        if constexpr (NV == 2 || VIRT) p2[u] = x2[c];
-        if constexpr (VIRT) p3[u] = a.x3[c];
+        if constexpr (XL) {
+          const int lc = ok ? lx + load_uniform(a.moff, k) : lx;
+          p1[u] = s_xw[lc];
+          if constexpr (NV == 2) p2[u] = s_xw[wlen + lc];
+        } else {
+          const int64_t c = ok ? xrow + load_uniform(a.moff, k) : xrow;
+          p1[u] = x1[c];
+          if constexpr (NV == 2 || VIRT) p2[u] = x2[c];
+          if constexpr (VIRT) p3[u] = a.x3[c];
+        }
       }
 #pragma unroll
       for (int u = 0; u < CH; ++u) {
@@ -1479,24 +1503,23 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(SpmvArgs a) {
   block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
 }
 
-template <int E, int CH>
-void spmv_dia_launch_ch(const SpmvArgs& a, int nblocks, hipStream_t s) {
+template <int E, bool XL>
+void spmv_dia_launch_xl(const SpmvArgs& a, int nblocks, hipStream_t s) {
+  const size_t lds = XL ? sizeof(double) * a.dia_wlen * EpiTraits<E>::NV : 0;
   switch (a.mw) {
-    case 8: spmv_dia_kernel<E, 8, CH><<<nblocks, kBlock, 0, s>>>(a); return;
-    case 16: spmv_dia_kernel<E, 16, CH><<<nblocks, kBlock, 0, s>>>(a); return;
-    case 32: spmv_dia_kernel<E, 32, CH><<<nblocks, kBlock, 0, s>>>(a); return;
-    default: spmv_dia_kernel<E, 64, CH><<<nblocks, kBlock, 0, s>>>(a); return;
+    case 8: spmv_dia_kernel<E, 8, 8, XL><<<nblocks, kBlock, lds, s>>>(a); return;
+    case 16: spmv_dia_kernel<E, 16, 8, XL><<<nblocks, kBlock, lds, s>>>(a); return;
+    case 32: spmv_dia_kernel<E, 32, 8, XL><<<nblocks, kBlock, lds, s>>>(a); return;
+    default: spmv_dia_kernel<E, 64, 8, XL><<<nblocks, kBlock, lds, s>>>(a); return;
   }
 }
 
 template <int E>
 void spmv_dia_launch(const SpmvArgs& a, int nblocks, hipStream_t s) {
-  const char* env = getenv("KR_DIA_CH");  // A/B: 4 or 8 offsets per load batch
-  const int ch = env ? atoi(env) : 8;
-  if (ch == 4)
-    spmv_dia_launch_ch<E, 4>(a, nblocks, s);
-  else
-    spmv_dia_launch_ch<E, 8>(a, nblocks, s);
+  if constexpr (!is_virtual<E>()) {
+    if (a.dia_wlen > 0) return spmv_dia_launch_xl<E, true>(a, nblocks, s);
+  }
+  spmv_dia_launch_xl<E, false>(a, nblocks, s);
 }
 
 // Which kernel serves a masked shard: the diagonal-offset kernel, except for
