@@ -412,10 +412,12 @@ void System::finalize() {
     }
     // Long rows on the DIA kernel: forming r1 at each of ~60 gathered columns
     // per row costs more than one vector pass (C5: 8.97 ms vs 0.54 + 6.32 ms,
-    // +3.6 %), so they keep the step-0 vector kernel unless KR_FUSE_FIRST=1.
+    // +3.6 %), so they keep the step-0 vector kernel unless KR_FUSE_FIRST=1;
+    // with the x window in LDS, r1 is formed once per column instead.
     bool long_dia = false;
     for (auto& s : shards)
-      if (s.n > 0 && s.dia && (double)s.nnz >= kLongRow * (double)s.n) long_dia = true;
+      if (s.n > 0 && s.dia && s.dia_wlen == 0 && (double)s.nnz >= kLongRow * (double)s.n)
+        long_dia = true;
     fuse_first = fuse_steps && !long_rows && v2 &&
                  (ff ? atoi(ff) != 0 : !long_dia);
   }

@@ -1455,7 +1455,10 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(SpmvArgs a) {
       __syncthreads();  // the previous row block is done with the window
       for (int t = tid; t < wlen; t += kBlock) {
         const int64_t xi = min(max(wbase + t, (int64_t)0), a.xlen - 1);
-        s_xw[t] = x1[xi];
+        if constexpr (VIRT)  // r1 formed once per column, rounded as at every gather
+          s_xw[t] = virtual_r1(a.c0, a.c1, x1[xi], x2[xi], a.x3[xi]);
+        else
+          s_xw[t] = x1[xi];
         if constexpr (NV == 2) s_xw[wlen + t] = x2[xi];
       }
       __syncthreads();
@@ -1484,7 +1487,7 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(SpmvArgs a) {
 #pragma unroll
       for (int u = 0; u < CH; ++u) {
         const bool ok = k0 + u < nm && ((m >> min(k0 + u, nm - 1)) & 1);
-        if constexpr (VIRT) {
+        if constexpr (VIRT && !XL) {
           const double t = sum1 + v[u] * virtual_r1(a.c0, a.c1, p1[u], p2[u], p3[u]);
           sum1 = ok ? t : sum1;
         } else {
@@ -1505,7 +1508,7 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(SpmvArgs a) {
 
 template <int E, bool XL>
 void spmv_dia_launch_xl(const SpmvArgs& a, int nblocks, hipStream_t s) {
-  const size_t lds = XL ? sizeof(double) * a.dia_wlen * EpiTraits<E>::NV : 0;
+  const size_t lds = XL ? sizeof(double) * a.dia_wlen * EpiTraits<E>::NV : 0;  // virtual: NV 1
   switch (a.mw) {
     case 8: spmv_dia_kernel<E, 8, 8, XL><<<nblocks, kBlock, lds, s>>>(a); return;
     case 16: spmv_dia_kernel<E, 16, 8, XL><<<nblocks, kBlock, lds, s>>>(a); return;
@@ -1516,9 +1519,7 @@ void spmv_dia_launch_xl(const SpmvArgs& a, int nblocks, hipStream_t s) {
 
 template <int E>
 void spmv_dia_launch(const SpmvArgs& a, int nblocks, hipStream_t s) {
-  if constexpr (!is_virtual<E>()) {
-    if (a.dia_wlen > 0) return spmv_dia_launch_xl<E, true>(a, nblocks, s);
-  }
+  if (a.dia_wlen > 0) return spmv_dia_launch_xl<E, true>(a, nblocks, s);
   spmv_dia_launch_xl<E, false>(a, nblocks, s);
 }
 
