@@ -169,6 +169,46 @@ System::~System() {
   }
 }
 
+// x window of the DIA kernel (SpmvArgs::nseg ...): offsets closer than 256
+// rows share a segment; at most 4 segments and 4096 rows (32 KiB per vector),
+// else the kernel gathers from global memory. KR_DIA_XL=0 disables (A/B).
+void System::plan_window(Shard& s, const std::vector<int32_t>& M) {
+  const char* xl = getenv("KR_DIA_XL");
+  if (xl && atoi(xl) == 0) return;
+  std::vector<std::pair<int64_t, int64_t>> seg;  // [lo, hi] offsets
+  for (int32_t o : M) {
+    if (!seg.empty() && (int64_t)o - seg.back().second <= kBlock)
+      seg.back().second = o;
+    else
+      seg.push_back({o, o});
+  }
+  if ((int)seg.size() > SpmvArgs::kMaxSeg) return;
+  int base = 0;
+  int g = 0;
+  std::vector<int32_t> woff(M.size());
+  for (auto& [lo, hi] : seg) {
+    const int64_t lo_e = lo - (lo & 1);                      // even start
+    const int64_t len = (kBlock + hi - lo_e + 1) / 2 * 2;    // even length
+    if (base + len > 4096) return;
+    s.seg_lo[g] = (int)lo_e;
+    s.seg_len[g] = (int)len;
+    s.seg_base[g] = base;
+    for (size_t b = 0; b < M.size(); ++b)
+      if (M[b] >= lo && M[b] <= hi) woff[b] = (int32_t)(base - lo_e + M[b]);
+    base += (int)len;
+    ++g;
+  }
+  int32_t* dW = nullptr;
+  KR_HIP_CHECK(hipMalloc(&dW, 64 * sizeof(int32_t)));
+  s.owned.push_back(dW);
+  KR_HIP_CHECK(hipMemcpyAsync(dW, woff.data(), woff.size() * sizeof(int32_t),
+                              hipMemcpyHostToDevice, s.stream));
+  KR_HIP_CHECK(hipStreamSynchronize(s.stream));
+  s.woff = dW;
+  s.nseg = g;
+  s.dia_wlen = base;
+}
+
 void System::build_masks(Shard& s) {
   const char* env = getenv("KR_MASK");
   if (env && atoi(env) == 0) return;
@@ -228,14 +268,7 @@ void System::build_masks(Shard& s) {
     launch_dia_fill(s.rowptr, s.rowptr64, s.n, s.col, s.val, s.pad, dM, nm, dia, s.dia_bs,
                     s.dia_ks, s.stream);
     s.dia = dia;
-    // x window in LDS for narrow bands (<= 2048 rows beyond the block:
-    // C3 W=64, C5 W=256); KR_DIA_XL=0 gathers from global memory (A/B).
-    const char* xl = getenv("KR_DIA_XL");
-    const int64_t band = (int64_t)M[nm - 1] - M[0];
-    if (!(xl && atoi(xl) == 0) && band <= 2048) {
-      s.dia_wlo = M[0];
-      s.dia_wlen = (int)(kBlock + band);
-    }
+    plan_window(s, M);
   }
   KR_HIP_CHECK(hipStreamSynchronize(s.stream));
   s.mask = mask;
@@ -642,8 +675,14 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
         a.dia = s.dia + (r_begin / kDiaRows) * s.dia_bs;
         a.dia_bs = s.dia_bs;
         a.dia_ks = s.dia_ks;
-        a.dia_wlo = s.dia_wlo;
         a.dia_wlen = s.dia_wlen;
+        a.nseg = s.nseg;
+        for (int g = 0; g < s.nseg; ++g) {
+          a.seg_lo[g] = s.seg_lo[g];
+          a.seg_len[g] = s.seg_len[g];
+          a.seg_base[g] = s.seg_base[g];
+        }
+        a.woff = s.woff;
         a.xlen = s.ld;
       }
     }

@@ -77,7 +77,9 @@ struct Shard {
   void* mask = nullptr;             // offset masks (SpmvArgs::mask), owned
   double* dia = nullptr;            // diagonal-offset values (SpmvArgs::dia), owned
   int64_t dia_bs = 0, dia_ks = 0;  // SpmvArgs::dia_bs / dia_ks
-  int dia_wlo = 0, dia_wlen = 0;   // SpmvArgs::dia_wlo / dia_wlen
+  int dia_wlen = 0, nseg = 0;       // SpmvArgs x window (dia_wlen, nseg, seg_*, woff)
+  int seg_lo[4] = {}, seg_len[4] = {}, seg_base[4] = {};
+  int32_t* woff = nullptr;
   int32_t* moff = nullptr;
   int nm = 0, mw = 0;
   hipStream_t comm_stream = nullptr;  // halo exchange, overlapped with interior rows
@@ -149,6 +151,7 @@ struct System {
   void alloc_vectors(int count);
   // Halo exchange of up to two vectors (ids), all shards.
   void build_masks(Shard& s);
+  void plan_window(Shard& s, const std::vector<int32_t>& M);
   void halo(int id1, int id2 = -1, int id3 = -1);
   // The same exchange on the shards' comm streams, ordered after ev_in and
   // signalling ev_out (overlapped path).

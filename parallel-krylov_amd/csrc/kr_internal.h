@@ -105,10 +105,15 @@ struct SpmvArgs {
   // dia_ks = 256. The SpMV then needs neither LDS staging nor rowptr.
   const double* dia = nullptr;
   int64_t dia_bs = 0, dia_ks = 0;
-  // x window in LDS (narrow bands): rows row0 + dia_wlo .. + dia_wlen - 1 of
-  // each row block (dia_wlen = 0: gathers from global memory); xlen = the
+  // x window in LDS (spmv_dia_kernel): nseg segments, segment g = rows
+  // row0 + seg_lo[g] .. + seg_len[g] - 1 of the row block at s_xw[seg_base[g]]
+  // (starts and lengths even), dia_wlen doubles in all (0: gathers from global
+  // memory); offset k of row lr of the block is s_xw[lr + woff[k]]. xlen = the
   // doubles of the halo-extended vectors (window loads clamp to it).
-  int dia_wlo = 0, dia_wlen = 0;
+  static constexpr int kMaxSeg = 4;
+  int dia_wlen = 0, nseg = 0;
+  int seg_lo[kMaxSeg] = {}, seg_len[kMaxSeg] = {}, seg_base[kMaxSeg] = {};
+  const int32_t* woff = nullptr;
   int64_t xlen = 0;
   // Fused-step operands (EPI_STEP_*), own rows: in/out u1, u2, x source/dest.
   double* u1 = nullptr;

@@ -1411,6 +1411,16 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel_prod2(SpmvArgs a) {
 // Loads are unconditional (absent entries read a valid slot and x[row]) and
 // absent entries are skipped by a select, so the sum is exactly the CSR one.
 // ---------------------------------------------------------------------------
+// x[xi], x[xi + 1] (xi even): one 16-byte load inside [0, xlen), clamped
+// scalar loads at the vector's ends (those window entries are never used).
+__device__ __forceinline__ double2 window_pair(const double* __restrict__ x, int64_t xi,
+                                               int64_t xlen) {
+  if (xi >= 0 && xi + 1 < xlen) return *reinterpret_cast<const double2*>(x + xi);
+  const int64_t i0 = min(max(xi, (int64_t)0), xlen - 1);
+  const int64_t i1 = min(max(xi + 1, (int64_t)0), xlen - 1);
+  return make_double2(x[i0], x[i1]);
+}
+
 template <int EPI, int MW, int CH, bool XL>  // CH: offsets per load batch; XL: x window in LDS
 __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(SpmvArgs a) {
   if (a.stop && *a.stop != 0.0) return;  // converged (device-resident scalars)
@@ -1436,11 +1446,13 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(SpmvArgs a) {
   sched.init(nrb, a.slab, a.slab_sub, true);
   sched.gap_at = a.rb_gap_at;
   sched.gap = a.rb_gap;
-  // XL (narrow bands): the x rows the row block reaches, [row0 + M[0],
-  // row0 + 255 + M[nm-1]], are staged in LDS with coalesced loads and the
-  // gathers read LDS: the vector-memory pipe then only carries the value
-  // stream (the kernel is bound by that pipe's issue, SQ_WAIT_INST_ANY).
-  extern __shared__ double s_xw[];
+  // XL: the x rows the row block reaches are staged in LDS and the gathers
+  // read LDS, so the vector-memory pipe carries the value stream plus a few
+  // 16-byte window loads instead of one gather per entry. The window is up
+  // to 4 segments of consecutive rows (one per cluster of offsets: a narrow
+  // band is one segment, a 3-D stencil three: -n^2 / -n..n / +n^2); offset k
+  // of the row at lr in the block sits at s_xw[lr + woff[k]].
+  extern __shared__ __attribute__((aligned(16))) double s_xw[];
   const int wlen = a.dia_wlen;
   for (int64_t j = sched.j0; j < sched.jcount; j += sched.jstep) {
     const int64_t rb0 = sched.rb(j) * kBlock;
@@ -1451,19 +1463,30 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(SpmvArgs a) {
     const EpiIn pin = epi_load<EPI>(a, rr);
     const int64_t xrow = a.xoff + rr;
     if constexpr (XL) {
-      const int64_t wbase = a.xoff + rb0 + a.dia_wlo;
       __syncthreads();  // the previous row block is done with the window
-      for (int t = tid; t < wlen; t += kBlock) {
-        const int64_t xi = min(max(wbase + t, (int64_t)0), a.xlen - 1);
-        if constexpr (VIRT)  // r1 formed once per column, rounded as at every gather
-          s_xw[t] = virtual_r1(a.c0, a.c1, x1[xi], x2[xi], a.x3[xi]);
-        else
-          s_xw[t] = x1[xi];
-        if constexpr (NV == 2) s_xw[wlen + t] = x2[xi];
+      for (int g = 0; g < a.nseg; ++g) {
+        // segment starts are even (host), xoff and rb0 too: 16-byte loads
+        const int64_t src = a.xoff + rb0 + a.seg_lo[g];
+        const int half = a.seg_len[g] >> 1;
+        double2* d1 = reinterpret_cast<double2*>(s_xw + a.seg_base[g]);
+        double2* d2 = reinterpret_cast<double2*>(s_xw + wlen + a.seg_base[g]);
+        for (int t = tid; t < half; t += kBlock) {
+          const int64_t xi = src + 2 * t;
+          const double2 w1 = window_pair(x1, xi, a.xlen);
+          if constexpr (VIRT) {  // r1 formed once per column, rounded as at every gather
+            const double2 w2 = window_pair(x2, xi, a.xlen);
+            const double2 w3 = window_pair(a.x3, xi, a.xlen);
+            d1[t] = make_double2(virtual_r1(a.c0, a.c1, w1.x, w2.x, w3.x),
+                                 virtual_r1(a.c0, a.c1, w1.y, w2.y, w3.y));
+          } else {
+            d1[t] = w1;
+          }
+          if constexpr (NV == 2) d2[t] = window_pair(x2, xi, a.xlen);
+        }
       }
       __syncthreads();
     }
-    const int lx = (int)(rr - rb0) - a.dia_wlo;  // own row in the window
+    const int lx = (int)(rr - rb0);  // own row in the block
     const double* dia_row = dia + (rr / kDiaRows) * a.dia_bs + (rr % kDiaRows);
     double sum1 = 0.0, sum2 = 0.0;
     for (int k0 = 0; k0 < nm; k0 += CH) {
@@ -1474,7 +1497,7 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(SpmvArgs a) {
         const bool ok = k0 + u < nm && ((m >> k) & 1);
         v[u] = __builtin_nontemporal_load(dia_row + (int64_t)k * a.dia_ks);
         if constexpr (XL) {
-          const int lc = ok ? lx + load_uniform(a.moff, k) : lx;
+          const int lc = lx + load_uniform(a.woff, k);  // inside the window even if absent
           p1[u] = s_xw[lc];
           if constexpr (NV == 2) p2[u] = s_xw[wlen + lc];
         } else {
@@ -1530,6 +1553,7 @@ void spmv_dia_launch(const SpmvArgs& a, int nblocks, hipStream_t s) {
 template <int E>
 bool use_dia(const SpmvArgs& a) {
   if (!a.dia) return false;
+  if (a.dia_wlen > 0) return true;  // x window in LDS: every epilogue
   constexpr bool multi = EpiTraits<E>::NV == 2 || is_virtual<E>();
   if (!multi || a.long_rows) return true;
   const bool vec = ((reinterpret_cast<uintptr_t>(a.val) | reinterpret_cast<uintptr_t>(a.col)) &
