@@ -122,6 +122,18 @@ class Communicator:
             pass
 
 
+def gpu_ids_range():
+    """The rank's GPU range from GPU_IDS, ids[0]..ids[-1] inclusive, as the
+    reference reads it (v3/gpu/mpi/common.py:77-83), or None when unset."""
+    env = os.environ.get("GPU_IDS")
+    if not env:
+        return None
+    ids = [int(t) for t in env.split(",") if t.strip() != ""]
+    if not ids or ids[-1] < ids[0]:
+        raise ValueError(f"GPU_IDS={env!r}: expected 'first,...,last' with last >= first")
+    return list(range(ids[0], ids[-1] + 1))
+
+
 def local_device(rank: int) -> int:
     """Device of this rank: LOCAL_RANK, else the first of GPU_IDS
     (v3/gpu/mpi/common.py:77-83), else rank modulo the device count."""

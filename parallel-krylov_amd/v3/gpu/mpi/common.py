@@ -19,7 +19,7 @@ import time
 
 import numpy as np
 
-from ....system import Communicator, KrylovSystem, local_device
+from ....system import Communicator, KrylovSystem, balanced_partition, gpu_ids_range, local_device
 from ...common import _finish, _start
 from ..common import _host_vector, _is_tensor
 
@@ -109,27 +109,44 @@ def run(method, banner, comm, local_A, b, x=None, tol=1e-05, maxiter=None, k=Non
     if sum(counts) != N:
         raise ValueError(f"row blocks cover {sum(counts)} rows but b has {N}")
     row0 = sum(counts[: d.rank])
-    device = local_device(d.rank)
-    torch.cuda.set_device(device)
-    comm_h = d.communicator(device)
-    sysm = KrylovSystem(N, [row0, row0 + local_n], [device], comm=comm_h)
+    gpu_range = gpu_ids_range()
+    if gpu_range is not None and len(gpu_range) > 1:
+        # GPU_IDS=first,...,last: the rank splits its row block over that range
+        # (MultiGpu.alloc, v3/gpu/mpi/common.py:100-118). Supported for a single
+        # rank (in-process shards); with several ranks each rank owns one GPU.
+        if d.size > 1:
+            raise NotImplementedError(
+                "GPU_IDS with several GPUs per rank needs one rank: launch one rank per "
+                "GPU instead (torchrun --nproc-per-node G, LOCAL_RANK picks the GPU)")
+        devices = gpu_range
+        comm_h = None
+    else:
+        devices = [local_device(d.rank)]
+        comm_h = d.communicator(devices[0])
+    torch.cuda.set_device(devices[0])
+    rows = [row0 + r for r in balanced_partition(local_n, len(devices))]
+    sysm = KrylovSystem(N, rows, devices, comm=comm_h)
     try:
-        if sp.issparse(local_A):
-            sysm.adopt_csr(0, local_A)
-        else:  # dense row block: GEMV path (v3/gpu/mpi/common.py:124-125)
-            sysm.adopt_dense(0, local_A)
+        for s_, (r0, r1) in enumerate(zip(rows[:-1], rows[1:])):
+            blk = local_A[r0 - row0:r1 - row0]
+            if sp.issparse(local_A):
+                sysm.adopt_csr(s_, blk)
+            else:  # dense row block: GEMV path (v3/gpu/mpi/common.py:124-125)
+                sysm.adopt_dense(s_, blk)
         sysm.finalize()
-        b_parts = [torch.from_numpy(np.ascontiguousarray(bh[row0:row0 + local_n])).to(
-            torch.device("cuda", device))]
+        dev_of = [torch.device("cuda", dv) for dv in devices]
+        b_parts = [torch.from_numpy(np.ascontiguousarray(bh[r0:r1])).to(dv)
+                   for r0, r1, dv in zip(rows[:-1], rows[1:], dev_of)]
         x0_parts = None
         if isinstance(x, np.ndarray) or _is_tensor(x):
             xh = _host_vector(x)
-            x0_parts = [torch.from_numpy(np.ascontiguousarray(xh[row0:row0 + local_n])).to(
-                torch.device("cuda", device))]
+            x0_parts = [torch.from_numpy(np.ascontiguousarray(xh[r0:r1])).to(dv)
+                        for r0, r1, dv in zip(rows[:-1], rows[1:], dev_of)]
         if d.rank == 0:
             _start(banner, k)
         out = sysm.solve(method, b_parts, x0_parts, tol=tol, maxiter=maxiter, k=k or 0)
-        x_full = d.gather_x(out.x[0], counts)
+        x_local = torch.cat([xs.to(dev_of[0]) for xs in out.x])
+        x_full = d.gather_x(x_local, counts)
     finally:
         sysm.close()
     if d.rank == 0:

@@ -185,3 +185,23 @@ def test_row_partitioned_path_over_gloo(tmp_path, world):
     for me, o in enumerate(outs):
         for peer, g0, cnt in o["plan"][1]:
             assert (me, g0, cnt) in outs[peer]["plan"][0]
+
+
+@pytest.mark.parametrize("env,expect", [(None, None), ("3", [3]), ("2,5", [2, 3, 4, 5]),
+                                        ("0,1,2,3", [0, 1, 2, 3]), ("4,4", [4])])
+def test_gpu_ids_range(monkeypatch, env, expect):
+    """GPU_IDS as the reference reads it: ids[0]..ids[-1] inclusive
+    (v3/gpu/mpi/common.py:77-83)."""
+    from parallel_krylov_amd.system import gpu_ids_range
+    if env is None:
+        monkeypatch.delenv("GPU_IDS", raising=False)
+    else:
+        monkeypatch.setenv("GPU_IDS", env)
+    assert gpu_ids_range() == expect
+
+
+def test_gpu_ids_range_rejects_descending(monkeypatch):
+    from parallel_krylov_amd.system import gpu_ids_range
+    monkeypatch.setenv("GPU_IDS", "3,1")
+    with pytest.raises(ValueError):
+        gpu_ids_range()

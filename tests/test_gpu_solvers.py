@@ -324,6 +324,31 @@ def test_dense_mpi_single_rank(dist_single):
     assert np.linalg.norm(x.cpu().numpy() - x_ref) <= 1e-8 * np.linalg.norm(x_ref)
 
 
+@pytest.mark.parametrize("method", ["cg", "kskipmrr", "adaptivekskipmrr"])
+def test_mpi_gpu_ids_range_single_rank(dist_single, monkeypatch, method):
+    """GPU_IDS=first,...,last on a single rank: the row block is split over the
+    range in-process (MultiGpu.alloc, v3/gpu/mpi/common.py:100-118). Two
+    shards on GPU 0 stand in for a range of two GPUs; the result equals the
+    one-GPU run bit for bit (shard sums in shard order = rank order)."""
+    import importlib
+    mpi_common = importlib.import_module("parallel_krylov_amd.v3.gpu.mpi.common")
+    A = golden_matrix(["poisson", 12, 3])
+    b = np.random.default_rng(4).standard_normal(A.shape[0])
+    kw = dict(tol=1e-10, maxiter=300)
+    if "kskip" in method:
+        kw["k"] = 3
+    with contextlib.redirect_stdout(io.StringIO()):
+        x1, i1 = _solver(method, "gpu.mpi")(None, A, b, **kw)
+        monkeypatch.setattr(mpi_common, "gpu_ids_range", lambda: [0, 0])
+        x2, i2 = _solver(method, "gpu.mpi")(None, A, b, **kw)
+        monkeypatch.setenv("KRYLOV_AMD_SHARDS", "0,0")
+        x3, i3 = _solver(method, "gpu")(A, b, **kw)
+    np.testing.assert_array_equal(i2["nosl"], i1["nosl"])
+    np.testing.assert_array_equal(i2["residual"], i3["residual"])
+    np.testing.assert_array_equal(x2.cpu().numpy(), x3.cpu().numpy())
+    np.testing.assert_allclose(i2["residual"], i1["residual"], rtol=1e-9, atol=0)
+
+
 @pytest.mark.parametrize("shards", ["0", "0,0"])
 def test_dense_fused_steps_bitwise_equal_unfused(monkeypatch, shards):
     """The fused k-skip steps in the GEMV epilogue == separate vector steps."""
