@@ -257,6 +257,50 @@ def test_device_scalars_bitwise_equal_host(monkeypatch, method, matrix, tol, max
         np.testing.assert_array_equal(x1, x0)
 
 
+def _irregular_spd(n, per_row, seed):
+    """Random sparse SPD matrix without a stencil structure (> 64 distinct
+    column offsets: no offset masks, the column-stream kernels)."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(seed)
+    rows = np.repeat(np.arange(n), per_row)
+    cols = rng.integers(0, n, size=n * per_row)
+    B = sp.csr_matrix((-rng.uniform(0.1, 1.0, size=n * per_row), (rows, cols)), shape=(n, n))
+    S = (B + B.T).tocsr()
+    S.setdiag(0)
+    S.eliminate_zeros()
+    d = np.asarray(abs(S).sum(axis=1)).ravel() + 1.0
+    A = (S + sp.diags(d)).tocsr()
+    A.sort_indices()
+    return A
+
+
+@pytest.mark.parametrize("shards", ["0", "0,0,0"])
+@pytest.mark.parametrize("method,per_row,k", [("cg", 3, 0), ("mrr", 3, 0), ("kskipmrr", 3, 4),
+                                              ("kskipcg", 3, 2), ("kskipmrr", 9, 3),
+                                              ("adaptivekskipmrr", 3, 4)])
+def test_irregular_spd_matches_oracle(monkeypatch, shards, method, per_row, k):
+    """An unstructured sparse SPD system (random columns, no offset masks,
+    every shard reaching every other): same iteration count as the oracle and
+    residual histories within rounding (no fixture envelope here, so a loose
+    1e-8 on entries above 1e-6; parity unpinned beyond the oracle)."""
+    from oracle import v3cpu
+    A = _irregular_spd(3000, per_row, 7 + per_row)
+    b = np.random.default_rng(2).standard_normal(A.shape[0])
+    kw = dict(tol=1e-9, maxiter=600)
+    if k:
+        kw["k"] = k
+    monkeypatch.setenv("KRYLOV_AMD_SHARDS", shards)
+    with contextlib.redirect_stdout(io.StringIO()):
+        x, info = _solver(method)(A, b, **kw)
+        x_ref, info_ref = getattr(v3cpu, method)(A, b, **kw)
+    np.testing.assert_array_equal(info["nosl"], info_ref["nosl"])
+    r, rr = info["residual"], info_ref["residual"]
+    big = rr > 1e-6
+    assert np.max(np.abs(r[big] - rr[big]) / rr[big]) < 1e-8
+    xr = np.linalg.norm(x.cpu().numpy() - x_ref) / np.linalg.norm(x_ref)
+    assert xr < 1e-6, xr
+
+
 def _dense_spd(n, seed):
     """Dense SPD matrix with no zero entry (every entry is used by the GEMV)."""
     rng = np.random.default_rng(seed)
