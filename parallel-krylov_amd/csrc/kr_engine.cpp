@@ -804,7 +804,7 @@ void System::ew(EwOp op, double c0, double c1, std::array<int, 6> ids, int slot0
 bool System::device_scalars() const {
   const char* env = getenv("KR_DEVICE_SCALARS");  // 0: one host sync per reduction (A/B)
   if (env && atoi(env) == 0) return false;
-  return shards.size() == 1 && !comm;
+  return shards.size() == 1;  // one shard, alone or one RCCL rank of several
 }
 
 void System::scalar_state_init(double gamma) {
@@ -855,6 +855,20 @@ void System::scalar(ScalarOp op, int need, int64_t it, int h, double thr, int ch
   a.thr = thr;
   hipEvent_t t0 = nullptr;
   prof_begin(s, "scalar", t0);
+  if (comm) {
+    // every rank: its slot totals (finalize order), all-gathered on the
+    // compute stream (after this SpMV's halo, before the next one's: one
+    // RCCL order on every rank), then the same scalar step everywhere
+    const int nslots = 32 - __builtin_clz((unsigned)need);
+    SlotCounts cnt{};
+    for (int q = 0; q < nslots; ++q) cnt.n[q] = s.slot_n[q];
+    launch_finalize_counts(s.partials, s.pstride, cnt, nslots, s.slots, s.stream);
+    KR_NCCL_CHECK(ncclAllGather(s.slots, s.gather, (size_t)nslots, ncclFloat64, comm->nccl,
+                                s.stream));
+    a.gathered = s.gather;
+    a.nranks = comm->nranks;
+    a.gstride = nslots;
+  }
   launch_scalar(a, s.stream);
   prof_end(s, "scalar", t0, 8.0 * s.pstride * __builtin_popcount(need));
 }

@@ -194,6 +194,10 @@ struct ScalarArgs {
   int h = 0;                       // ST_HIST index
   int check = 1;                   // 0: no convergence test
   double thr = 0;                  // converged <=> 0 <= g < thr
+  // RCCL ranks: the per-rank slot totals all-gathered as [nranks][gstride];
+  // each reduction is then 0.0 + rank 0 + rank 1 + ... (the host's order).
+  const double* gathered = nullptr;
+  int nranks = 0, gstride = 0;
 };
 void launch_scalar(const ScalarArgs& a, hipStream_t s);
 

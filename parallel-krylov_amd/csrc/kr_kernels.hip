@@ -310,11 +310,21 @@ __global__ __launch_bounds__(kBlock) void scalar_kernel(ScalarArgs a) {
   double* st = a.st;
   if (st[ST_STOP] != 0.0) return;
   double v[5];
+  if (a.gathered) {  // ranks' totals in rank order, as System::reduce sums them
 #pragma unroll
-  for (int q = 0; q < 5; ++q)
-    v[q] = (a.need >> q) & 1
-               ? 0.0 + block_slot_sum(a.partials + (int64_t)q * a.stride, a.cnt[q], s_red)
-               : 0.0;
+    for (int q = 0; q < 5; ++q) {
+      double t = 0.0;
+      if ((a.need >> q) & 1)
+        for (int r = 0; r < a.nranks; ++r) t = t + a.gathered[(int64_t)r * a.gstride + q];
+      v[q] = t;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 5; ++q)
+      v[q] = (a.need >> q) & 1
+                 ? 0.0 + block_slot_sum(a.partials + (int64_t)q * a.stride, a.cnt[q], s_red)
+                 : 0.0;
+  }
   if (threadIdx.x != 0) return;
   auto converged = [&](double g) {
     return a.check && g >= 0.0 && g < a.thr;

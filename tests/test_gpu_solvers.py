@@ -257,6 +257,25 @@ def test_device_scalars_bitwise_equal_host(monkeypatch, method, matrix, tol, max
         np.testing.assert_array_equal(x1, x0)
 
 
+@pytest.mark.parametrize("method,tol,maxiter", [("cg", 1e-10, 400), ("mrr", 1e-10, 400),
+                                                ("cg", 1e-8, 13)])
+def test_device_scalars_mpi_single_rank_bitwise(dist_single, monkeypatch, method, tol, maxiter):
+    """The MPI family's device-resident scalars (slot totals all-gathered over
+    RCCL, summed in rank order by the scalar kernel) equal its host-scalar
+    path bit for bit on one rank."""
+    A = golden_matrix(["poisson", 16, 2])
+    b = np.random.default_rng(12).standard_normal(A.shape[0])
+    out = []
+    for env in ("0", "1"):
+        monkeypatch.setenv("KR_DEVICE_SCALARS", env)
+        with contextlib.redirect_stdout(io.StringIO()):
+            x, info = _solver(method, "gpu.mpi")(None, A, b, tol=tol, maxiter=maxiter)
+        out.append((x.cpu().numpy(), info))
+    np.testing.assert_array_equal(out[0][1]["nosl"], out[1][1]["nosl"])
+    np.testing.assert_array_equal(out[0][1]["residual"], out[1][1]["residual"])
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+
+
 def _irregular_spd(n, per_row, seed):
     """Random sparse SPD matrix without a stencil structure (> 64 distinct
     column offsets: no offset masks, the column-stream kernels)."""
