@@ -366,6 +366,10 @@ class KrylovSystem:
         torch = _torch()
         xs = [torch.empty(self.row_begin[s + 1] - self.row_begin[s], dtype=torch.float64,
                           device=self.device(s)) for s in range(self.nshards)]
+        # the engine writes x on its own streams: torch's pending work on the
+        # recycled memory must be done first
+        for dv in sorted(set(self.devices)):
+            torch.cuda.synchronize(dv)
         res = _lib.SolveResult()
         call("kr_solve_end", self.handle, ptr_array([x.data_ptr() for x in xs]),
              ctypes.byref(res))
