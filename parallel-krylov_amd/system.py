@@ -137,8 +137,8 @@ def gpu_ids_range():
 def local_device(rank: int) -> int:
     """Device of this rank: LOCAL_RANK, else the first of GPU_IDS
     (v3/gpu/mpi/common.py:77-83), else rank modulo the device count."""
-    if "LOCAL_RANK" in os.environ:
-        return int(os.environ["LOCAL_RANK"])
+    if "LOCAL_RANK" in os.environ:  # more ranks than GPUs share them round-robin
+        return int(os.environ["LOCAL_RANK"]) % max(_lib.device_count(), 1)
     if os.environ.get("GPU_IDS"):
         return int(os.environ["GPU_IDS"].split(",")[0])
     n = _lib.device_count()
