@@ -1546,9 +1546,11 @@ void spmv_dia_launch(const SpmvArgs& a, int nblocks, hipStream_t s) {
   spmv_dia_launch_xl<E, false>(a, nblocks, s);
 }
 
-// Which kernel serves a masked shard: the diagonal-offset kernel, except for
-// short-row multi-vector SpMVs (dual, fused first step), where the row walk
-// v2 measured faster (512^3 dual 2.77 vs 2.82 ms, first step 3.93 vs 4.20 ms).
+// Which kernel serves a shard that has diagonal-offset values (long rows by
+// default, every masked shard with KR_DIA=2): the DIA kernel for every
+// epilogue when the x window fits in LDS; without a window, the row walk v2
+// for short-row multi-vector SpMVs (dual, fused first step), where it measured
+// faster (512^3 dual 2.77 vs 2.82 ms, first step 3.93 vs 4.20 ms).
 // KR_DIA_ALL=1 routes those to the diagonal-offset kernel too (A/B).
 template <int E>
 bool use_dia(const SpmvArgs& a) {
