@@ -53,6 +53,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="C4", choices=sorted(CONFIGS))
     p.add_argument("--n-side", type=int, default=None, help="override the Poisson grid side")
+    p.add_argument("--nz", type=int, default=None,
+                   help="Poisson planes (a side^2 x nz box, e.g. --nz 64: one rank's slab of "
+                        "512^3 at 8 GPUs, for per-rank studies on one GPU)")
     p.add_argument("--k", type=int, default=None)
     p.add_argument("--method", default=None)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -139,7 +142,11 @@ def main():
     if world > 1:
         dist.init_process_group("gloo")
         comm = Communicator.from_torch(None, local)
-    n = mat[1] ** mat[2] if mat[0] == "poisson" else mat[1]
+    if args.nz is not None and mat[0] == "poisson":
+        n = mat[1] ** (mat[2] - 1) * args.nz
+        mat.append(args.nz)
+    else:
+        n = mat[1] ** mat[2] if mat[0] == "poisson" else mat[1]
     part = balanced_partition(n, world)
     sysm = KrylovSystem(n, [part[rank], part[rank + 1]], [local], comm)
     if mat[0] == "poisson":

@@ -186,7 +186,9 @@ int kr_system_adopt_dense(kr_system* sys, int shard, const double* a_dev, int64_
 
 /* Generate this shard's rows of a synthetic SPD matrix on the device.
  * dim = 2 or 3: 5-/7-point Poisson on an n_side^dim grid, lexicographic
- * order, diagonal 2*dim, off-diagonals -1 (scipy kronsum of tridiag(-1,2,-1)).
+ * order, diagonal 2*dim, off-diagonals -1 (scipy kronsum of tridiag(-1,2,-1));
+ * when n_global = n_side^(dim-1) * nz with nz != n_side, the same operator on
+ * a box of nz planes (e.g. the slab one rank of a multi-GPU cube owns).
  * Banded: h distinct offsets in [1,W] drawn from `seed`, a(i,i+-o) = -u,
  * diagonal = sum|off| + 1 (see DESIGN.md for the exact definition). */
 int kr_system_gen_poisson(kr_system* sys, int dim, int64_t n_side);

@@ -559,16 +559,19 @@ int kr_system_gen_poisson(kr_system* sys, int dim, int64_t n_side) {
   return guarded([&] {
     KR_REQUIRE(dim == 2 || dim == 3, "dim must be 2 or 3");
     KR_REQUIRE(n_side >= 1, "n_side must be positive");
-    int64_t N = 1;
-    for (int d = 0; d < dim; ++d) N *= n_side;
-    KR_REQUIRE(N == sys->n_global, "n_side^dim must equal n_global");
+    // n_global = n_side^(dim-1) * nz: the cube (nz = n_side), or a box of nz
+    // planes (outermost dimension), e.g. one rank's slab of a larger cube
+    int64_t plane = 1;
+    for (int d = 0; d < dim - 1; ++d) plane *= n_side;
+    KR_REQUIRE(sys->n_global % plane == 0, "n_global must be n_side^(dim-1) * nz");
+    const int64_t nz = sys->n_global / plane;
     generate(
         sys, 0, 2 * dim + 1,
         [&](Shard& s, void* rp, int rp64) {
-          launch_poisson_count(dim, n_side, s.row0, s.n, rp, rp64, s.stream);
+          launch_poisson_count(dim, n_side, nz, s.row0, s.n, rp, rp64, s.stream);
         },
         [&](Shard& s, void* rp, int rp64, int32_t* col, double* val) {
-          launch_poisson_fill(dim, n_side, s.row0, s.n, rp, rp64, col, val, s.stream);
+          launch_poisson_fill(dim, n_side, nz, s.row0, s.n, rp, rp64, col, val, s.stream);
         });
   });
 }

@@ -231,9 +231,10 @@ void launch_multidot(const MultiDotArgs& a, hipStream_t s);
 // Synthetic generators (rows [row0, row0+n) of the global matrix).
 // ---------------------------------------------------------------------------
 // Poisson: counts (rowptr[i+1] = nnz of row i) then fill after the scan.
-void launch_poisson_count(int dim, int64_t side, int64_t row0, int64_t n, void* rowptr,
-                          int rowptr64, hipStream_t s);
-void launch_poisson_fill(int dim, int64_t side, int64_t row0, int64_t n,
+// Poisson on side^(dim-1) x nz points (nz = side: the cube).
+void launch_poisson_count(int dim, int64_t side, int64_t nz, int64_t row0, int64_t n,
+                          void* rowptr, int rowptr64, hipStream_t s);
+void launch_poisson_fill(int dim, int64_t side, int64_t nz, int64_t row0, int64_t n,
                          const void* rowptr, int rowptr64, int32_t* col, double* val,
                          hipStream_t s);
 struct BandSpec {

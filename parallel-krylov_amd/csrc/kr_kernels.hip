@@ -407,32 +407,36 @@ __global__ __launch_bounds__(kBlock) void multidot_kernel(MultiDotArgs a, int ba
 // Generators.
 // ---------------------------------------------------------------------------
 template <typename RP>
-__global__ void poisson_count_kernel(int dim, int64_t side, int64_t row0, int64_t n,
+// Grid side^(dim-1) x nz (nz = side: the cube of the reference's Poisson).
+__global__ void poisson_count_kernel(int dim, int64_t side, int64_t nz, int64_t row0, int64_t n,
                                      RP* rowptr) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   int64_t g = row0 + i;
   int cnt = 1;
   for (int d = 0; d < dim; ++d) {
-    const int64_t c = g % side;
-    g /= side;
-    cnt += (c > 0) + (c < side - 1);
+    const int64_t sz = d == dim - 1 ? nz : side;
+    const int64_t c = g % sz;
+    g /= sz;
+    cnt += (c > 0) + (c < sz - 1);
   }
   rowptr[i + 1] = (RP)cnt;
 }
 
 template <typename RP>
-__global__ void poisson_fill_kernel(int dim, int64_t side, int64_t row0, int64_t n,
+__global__ void poisson_fill_kernel(int dim, int64_t side, int64_t nz, int64_t row0, int64_t n,
                                     const RP* rowptr, int32_t* col, double* val) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t g = row0 + i;
   int64_t coord[3] = {0, 0, 0};
   int64_t stride[3] = {1, side, side * side};
+  int64_t size[3] = {side, side, side};
+  size[dim - 1] = nz;
   int64_t t = g;
   for (int d = 0; d < dim; ++d) {
-    coord[d] = t % side;
-    t /= side;
+    coord[d] = t % size[d];
+    t /= size[d];
   }
   int64_t j = (int64_t)rowptr[i];
   // Sorted column order: outermost lower neighbours first.
@@ -446,7 +450,7 @@ __global__ void poisson_fill_kernel(int dim, int64_t side, int64_t row0, int64_t
   val[j] = 2.0 * dim;
   ++j;
   for (int d = 0; d < dim; ++d)
-    if (coord[d] < side - 1) {
+    if (coord[d] < size[d] - 1) {
       col[j] = (int32_t)(g + stride[d]);
       val[j] = -1.0;
       ++j;
@@ -759,28 +763,28 @@ void launch_multidot(const MultiDotArgs& a, hipStream_t s) {
   }
 }
 
-void launch_poisson_count(int dim, int64_t side, int64_t row0, int64_t n, void* rowptr,
-                          int rowptr64, hipStream_t s) {
+void launch_poisson_count(int dim, int64_t side, int64_t nz, int64_t row0, int64_t n,
+                          void* rowptr, int rowptr64, hipStream_t s) {
   if (n <= 0) return;
   if (rowptr64)
     poisson_count_kernel<int64_t><<<blocks_for(n, 256), 256, 0, s>>>(
-        dim, side, row0, n, static_cast<int64_t*>(rowptr));
+        dim, side, nz, row0, n, static_cast<int64_t*>(rowptr));
   else
     poisson_count_kernel<int32_t><<<blocks_for(n, 256), 256, 0, s>>>(
-        dim, side, row0, n, static_cast<int32_t*>(rowptr));
+        dim, side, nz, row0, n, static_cast<int32_t*>(rowptr));
   KR_HIP_CHECK(hipGetLastError());
 }
 
-void launch_poisson_fill(int dim, int64_t side, int64_t row0, int64_t n,
+void launch_poisson_fill(int dim, int64_t side, int64_t nz, int64_t row0, int64_t n,
                          const void* rowptr, int rowptr64, int32_t* col, double* val,
                          hipStream_t s) {
   if (n <= 0) return;
   if (rowptr64)
     poisson_fill_kernel<int64_t><<<blocks_for(n, 256), 256, 0, s>>>(
-        dim, side, row0, n, static_cast<const int64_t*>(rowptr), col, val);
+        dim, side, nz, row0, n, static_cast<const int64_t*>(rowptr), col, val);
   else
     poisson_fill_kernel<int32_t><<<blocks_for(n, 256), 256, 0, s>>>(
-        dim, side, row0, n, static_cast<const int32_t*>(rowptr), col, val);
+        dim, side, nz, row0, n, static_cast<const int32_t*>(rowptr), col, val);
   KR_HIP_CHECK(hipGetLastError());
 }
 

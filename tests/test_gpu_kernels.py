@@ -309,6 +309,30 @@ def test_device_generators_and_sharded_spmv_bitwise(torch_dev, spec, shards):
     sysm.close()
 
 
+@pytest.mark.parametrize("side,nz,shards", [(13, 5, 1), (16, 7, 2), (9, 20, 3)])
+def test_device_poisson_box_matches_scipy(torch_dev, side, nz, shards):
+    """The Poisson generator on a side x side x nz box (n_global = side^2 nz):
+    the 7-point operator of scipy's kronsum with a z-size of nz, bitwise."""
+    import scipy.sparse as sp
+    from parallel_krylov_amd.system import KrylovSystem, balanced_partition
+
+    def t(m):
+        return sp.diags([-np.ones(m - 1), 2 * np.ones(m), -np.ones(m - 1)], [-1, 0, 1])
+    A = sp.kronsum(sp.kronsum(t(side), t(side)), t(nz)).tocsr()
+    A.sort_indices()
+    n = A.shape[0]
+    sysm = KrylovSystem(n, balanced_partition(n, shards), [0] * shards)
+    sysm.gen_poisson(side, 3)
+    sysm.finalize()
+    for q in range(shards):
+        r0, r1 = sysm.shard_rows(q)
+        assert sysm.shard_info(q)["nnz"] == A[r0:r1].nnz
+    x = np.random.default_rng(4).standard_normal(n)
+    y = sysm.gather(sysm.spmv(sysm.split(x))).cpu().numpy()
+    np.testing.assert_array_equal(y, A.dot(x))
+    sysm.close()
+
+
 def test_adopted_csr_sharded_spmv_bitwise(torch_dev):
     from parallel_krylov_amd.system import KrylovSystem, balanced_partition
     A = _irregular(3000, 2)
