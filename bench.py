@@ -106,6 +106,31 @@ def cpu_baseline(n_side: int, k: int, method: str):
                         f"{cores} affinity cores; wall {wall:.1f} s"))
 
 
+def stored_format_delta(nnz, n, lay, long_row=12.0):
+    """CSR algorithmic bytes (12 nnz + rowptr + vectors) minus
+    the bytes the shard's stored format streams for the same SpMV: offset
+    masks replace the 4-byte columns by mw/8 bytes per row, a value
+    dictionary the 8-byte values by 1-byte codes; long masked rows use the
+    diagonal-offset values (8 bytes per offset and row, no rowptr)."""
+    mw = lay["mask_bits"]
+    if mw and lay["dict_values"] == 0 and nnz >= long_row * n:  # DIA (KR_DIA=1)
+        n_pad = -(-n // 256) * 256
+        return 12.0 * nnz + 4.0 * (n + 1) - (8.0 * lay["n_offsets"] * n_pad + mw / 8 * n)
+    d = 0.0
+    if mw:
+        d += 4.0 * nnz - mw / 8 * n
+    if lay["dict_values"]:
+        d += 7.0 * nnz
+    return d
+
+
+def format_name(lay):
+    parts = [f"offset masks ({lay['mask_bits']}-bit)" if lay["mask_bits"] else "CSR columns"]
+    parts.append(f"{lay['dict_values']}-entry value dictionary (1-byte codes)"
+                 if lay["dict_values"] else "8-byte values")
+    return ", ".join(parts)
+
+
 def pmc_traffic(kernel):
     """Beyond-L2 bytes per launch of `kernel` from the committed rocprofv3 PMC
     summary (profiles/latest.json, made by tools/profile.sh +
@@ -183,26 +208,36 @@ def main():
         elapsed = float(t.item())
     stats = sysm.kernel_stats()
     out = sysm.finish(args.method)
+    lay = sysm.shard_layout(0)
+    delta = stored_format_delta(info["nnz"], info["n_local"], lay)
     iterations = args.steps * per_step
     value = iterations / elapsed
 
     roofline = None
     kernels = {}
     if stats:
+        stored = {}
         for s in stats:
             if s["launches"]:
                 avg = s["total_ms"] / s["launches"]
+                csr = s["bytes_per_launch"]
+                st = csr - (delta if s["name"].startswith("spmv") else 0.0)
+                stored[s["name"]] = (st, csr)
                 kernels[s["name"]] = dict(launches=s["launches"], avg_ms=round(avg, 5),
-                                          gbs=round(s["bytes_per_launch"] / avg / 1e6, 1),
+                                          gbs=round(st / avg / 1e6, 1),
+                                          csr_gbs=round(csr / avg / 1e6, 1),
                                           total_ms=round(s["total_ms"], 3))
         spmv = {n_: v for n_, v in kernels.items() if n_.startswith("spmv")}
         dom = max(spmv or kernels, key=lambda n_: kernels[n_]["total_ms"])
         d = kernels[dom]
         ach = d["gbs"]
+        # achieved = the minimum bytes of the format the kernel streams (offset
+        # masks instead of columns, 1-byte dictionary codes instead of values:
+        # DESIGN.md 9); the CSR figure of SURVEY.md 8(d) is csr_equiv_gbs
         roofline = dict(bound="hbm", kernel=dom, achieved=ach, peak=HBM_PEAK_GBS, unit="GB/s",
                         frac=round(ach / HBM_PEAK_GBS, 4), traffic=pmc_traffic(dom),
-                        bytes_per_launch=next(s["bytes_per_launch"] for s in stats
-                                              if s["name"] == dom),
+                        bytes_per_launch=stored[dom][0], csr_bytes_per_launch=stored[dom][1],
+                        csr_equiv_gbs=d["csr_gbs"], format=format_name(lay),
                         avg_ms=d["avg_ms"])
     base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "C4":

@@ -212,6 +212,13 @@ int kr_system_shard_info(kr_system* sys, int shard, int64_t* n_local, int64_t* h
  * SpMV that overlaps the exchange). Pointers may be NULL. */
 int kr_system_shard_layout(kr_system* sys, int shard, int* mask_bits, int* n_offsets,
                            int64_t* interior_lo, int64_t* interior_hi);
+/* Value storage the row-walk SpMV uses for shard s (after finalize):
+ * dict_values = 0 for the 8-byte value stream, else the number (<= 256) of
+ * distinct value bit patterns, each entry then streamed as a 1-byte code into
+ * that table (lossless; short-row CSR blocks such as stencils; KR_VDICT=0
+ * disables). Replaces nothing in the reference: the cuSPARSE csrmv behind
+ * v3/gpu/common.py:119 always streams 8-byte values. */
+int kr_system_shard_values(kr_system* sys, int shard, int* dict_values);
 
 /* Halo exchange plan (pure host arithmetic, no device; test hook and the
  * planner kr_system_finalize uses). part[0..nshards] is the global row

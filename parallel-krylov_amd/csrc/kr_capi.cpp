@@ -627,6 +627,14 @@ int kr_system_shard_layout(kr_system* sys, int shard, int* mask_bits, int* n_off
   });
 }
 
+int kr_system_shard_values(kr_system* sys, int shard, int* dict_values) {
+  return guarded([&] {
+    KR_REQUIRE(sys && shard >= 0 && shard < (int)sys->shards.size(), "bad shard");
+    KR_REQUIRE(sys->finalized, "system not finalized");
+    if (dict_values) *dict_values = sys->shards[shard].vcode ? sys->shards[shard].ntab : 0;
+  });
+}
+
 int kr_system_csr(kr_system* sys, int shard, const void** rowptr, int* rowptr64,
                   const int32_t** col, const double** val, int64_t* pad) {
   return guarded([&] {

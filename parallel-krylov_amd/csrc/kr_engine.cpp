@@ -284,6 +284,60 @@ void System::build_masks(Shard& s) {
   s.mw = mw;
 }
 
+void System::build_vdict(Shard& s) {
+  const char* env = getenv("KR_VDICT");
+  if (env && atoi(env) == 0) return;
+  // Only the row walk v2 reads codes: short rows, no DIA values, 16-byte
+  // aligned val/col, >= 4 entries (the v2 host conditions in spmv_dispatch_epi).
+  if (s.n == 0 || s.dense || s.dia || s.nnz < 8) return;
+  if ((double)s.nnz >= kLongRow * (double)s.n) return;
+  if ((reinterpret_cast<uintptr_t>(s.val) | reinterpret_cast<uintptr_t>(s.col)) & 15) return;
+  unsigned long long* gtab = nullptr;
+  const size_t tb = kVdGlobal * sizeof(unsigned long long);
+  KR_HIP_CHECK(hipMalloc(&gtab, tb + 16));
+  int* flags = reinterpret_cast<int*>(reinterpret_cast<char*>(gtab) + tb);
+  launch_vdict_collect(s.val + s.nz0, s.nnz, gtab, flags, s.stream);
+  std::vector<unsigned long long> h(kVdGlobal);
+  int hflags[2] = {0, 0};
+  KR_HIP_CHECK(hipMemcpyAsync(h.data(), gtab, tb, hipMemcpyDeviceToHost, s.stream));
+  KR_HIP_CHECK(hipMemcpyAsync(hflags, flags, sizeof(hflags), hipMemcpyDeviceToHost, s.stream));
+  KR_HIP_CHECK(hipStreamSynchronize(s.stream));
+  std::vector<unsigned long long> keys;
+  for (auto k : h)
+    if (k != ~0ull) keys.push_back(k);
+  if (hflags[0] || keys.empty() || (int)keys.size() > kVdMax) {
+    KR_HIP_CHECK(hipFree(gtab));
+    return;
+  }
+  std::sort(keys.begin(), keys.end());
+  const int nk = (int)keys.size();
+  // vcode (indexed like val) must be 8-byte aligned with readable bytes on
+  // both sides: windows start at (first entry) & ~7 and load 8 codes per lane
+  const int64_t pre = 8 + (s.nz0 & 7);
+  uint8_t* code = nullptr;
+  if (hipMalloc(&code, (size_t)(pre + s.nnz + 16)) != hipSuccess) {
+    KR_HIP_CHECK(hipFree(gtab));
+    (void)hipGetLastError();
+    return;  // no room for the codes: keep the 8-byte values
+  }
+  s.owned.push_back(code);
+  double* tab = nullptr;
+  KR_HIP_CHECK(hipMalloc(&tab, kVdMax * sizeof(double)));
+  s.owned.push_back(tab);
+  // the sorted keys (bit patterns) double as the value table
+  KR_HIP_CHECK(hipMemcpyAsync(gtab, keys.data(), nk * sizeof(unsigned long long),
+                              hipMemcpyHostToDevice, s.stream));
+  KR_HIP_CHECK(hipMemcpyAsync(tab, keys.data(), nk * sizeof(unsigned long long),
+                              hipMemcpyHostToDevice, s.stream));
+  KR_HIP_CHECK(hipMemsetAsync(code, 0, (size_t)(pre + s.nnz + 16), s.stream));
+  launch_vdict_encode(s.val + s.nz0, s.nnz, gtab, nk, code + pre, s.stream);
+  KR_HIP_CHECK(hipStreamSynchronize(s.stream));
+  KR_HIP_CHECK(hipFree(gtab));
+  s.vcode = code + pre - s.nz0;  // indexed like val
+  s.vtab = tab;
+  s.ntab = nk;
+}
+
 void System::finalize() {
   KR_REQUIRE(!finalized, "system already finalized");
   const int P = nglobal_shards();
@@ -319,11 +373,13 @@ void System::finalize() {
       KR_HIP_CHECK(hipMemcpy(&e[0], s.rowptr, 8, hipMemcpyDeviceToHost));
       KR_HIP_CHECK(hipMemcpy(&e[1], (const int64_t*)s.rowptr + s.n, 8, hipMemcpyDeviceToHost));
       s.nnz = e[1] - e[0];
+      s.nz0 = e[0];
     } else {
       int32_t e[2];
       KR_HIP_CHECK(hipMemcpy(&e[0], s.rowptr, 4, hipMemcpyDeviceToHost));
       KR_HIP_CHECK(hipMemcpy(&e[1], (const int32_t*)s.rowptr + s.n, 4, hipMemcpyDeviceToHost));
       s.nnz = (int64_t)e[1] - e[0];
+      s.nz0 = e[0];
     }
   }
   // 2. everybody's needed range [lo, hi]
@@ -405,6 +461,9 @@ void System::finalize() {
       // column offsets (stencils, banded): the SpMV then reads a 1-8 byte mask
       // per row instead of a 4-byte column per entry. KR_MASK=0 disables.
       build_masks(s);
+      // 6b. value dictionary for short-row blocks with <= 256 distinct values
+      // (stencils): 1-byte codes instead of 8-byte values. KR_VDICT=0 disables.
+      build_vdict(s);
     }
     // 7. reduction buffers
     s.grid = default_grid(s.n);
@@ -692,6 +751,11 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
         a.woff = s.woff;
         a.xlen = s.ld;
       }
+    }
+    if (s.vcode) {
+      a.vcode = s.vcode;
+      a.vtab = s.vtab;
+      a.ntab = s.ntab;
     }
     a.epi_late = epi_late;
     a.stop = dev_stop;

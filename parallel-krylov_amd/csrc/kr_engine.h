@@ -82,6 +82,10 @@ struct Shard {
   int32_t* woff = nullptr;
   int32_t* moff = nullptr;
   int nm = 0, mw = 0;
+  uint8_t* vcode = nullptr;         // value dictionary codes (SpmvArgs::vcode), val's index space
+  double* vtab = nullptr;           // its table (<= kVdMax doubles), owned
+  int ntab = 0;
+  int64_t nz0 = 0;                  // rowptr[0]: index of the block's first stored entry
   hipStream_t comm_stream = nullptr;  // halo exchange, overlapped with interior rows
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   int grid = 1;                 // workgroups of the vector kernels
@@ -151,6 +155,7 @@ struct System {
   void alloc_vectors(int count);
   // Halo exchange of up to two vectors (ids), all shards.
   void build_masks(Shard& s);
+  void build_vdict(Shard& s);
   void plan_window(Shard& s, const std::vector<int32_t>& M);
   void halo(int id1, int id2 = -1, int id3 = -1);
   // The same exchange on the shards' comm streams, ordered after ev_in and

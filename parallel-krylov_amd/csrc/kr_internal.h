@@ -133,6 +133,12 @@ struct SpmvArgs {
   // Row-block gap (boundary launch of a split SpMV): the launch covers the
   // row blocks [0, rb_gap_at) and [rb_gap_at + rb_gap, ceil(n / kBlock)).
   int64_t rb_gap_at = 0, rb_gap = 0;
+  // Value dictionary (optional, row walk v2): entry j's value is
+  // vtab[vcode[j]] (same index space as val; val stays valid for the other
+  // kernels). vtab holds <= kVdMax doubles.
+  const uint8_t* vcode = nullptr;
+  const double* vtab = nullptr;
+  int ntab = 0;
 };
 // Mean row length from which the product-then-sum SpMV is used.
 constexpr double kLongRow = 12.0;
@@ -274,6 +280,17 @@ void launch_offsets(const void* rowptr, int rowptr64, int64_t n, const int32_t* 
 // mask[i] (mw-bit integers) = the bits of row i's offsets in M[0..nm).
 void launch_masks(const void* rowptr, int rowptr64, int64_t n, const int32_t* col, int64_t base,
                   const int32_t* M, int nm, int mw, void* mask, hipStream_t s);
+// Value dictionary (SpmvArgs::vcode). launch_vdict_collect: the distinct bit
+// patterns of val[0, nnz) into gtab[kVdGlobal] (~0 = free slot); flags[0] != 0
+// if there are more than kVdMax of them (or the ~0 pattern occurs), flags[1] =
+// their count. launch_vdict_encode: code[j] = position of val[j]'s pattern in
+// the ascending keys[0, nk).
+constexpr int kVdMax = 256;
+constexpr int kVdGlobal = 1024;
+void launch_vdict_collect(const double* val, int64_t nnz, unsigned long long* gtab, int* flags,
+                          hipStream_t s);
+void launch_vdict_encode(const double* val, int64_t nnz, const unsigned long long* keys, int nk,
+                         uint8_t* code, hipStream_t s);
 // col[j] += delta for all stored entries of the block.
 void launch_col_shift(const void* rowptr, int rowptr64, int64_t n, int32_t* col,
                       int64_t delta, hipStream_t s);

@@ -935,4 +935,133 @@ void launch_col_shift(const void* rowptr, int rowptr64, int64_t n, int32_t* col,
   KR_HIP_CHECK(hipGetLastError());
 }
 
+// ---------------------------------------------------------------------------
+// Value dictionary (SpmvArgs::vcode): a block whose stored values take at most
+// kVdMax distinct bit patterns is re-stored as one 8-bit code per entry plus a
+// table, so the row walk streams 1 byte per entry instead of 8 (lossless:
+// codes map back to the exact bit patterns; CSR-VI, Kourtis et al. 2008).
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int kVdSet = 512;  // per-workgroup LDS set slots (open addressing)
+constexpr unsigned long long kVdEmpty = ~0ull;  // a NaN payload: never stored (flag 2)
+
+__device__ __forceinline__ unsigned vd_hash(unsigned long long k, int slots) {
+  return (unsigned)((k * 0x9E3779B97F4A7C15ull) >> 40) & (unsigned)(slots - 1);
+}
+
+// Distinct bit patterns of val[0, nnz) into gtab[kVdGlobal] (kVdEmpty = free).
+// flags[0]: 1 = more than kVdMax patterns, 2 = the sentinel pattern occurs.
+// Each workgroup first collects into an LDS set and stops as soon as it holds
+// more than kVdMax patterns (matrices with many values exit in one chunk).
+__global__ __launch_bounds__(256) void vdict_collect_kernel(const unsigned long long* val,
+                                                            int64_t nnz,
+                                                            unsigned long long* gtab,
+                                                            int* flags) {
+  __shared__ unsigned long long set[kVdSet];
+  __shared__ int cnt, over;
+  for (int i = threadIdx.x; i < kVdSet; i += blockDim.x) set[i] = kVdEmpty;
+  if (threadIdx.x == 0) {
+    cnt = 0;
+    over = 0;
+  }
+  __syncthreads();
+  constexpr int kPer = 64;  // entries per lane per chunk
+  const int64_t chunk = (int64_t)blockDim.x * kPer;
+  for (int64_t c0 = (int64_t)blockIdx.x * chunk; c0 < nnz; c0 += (int64_t)gridDim.x * chunk) {
+    for (int u = 0; u < kPer; ++u) {
+      const int64_t j = c0 + (int64_t)u * blockDim.x + threadIdx.x;
+      if (j >= nnz) break;
+      if (*(volatile int*)&over) break;
+      const unsigned long long key = val[j];
+      if (key == kVdEmpty) {
+        atomicOr(&over, 2);
+        break;
+      }
+      unsigned h = vd_hash(key, kVdSet);
+      for (int probe = 0; probe < kVdSet; ++probe) {
+        const unsigned long long v = *(volatile unsigned long long*)&set[h];
+        if (v == key) break;
+        if (v == kVdEmpty) {
+          const unsigned long long old = atomicCAS(&set[h], kVdEmpty, key);
+          if (old == kVdEmpty) {
+            if (atomicAdd(&cnt, 1) >= kVdMax) atomicOr(&over, 1);
+            break;
+          }
+          if (old == key) break;
+        }
+        h = (h + 1) & (kVdSet - 1);
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && __atomic_load_n(flags, __ATOMIC_RELAXED)) atomicOr(&over, 1);
+    __syncthreads();
+    if (over) break;
+  }
+  if (over) {
+    if (threadIdx.x == 0) atomicOr(flags, over);
+    return;
+  }
+  // merge this workgroup's patterns into the global set
+  for (int i = threadIdx.x; i < kVdSet; i += blockDim.x) {
+    const unsigned long long key = set[i];
+    if (key == kVdEmpty) continue;
+    unsigned h = vd_hash(key, kVdGlobal);
+    int probe = 0;
+    for (; probe < kVdGlobal; ++probe) {
+      const unsigned long long old = atomicCAS(&gtab[h], kVdEmpty, key);
+      if (old == kVdEmpty) {
+        if (atomicAdd(&flags[1], 1) >= kVdMax) atomicOr(flags, 1);
+        break;
+      }
+      if (old == key) break;
+      h = (h + 1) & (kVdGlobal - 1);
+    }
+    if (probe == kVdGlobal) atomicOr(flags, 1);
+  }
+}
+
+// code[j] = index of val[j]'s bit pattern in the ascending table keys[0, nk).
+__global__ __launch_bounds__(256) void vdict_encode_kernel(const unsigned long long* val,
+                                                           int64_t nnz,
+                                                           const unsigned long long* keys,
+                                                           int nk, uint8_t* code) {
+  __shared__ unsigned long long sk[kVdMax];
+  for (int i = threadIdx.x; i < nk; i += blockDim.x) sk[i] = keys[i];
+  __syncthreads();
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nnz;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    const unsigned long long key = val[j];
+    int lo = 0, hi = nk - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (sk[mid] < key)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    code[j] = (uint8_t)lo;
+  }
+}
+}  // namespace
+
+void launch_vdict_collect(const double* val, int64_t nnz, unsigned long long* gtab, int* flags,
+                          hipStream_t s) {
+  KR_HIP_CHECK(hipMemsetAsync(gtab, 0xff, kVdGlobal * sizeof(unsigned long long), s));
+  KR_HIP_CHECK(hipMemsetAsync(flags, 0, 2 * sizeof(int), s));
+  if (nnz <= 0) return;
+  const unsigned g = std::min<unsigned>(blocks_for(nnz, 256 * 64), 2048);
+  vdict_collect_kernel<<<g, 256, 0, s>>>(reinterpret_cast<const unsigned long long*>(val), nnz,
+                                         gtab, flags);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_vdict_encode(const double* val, int64_t nnz, const unsigned long long* keys, int nk,
+                         uint8_t* code, hipStream_t s) {
+  if (nnz <= 0) return;
+  const unsigned g = std::min<unsigned>(blocks_for(nnz, 256), 8192);
+  vdict_encode_kernel<<<g, 256, 0, s>>>(reinterpret_cast<const unsigned long long*>(val), nnz,
+                                        keys, nk, code);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace kr

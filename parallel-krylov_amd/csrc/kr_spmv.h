@@ -917,13 +917,13 @@ __device__ __forceinline__ T load_uniform(const T* p, int64_t i) {
 // compiler wait for exactly the loads it needs (vmcnt counts in issue order;
 // with a skippable load it has to assume the fewer-loads path and waits for
 // everything). Needs >= 4 entries in the matrix (host check).
-template <bool COLS, bool NT = false>
+template <bool COLS, bool NT = false, bool VALS = true>
 __device__ __forceinline__ void stage_load2(Stage& st, const double* __restrict__ val,
                                             const int32_t* __restrict__ col, int64_t ws,
                                             int64_t be, int tid) {
   const int64_t vlast = max((be - 1) & ~(int64_t)1, (int64_t)0);
 #pragma unroll
-  for (int q = 0; q < kVSlots; ++q) {
+  for (int q = 0; q < (VALS ? kVSlots : 0); ++q) {
     const int64_t g0 = min(ws + (int64_t)(tid + q * kBlock) * 2, vlast);
     if constexpr (NT)
       st.v[q] = __builtin_nontemporal_load(reinterpret_cast<const dbl2v*>(val + g0));
@@ -953,7 +953,11 @@ __device__ __forceinline__ void stage_load2(Stage& st, const double* __restrict_
 // the scalar cache (load_uniform), the LDS windows are double-buffered (one
 // barrier per window), and each lane loads its own row range (no LDS
 // exchange of row pointers).
-template <typename RP, int EPI, bool VEC, int MW, bool DB = true, bool NT = false>
+// VI: values through the dictionary (SpmvArgs::vcode): each lane loads the 8
+// one-byte codes of its 8 window entries (one 8-byte load: windows start on a
+// multiple of 8) and decodes them from the LDS table when it commits the window.
+template <typename RP, int EPI, bool VEC, int MW, bool DB = true, bool NT = false,
+          bool VI = false>
 __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
   if (a.stop && *a.stop != 0.0) return;  // converged (device-resident scalars)
   using T = EpiTraits<EPI>;
@@ -982,6 +986,12 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
   if constexpr (!COLS) {
     if (tid < a.nm) s_M[tid] = a.moff[tid];  // seen after the first barrier
   }
+  static_assert(!VI || (VEC && kWindow == 8 * kBlock), "dictionary staging: 8 codes per lane");
+  __shared__ double s_tab[VI ? kVdMax : 1];
+  if constexpr (VI) {
+    if (tid < a.ntab) s_tab[tid] = a.vtab[tid];
+    __syncthreads();  // the first commit decodes through s_tab
+  }
 
   double acc[NP > 0 ? NP : 1];
 #pragma unroll
@@ -999,7 +1009,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
     return;
   }
   auto block_rows = [&](int64_t b) { return (int)min((int64_t)kBlock, a.n - b * kBlock); };
-  auto wstart = [](int64_t e) { return VEC ? (e & ~(int64_t)3) : e; };
+  auto wstart = [](int64_t e) { return VI ? (e & ~(int64_t)7) : VEC ? (e & ~(int64_t)3) : e; };
 
   // current row block: boundaries (uniform), this lane's row range and mask
   int64_t r0 = sched.rb(j) * kBlock;
@@ -1021,12 +1031,24 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
     ben = (int64_t)load_uniform(rowptr, rbn * kBlock + block_rows(rbn));
   }
   Stage st;
+  uint64_t cw = 0;  // VI: this lane's 8 codes of the staged window
   int64_t ws = wstart(bs);
   auto stage = [&](int64_t w, int64_t lo, int64_t hi) {
-    if constexpr (VEC)
+    if constexpr (VI) {
+      // same load count on every path (see stage_load2): clamp to the last
+      // 8-code chunk holding an entry of the block (codes are padded by 8)
+      const int64_t c0 = min(w + (int64_t)tid * 8, max((hi - 1) & ~(int64_t)7, (int64_t)0));
+      const uint64_t* cp = reinterpret_cast<const uint64_t*>(a.vcode + c0);
+      if constexpr (NT)
+        cw = __builtin_nontemporal_load(cp);
+      else
+        cw = *cp;
+      if constexpr (COLS) stage_load2<COLS, NT, false>(st, val, col, w, hi, tid);
+    } else if constexpr (VEC) {
       stage_load2<COLS, NT>(st, val, col, w, hi, tid);
-    else
+    } else {
       stage_load<false, false, COLS>(st, val, col, w, lo, hi, tid);
+    }
   };
   stage(ws, bs, be);
   int buf = 0;
@@ -1043,7 +1065,19 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
   for (;;) {
     double* sv = s_val[DB ? buf : 0];
     int32_t* sc = s_col[COLS && DB ? buf : 0];
-    stage_commit<COLS>(st, sv, sc, tid);
+    if constexpr (VI) {
+      dbl2v* dst = reinterpret_cast<dbl2v*>(sv) + tid * 4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        dst[q] = dbl2v{s_tab[(cw >> (16 * q)) & 0xff], s_tab[(cw >> (16 * q + 8)) & 0xff]};
+      if constexpr (COLS) {
+#pragma unroll
+        for (int q = 0; q < kCSlots; ++q)
+          reinterpret_cast<int4v*>(sc)[tid + q * kBlock] = st.c[q];
+      }
+    } else {
+      stage_commit<COLS>(st, sv, sc, tid);
+    }
     __syncthreads();
     const bool active = tid < nr;
     if (first_window) {
@@ -1161,6 +1195,17 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
 
 template <typename RP, int E, bool VEC, bool DB = true, bool NT = false>
 void spmv2_launch(const SpmvArgs& a, dim3 grid, dim3 block, hipStream_t s) {
+  if constexpr (VEC) {
+    if (a.vcode) {
+      switch (a.mask ? a.mw : 0) {
+        case 8: spmv_kernel2<RP, E, VEC, 8, DB, NT, true><<<grid, block, 0, s>>>(a); return;
+        case 16: spmv_kernel2<RP, E, VEC, 16, DB, NT, true><<<grid, block, 0, s>>>(a); return;
+        case 32: spmv_kernel2<RP, E, VEC, 32, DB, NT, true><<<grid, block, 0, s>>>(a); return;
+        case 64: spmv_kernel2<RP, E, VEC, 64, DB, NT, true><<<grid, block, 0, s>>>(a); return;
+        default: spmv_kernel2<RP, E, VEC, 0, DB, NT, true><<<grid, block, 0, s>>>(a); return;
+      }
+    }
+  }
   switch (a.mask ? a.mw : 0) {
     case 8: spmv_kernel2<RP, E, VEC, 8, DB, NT><<<grid, block, 0, s>>>(a); return;
     case 16: spmv_kernel2<RP, E, VEC, 16, DB, NT><<<grid, block, 0, s>>>(a); return;

@@ -263,13 +263,16 @@ class KrylovSystem:
 
     def shard_layout(self, s: int) -> dict:
         """SpMV storage of shard s: mask_bits (0 = CSR columns), n_offsets,
-        interior row range [interior_lo, interior_hi)."""
+        interior row range [interior_lo, interior_hi), dict_values (0 = 8-byte
+        values, else the size of the value dictionary)."""
         mb, no = ctypes.c_int(), ctypes.c_int()
         lo, hi = ctypes.c_int64(), ctypes.c_int64()
         call("kr_system_shard_layout", self.handle, s, ctypes.byref(mb), ctypes.byref(no),
              ctypes.byref(lo), ctypes.byref(hi))
+        dv = ctypes.c_int()
+        call("kr_system_shard_values", self.handle, s, ctypes.byref(dv))
         return dict(mask_bits=mb.value, n_offsets=no.value, interior_lo=lo.value,
-                    interior_hi=hi.value)
+                    interior_hi=hi.value, dict_values=dv.value)
 
     def csr_pointers(self, s: int) -> dict:
         """Raw device CSR of shard s (local columns after finalize)."""

@@ -34,3 +34,21 @@ def test_pmc_traffic_from_committed_profile():
     t = bench.pmc_traffic("spmv2_gram_mrr")
     assert t == prof["spmv2_gram_mrr"]["traffic_bytes"] and t > 1e9
     assert bench.pmc_traffic("no_such_kernel") is None
+
+
+def test_stored_format_bytes():
+    """The roofline's bytes are the stored format's: masks replace the 4-byte
+    columns, a value dictionary the 8-byte values; long masked rows are DIA."""
+    import bench
+    n, nnz = 1000, 7000
+    csr = dict(mask_bits=0, n_offsets=0, dict_values=0)
+    assert bench.stored_format_delta(nnz, n, csr) == 0.0
+    masked = dict(mask_bits=8, n_offsets=7, dict_values=0)
+    assert bench.stored_format_delta(nnz, n, masked) == 4.0 * nnz - 1.0 * n
+    both = dict(mask_bits=8, n_offsets=7, dict_values=2)
+    assert bench.stored_format_delta(nnz, n, both) == 11.0 * nnz - 1.0 * n
+    dia = dict(mask_bits=32, n_offsets=27, dict_values=0)
+    nnz_long = 27 * n
+    assert bench.stored_format_delta(nnz_long, n, dia) == (
+        12.0 * nnz_long + 4.0 * (n + 1) - (8.0 * 27 * 1024 + 4.0 * n))
+    assert "dictionary" in bench.format_name(both) and "masks" in bench.format_name(both)

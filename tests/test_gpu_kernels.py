@@ -466,3 +466,71 @@ def test_offset_mask_layout_spmv_bitwise(torch_dev, monkeypatch, name, shards, d
         else:
             np.testing.assert_array_equal(y, A.dot(x))
         sysm.close()
+
+
+def _few_values_matrix(n, nvals, seed, per_row=9, zeros=False):
+    """Random-pattern CSR (plain columns: too many offsets for masks) whose
+    values are drawn from `nvals` distinct doubles; with zeros=True the set
+    holds +0.0 and -0.0 as two explicit stored values."""
+    rng = np.random.default_rng(seed)
+    table = rng.standard_normal(nvals)
+    if zeros:
+        table[0], table[1] = 0.0, -0.0
+    rows, cols = [], []
+    for i in range(n):
+        c = np.unique(rng.integers(0, n, size=per_row))
+        rows.append(np.full(c.size, i))
+        cols.append(c)
+    r, c = np.concatenate(rows), np.concatenate(cols)
+    v = table[rng.integers(0, nvals, size=r.size)]
+    v[:nvals] = table  # every value occurs
+    A = sp.csr_matrix((v, (r, c)), shape=(n, n))  # (i, j) unique: no summing
+    A.sort_indices()
+    return A
+
+
+VALUE_SETS = {
+    # name: (builder, expected dictionary size)
+    "poisson3d_21": (lambda: golden_matrix(["poisson", 21, 3]), 2),
+    "poisson2d_40": (lambda: golden_matrix(["poisson", 40, 2]), 2),
+    "cols_3": (lambda: _few_values_matrix(5000, 3, 1), 3),
+    "cols_signed_zeros": (lambda: _few_values_matrix(5000, 5, 2, zeros=True), 5),
+    "cols_256": (lambda: _few_values_matrix(6000, 256, 3), 256),
+    "cols_257": (lambda: _few_values_matrix(6000, 257, 4), 0),
+    "banded7_random": (lambda: golden_matrix(["banded", 4099, 3, 64, 0]), 0),
+    "irregular": (lambda: _irregular(3000, 2), 0),
+    "long_rows": (lambda: golden_matrix(["banded", 3001, 13, 64, 0]), 0),
+}
+
+
+@pytest.mark.parametrize("shards", [1, 3])
+@pytest.mark.parametrize("name", list(VALUE_SETS))
+def test_value_dictionary_spmv_bitwise(torch_dev, monkeypatch, name, shards):
+    """Short-row blocks whose stored values take <= 256 distinct bit patterns
+    stream 1-byte codes into a value table (row walk v2, with offset masks or
+    plain columns); the SpMV stays bitwise scipy's, signed zeros included,
+    with KR_VDICT=0 (8-byte values) as the control. 257 values, random
+    values and long rows keep the 8-byte stream."""
+    from parallel_krylov_amd.system import KrylovSystem, balanced_partition
+    builder, nd = VALUE_SETS[name]
+    A = builder()
+    n = A.shape[0]
+    x = np.random.default_rng(11).standard_normal(n)
+    x[::7] *= -1e-300  # tiny products: a -0.0 table entry must stay -0.0
+    ref = A.dot(x)
+    for vd in ("1", "0"):
+        monkeypatch.setenv("KR_VDICT", vd)
+        sysm = KrylovSystem(n, balanced_partition(n, shards), [0] * shards)
+        sysm.set_matrix(A)
+        sysm.finalize()
+        got = [sysm.shard_layout(s)["dict_values"] for s in range(shards)]
+        if vd == "0" or nd == 0:
+            assert got == [0] * shards
+        elif shards == 1:
+            assert got == [nd]
+        else:
+            assert all(0 < g <= nd for g in got)
+        y = sysm.gather(sysm.spmv(sysm.split(x))).cpu().numpy()
+        np.testing.assert_array_equal(y, ref)
+        assert np.array_equal(np.signbit(y), np.signbit(ref))
+        sysm.close()

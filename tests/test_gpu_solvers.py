@@ -216,7 +216,8 @@ def test_fused_steps_bitwise_equal_unfused(monkeypatch, shards, method, matrix, 
     long rows (row-walk and product-then-sum kernels), sharded or not, with
     the epilogue operands loaded early or late, and with k-skip MrR's steps 0
     and 1 in one SpMV (EPI_STEP_MRR_FIRST2, r1 formed at every gathered
-    column) or not, on the diagonal-offset kernel or the row walks (KR_DIA)."""
+    column) or not, on the diagonal-offset kernel or the row walks (KR_DIA),
+    with the values streamed as dictionary codes or as doubles (KR_VDICT)."""
     A = golden_matrix(matrix)
     b = np.random.default_rng(3).standard_normal(A.shape[0])
     kw = dict(tol=1e-10, maxiter=400, k=k)
@@ -224,7 +225,8 @@ def test_fused_steps_bitwise_equal_unfused(monkeypatch, shards, method, matrix, 
     x0, i0 = _run_env(monkeypatch, {**base, "KR_FUSE": "0"}, method, A, b, **kw)
     for env in ({"KR_FUSE": "1", "KR_EPI_LATE": "1"}, {"KR_FUSE": "1", "KR_EPI_LATE": "0"},
                 {"KR_FUSE": "1", "KR_FUSE_FIRST": "0"}, {"KR_FUSE": "1", "KR_FUSE_FIRST": "1"},
-                {"KR_FUSE": "1", "KR_DIA": "0"}, {"KR_FUSE": "1", "KR_DIA": "2"}):
+                {"KR_FUSE": "1", "KR_DIA": "0"}, {"KR_FUSE": "1", "KR_DIA": "2"},
+                {"KR_FUSE": "1", "KR_VDICT": "0"}, {"KR_FUSE": "0", "KR_VDICT": "0"}):
         x1, i1 = _run_env(monkeypatch, {**base, **env}, method, A, b, **kw)
         np.testing.assert_array_equal(i1["nosl"], i0["nosl"])
         np.testing.assert_array_equal(i1["residual"], i0["residual"])
