@@ -397,8 +397,16 @@ struct MaskType<32> {
   using type = uint32_t;
 };
 
-template <int NV, int GATHER, typename W>
-__device__ __forceinline__ void row_window_mask(const double* s_val, const int32_t* s_M,
+// LDS view of a window's values for the dictionary path (spmv_kernel2 VI):
+// the window holds 1-byte codes, decoded through the LDS table on read.
+struct CodeView {
+  const uint8_t* c;
+  const double* t;
+  __device__ __forceinline__ double operator[](int j) const { return t[c[j]]; }
+};
+
+template <int NV, int GATHER, typename W, typename VS>
+__device__ __forceinline__ void row_window_mask(VS s_val, const int32_t* s_M,
                                                 const double* __restrict__ x1,
                                                 const double* __restrict__ x2, int64_t xrow,
                                                 int js, int je, W& mrem, double& sum1,
@@ -429,8 +437,8 @@ __device__ __forceinline__ void row_window_mask(const double* s_val, const int32
 }
 
 // One lane's entries [js, je) of the staged window, in stored order.
-template <int NV, int GATHER = kGather>
-__device__ __forceinline__ void row_window(const double* s_val, const int32_t* s_col,
+template <int NV, int GATHER = kGather, typename VS = const double*>
+__device__ __forceinline__ void row_window(VS s_val, const int32_t* s_col,
                                            const double* __restrict__ x1,
                                            const double* __restrict__ x2, int js, int je,
                                            double& sum1, double& sum2) {
@@ -457,8 +465,8 @@ __device__ __forceinline__ void row_window(const double* s_val, const int32_t* s
 // Further gather batches of a row whose input is virtual (is_virtual):
 // x(c) = r1 at column c from r0 = x1, y0 = x2, Ar1 = x3 (SpmvArgs), summed in
 // stored order. Columns from the LDS column window or the offset masks.
-template <int GATHER, typename W>
-__device__ __forceinline__ void row_window_virtual(const double* s_val, const int32_t* s_col,
+template <int GATHER, typename W, typename VS>
+__device__ __forceinline__ void row_window_virtual(VS s_val, const int32_t* s_col,
                                                    const int32_t* s_M, int64_t xrow,
                                                    const SpmvArgs& a, int js, int je, W& mrem,
                                                    double& sum1) {
@@ -955,7 +963,8 @@ __device__ __forceinline__ void stage_load2(Stage& st, const double* __restrict_
 // exchange of row pointers).
 // VI: values through the dictionary (SpmvArgs::vcode): each lane loads the 8
 // one-byte codes of its 8 window entries (one 8-byte load: windows start on a
-// multiple of 8) and decodes them from the LDS table when it commits the window.
+// multiple of 8) and commits them to an LDS code window (2 KiB instead of the
+// 16 KiB value window); entries are decoded through the LDS table on read.
 template <typename RP, int EPI, bool VEC, int MW, bool DB = true, bool NT = false,
           bool VI = false>
 __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
@@ -971,7 +980,9 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
   // DB: double-buffered windows, one barrier per window; else one buffer
   // (half the LDS: more workgroups per CU) and a second barrier.
   constexpr int NB = DB ? 2 : 1;
-  __shared__ __attribute__((aligned(16))) double s_val[NB][kWindow];
+  // VI: the window holds 1-byte codes (s_code), decoded through s_tab on read
+  __shared__ __attribute__((aligned(16))) double s_val[NB][VI ? 2 : kWindow];
+  __shared__ __attribute__((aligned(16))) uint8_t s_code[VI ? NB : 1][VI ? kWindow : 16];
   __shared__ __attribute__((aligned(16))) int32_t s_col[COLS ? NB : 1][COLS ? kWindow : 4];
   __shared__ int32_t s_M[COLS ? 1 : 64];
   __shared__ double s_red[(NP > 0 ? NP : 1) * 4];
@@ -1063,20 +1074,22 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
   W mask_n = 0;
 
   for (;;) {
-    double* sv = s_val[DB ? buf : 0];
+    using VS = typename std::conditional<VI, CodeView, const double*>::type;
+    VS sv;
+    if constexpr (VI)
+      sv = CodeView{s_code[DB ? buf : 0], s_tab};
+    else
+      sv = s_val[DB ? buf : 0];
     int32_t* sc = s_col[COLS && DB ? buf : 0];
     if constexpr (VI) {
-      dbl2v* dst = reinterpret_cast<dbl2v*>(sv) + tid * 4;
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        dst[q] = dbl2v{s_tab[(cw >> (16 * q)) & 0xff], s_tab[(cw >> (16 * q + 8)) & 0xff]};
+      reinterpret_cast<uint64_t*>(s_code[DB ? buf : 0])[tid] = cw;
       if constexpr (COLS) {
 #pragma unroll
         for (int q = 0; q < kCSlots; ++q)
           reinterpret_cast<int4v*>(sc)[tid + q * kBlock] = st.c[q];
       }
     } else {
-      stage_commit<COLS>(st, sv, sc, tid);
+      stage_commit<COLS>(st, s_val[DB ? buf : 0], sc, tid);
     }
     __syncthreads();
     const bool active = tid < nr;
@@ -1193,17 +1206,23 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
   block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
 }
 
+template <typename RP, int E, bool VEC, bool DB, bool NT>
+void spmv2_launch_vi(const SpmvArgs& a, dim3 grid, dim3 block, hipStream_t s) {
+  switch (a.mask ? a.mw : 0) {
+    case 8: spmv_kernel2<RP, E, VEC, 8, DB, NT, true><<<grid, block, 0, s>>>(a); return;
+    case 16: spmv_kernel2<RP, E, VEC, 16, DB, NT, true><<<grid, block, 0, s>>>(a); return;
+    case 32: spmv_kernel2<RP, E, VEC, 32, DB, NT, true><<<grid, block, 0, s>>>(a); return;
+    case 64: spmv_kernel2<RP, E, VEC, 64, DB, NT, true><<<grid, block, 0, s>>>(a); return;
+    default: spmv_kernel2<RP, E, VEC, 0, DB, NT, true><<<grid, block, 0, s>>>(a); return;
+  }
+}
+
 template <typename RP, int E, bool VEC, bool DB = true, bool NT = false>
 void spmv2_launch(const SpmvArgs& a, dim3 grid, dim3 block, hipStream_t s) {
   if constexpr (VEC) {
     if (a.vcode) {
-      switch (a.mask ? a.mw : 0) {
-        case 8: spmv_kernel2<RP, E, VEC, 8, DB, NT, true><<<grid, block, 0, s>>>(a); return;
-        case 16: spmv_kernel2<RP, E, VEC, 16, DB, NT, true><<<grid, block, 0, s>>>(a); return;
-        case 32: spmv_kernel2<RP, E, VEC, 32, DB, NT, true><<<grid, block, 0, s>>>(a); return;
-        case 64: spmv_kernel2<RP, E, VEC, 64, DB, NT, true><<<grid, block, 0, s>>>(a); return;
-        default: spmv_kernel2<RP, E, VEC, 0, DB, NT, true><<<grid, block, 0, s>>>(a); return;
-      }
+      spmv2_launch_vi<RP, E, VEC, DB, NT>(a, grid, block, s);
+      return;
     }
   }
   switch (a.mask ? a.mw : 0) {
