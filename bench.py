@@ -59,6 +59,8 @@ def parse():
     p.add_argument("--k", type=int, default=None)
     p.add_argument("--method", default=None)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-csr", action="store_true",
+                   help="skip the plain-CSR sub-record (KR_MASK=0 KR_VDICT=0 run)")
     p.add_argument("--cpu-n-side", type=int, default=512,
                    help="grid side of the CPU-baseline sample (512 = the benchmark system)")
     p.add_argument("--no-profile", action="store_true",
@@ -68,12 +70,14 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(n_side: int, k: int, method: str):
+def cpu_baseline(n_side: int, k: int, method: str, return_info: bool = False):
     """The oracle (numpy/scipy restatement of v3/cpu, bitwise the reference) on
     the host cores, on a bounded sample: the initial MrR step plus ONE outer
     k-skip iteration (k+2 solver iterations) of the same system (512^3 by
     default; a smaller n_side is scaled to 512^3 by the row ratio, since SpMV
-    and dots are linear in N). Timed region = the reference's info['time']."""
+    and dots are linear in N). Timed region = the reference's info['time'].
+    With return_info, also the oracle's (x-free) info dict: its residual
+    history is the full-size parity check of the GPU run (bench `parity`)."""
     import numpy as np
     from oracle import matrices, v3cpu
     try:
@@ -91,19 +95,45 @@ def cpu_baseline(n_side: int, k: int, method: str):
     t0 = time.perf_counter()
     _, info = fn(A, b, **kw)
     wall = time.perf_counter() - t0
+    del A, b
     its = int(info["nosl"][-1])
     rate = its / info["time"]
     cores = len(os.sched_getaffinity(0))
     scale = (n_side ** 3) / (512 ** 3)
     scaled = "" if n_side == 512 else f", scaled x{scale:.4f} to 512^3"
-    return dict(value=rate * scale, unit="iterations/s",
-                cores=blas_threads if blas_threads else cores,
-                kind="port",
-                sample=(f"oracle.v3cpu.{method} (numpy/scipy restatement of v3/cpu, bitwise "
-                        f"the reference) on {n_side}^3 Poisson, {its} iterations in "
-                        f"{info['time']:.2f} s ({rate:.3f} it/s){scaled}; "
-                        f"scipy SpMV 1 thread, OpenBLAS dot {blas_threads} threads, "
-                        f"{cores} affinity cores; wall {wall:.1f} s"))
+    rec = dict(value=rate * scale, unit="iterations/s",
+               cores=blas_threads if blas_threads else cores,
+               kind="port",
+               sample=(f"oracle.v3cpu.{method} (numpy/scipy restatement of v3/cpu, bitwise "
+                       f"the reference) on {n_side}^3 Poisson, {its} iterations in "
+                       f"{info['time']:.2f} s ({rate:.3f} it/s){scaled}; "
+                       f"scipy SpMV 1 thread, OpenBLAS dot {blas_threads} threads, "
+                       f"{cores} affinity cores; wall {wall:.1f} s"))
+    return (rec, info) if return_info else rec
+
+
+# SURVEY.md 8(c) contract for k-skip MrR (k <= 4): nosl identical, residual
+# entries >= 1e-8 within 1e-12 relative.
+PARITY_RTOL = 1e-12
+
+
+def history_parity(gpu_info, ref_info, rtol=PARITY_RTOL):
+    """Full-size parity: the GPU run's first history entries against the
+    oracle's run of the SAME system (same b, x0 = 0) in the cpu_baseline leg.
+    The oracle stops at maxiter (its last entry is the exit branch's
+    recomputed norm of the same r), so entries are compared by index."""
+    import numpy as np
+    m = len(ref_info["residual"])
+    g_res = np.asarray(gpu_info["residual"][:m], dtype=np.float64)
+    r_res = np.asarray(ref_info["residual"], dtype=np.float64)
+    nosl_eq = bool(np.array_equal(np.asarray(gpu_info["nosl"][:m]), ref_info["nosl"]))
+    big = r_res >= 1e-8
+    rel = np.abs(g_res - r_res) / np.abs(r_res)
+    max_rel = float(rel[big].max()) if big.any() else 0.0
+    ok = nosl_eq and len(g_res) == m and max_rel <= rtol
+    return dict(ok=bool(ok), entries=int(m), nosl_equal=nosl_eq, max_rel=max_rel, rtol=rtol,
+                reference="oracle.v3cpu (bitwise the reference's v3/cpu), same b, x0 = 0",
+                gpu=[float(v) for v in g_res], oracle=[float(v) for v in r_res])
 
 
 def stored_format_delta(nnz, n, lay, long_row=12.0):
@@ -131,62 +161,56 @@ def format_name(lay):
     return ", ".join(parts)
 
 
-def pmc_traffic(kernel):
-    """Beyond-L2 bytes per launch of `kernel` from the committed rocprofv3 PMC
-    summary (profiles/latest.json, made by tools/profile.sh +
-    tools/pmc_summary.py from TCC_EA0_RDREQ_{32B,64B,128B} / WRREQ request
-    counts on this same command). None if no profile of this kernel exists."""
-    path = os.path.join(REPO, "profiles", "latest.json")
+def pmc_traffic(config, kernel):
+    """Beyond-L2 bytes per launch of `kernel` in config `config` (e.g. "C4",
+    "C4_csr") from the committed rocprofv3 PMC summary profiles/pmc/<config>.json
+    (tools/profile.sh + tools/pmc_summary.py on that config's bench command:
+    TCC_EA0_RDREQ_{32B,64B,128B} / WRREQ request sizes). None when no profile
+    of this (config, kernel) pair exists: a kernel of another config or
+    another format never lends its bytes."""
+    path = os.path.join(REPO, "profiles", "pmc", f"{config}.json")
     try:
         with open(path) as f:
-            rec = json.load(f).get(kernel)
-        return None if rec is None else rec.get("traffic_bytes")
+            prof = json.load(f)
     except (OSError, ValueError):
         return None
+    if prof.get("_meta", {}).get("config") != config:
+        return None
+    rec = prof.get("kernels", {}).get(kernel)
+    return None if rec is None else rec.get("traffic_bytes")
 
 
-def main():
-    args = parse()
-    import numpy as np
+def run_system(args, cfg, mat, n, world, rank, local, comm, method, k, env=None):
+    """Build the system (optionally under KR_* format overrides, read at
+    finalize), run warmup + the timed steps, and return the measurements.
+    Timed region: barrier + device sync on both sides, max over ranks."""
     import torch
     import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local)
-    from parallel_krylov_amd.system import Communicator, KrylovSystem, balanced_partition
-
-    cfg = dict(CONFIGS[args.config])
-    method = args.method or cfg["method"]
-    mat = list(cfg["matrix"])
-    if args.n_side is not None and mat[0] == "poisson":
-        mat[1] = args.n_side
-    args.method = method
-    comm = None
-    if world > 1:
-        dist.init_process_group("gloo")
-        comm = Communicator.from_torch(None, local)
-    if args.nz is not None and mat[0] == "poisson":
-        n = mat[1] ** (mat[2] - 1) * args.nz
-        mat.append(args.nz)
-    else:
-        n = mat[1] ** mat[2] if mat[0] == "poisson" else mat[1]
-    part = balanced_partition(n, world)
-    sysm = KrylovSystem(n, [part[rank], part[rank + 1]], [local], comm)
-    if mat[0] == "poisson":
-        sysm.gen_poisson(mat[1], mat[2])
-    else:
-        sysm.gen_banded(mat[2], mat[3], mat[4])
-    sysm.finalize()
+    from parallel_krylov_amd.system import KrylovSystem, balanced_partition
+    saved = {key: os.environ.get(key) for key in (env or {})}
+    os.environ.update(env or {})
+    try:
+        part = balanced_partition(n, world)
+        sysm = KrylovSystem(n, [part[rank], part[rank + 1]], [local], comm)
+        if mat[0] == "poisson":
+            sysm.gen_poisson(mat[1], mat[2])
+        else:
+            sysm.gen_banded(mat[2], mat[3], mat[4])
+        sysm.finalize()
+    finally:
+        for key, v in saved.items():
+            if v is None:
+                os.environ.pop(key, None)
+            else:
+                os.environ[key] = v
     info = sysm.shard_info(0)
+    lay = sysm.shard_layout(0)
     b = sysm.rhs(1)
-    k = (args.k if args.k is not None else cfg["k"]) if "kskip" in method else 0
     per_step = (k + 1) if "kskip" in method else 1
     maxiter = (args.warmup + args.steps + 4) * per_step + 2
     # per-kernel HIP events on every 4th step (each event pair costs ~10 us of
     # launch gap; sampled, the timing costs <1 % at the 8-GPU shard size)
-    sysm.begin(args.method, b, None, tol=0.0, maxiter=maxiter, k=k,
+    sysm.begin(method, b, None, tol=0.0, maxiter=maxiter, k=k,
                profile=0 if args.no_profile else args.profile_every)
     sysm.step(args.warmup)
     sysm.reset_kernel_stats()
@@ -207,41 +231,110 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     stats = sysm.kernel_stats()
-    out = sysm.finish(args.method)
-    lay = sysm.shard_layout(0)
+    out = sysm.finish(method)
+    sysm.close()
+    del b
+    torch.cuda.empty_cache()
+    return dict(info=info, lay=lay, per_step=per_step, elapsed=elapsed, stats=stats,
+                history=out.info)
+
+
+def kernel_table(stats, delta):
+    """Per kernel: launches, average ms (HIP events on the solver's stream),
+    GB/s on the stored format's bytes and on SURVEY.md 8(d)'s CSR bytes."""
+    kernels, stored = {}, {}
+    for s_ in stats:
+        if s_["launches"]:
+            avg = s_["total_ms"] / s_["launches"]
+            csr = s_["bytes_per_launch"]
+            st = csr - (delta if s_["name"].startswith("spmv") else 0.0)
+            stored[s_["name"]] = (st, csr)
+            kernels[s_["name"]] = dict(launches=s_["launches"], avg_ms=round(avg, 5),
+                                       gbs=round(st / avg / 1e6, 1),
+                                       csr_gbs=round(csr / avg / 1e6, 1),
+                                       total_ms=round(s_["total_ms"], 3))
+    return kernels, stored
+
+
+def dominant(kernels):
+    spmv = {n_: v for n_, v in kernels.items() if n_.startswith("spmv")}
+    return max(spmv or kernels, key=lambda n_: kernels[n_]["total_ms"])
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local)
+    from parallel_krylov_amd.system import Communicator
+
+    cfg = dict(CONFIGS[args.config])
+    method = args.method or cfg["method"]
+    mat = list(cfg["matrix"])
+    if args.n_side is not None and mat[0] == "poisson":
+        mat[1] = args.n_side
+    comm = None
+    if world > 1:
+        dist.init_process_group("gloo")
+        comm = Communicator.from_torch(None, local)
+    if args.nz is not None and mat[0] == "poisson":
+        n = mat[1] ** (mat[2] - 1) * args.nz
+        mat.append(args.nz)
+    else:
+        n = mat[1] ** mat[2] if mat[0] == "poisson" else mat[1]
+    k = (args.k if args.k is not None else cfg["k"]) if "kskip" in method else 0
+
+    run = run_system(args, cfg, mat, n, world, rank, local, comm, method, k)
+    info, lay, per_step = run["info"], run["lay"], run["per_step"]
     delta = stored_format_delta(info["nnz"], info["n_local"], lay)
     iterations = args.steps * per_step
-    value = iterations / elapsed
-
+    value = iterations / run["elapsed"]
+    kernels, stored = kernel_table(run["stats"], delta)
     roofline = None
-    kernels = {}
-    if stats:
-        stored = {}
-        for s in stats:
-            if s["launches"]:
-                avg = s["total_ms"] / s["launches"]
-                csr = s["bytes_per_launch"]
-                st = csr - (delta if s["name"].startswith("spmv") else 0.0)
-                stored[s["name"]] = (st, csr)
-                kernels[s["name"]] = dict(launches=s["launches"], avg_ms=round(avg, 5),
-                                          gbs=round(st / avg / 1e6, 1),
-                                          csr_gbs=round(csr / avg / 1e6, 1),
-                                          total_ms=round(s["total_ms"], 3))
-        spmv = {n_: v for n_, v in kernels.items() if n_.startswith("spmv")}
-        dom = max(spmv or kernels, key=lambda n_: kernels[n_]["total_ms"])
+    if kernels:
+        dom = dominant(kernels)
         d = kernels[dom]
         ach = d["gbs"]
         # achieved = the minimum bytes of the format the kernel streams (offset
         # masks instead of columns, 1-byte dictionary codes instead of values:
         # DESIGN.md 9); the CSR figure of SURVEY.md 8(d) is csr_equiv_gbs
         roofline = dict(bound="hbm", kernel=dom, achieved=ach, peak=HBM_PEAK_GBS, unit="GB/s",
-                        frac=round(ach / HBM_PEAK_GBS, 4), traffic=pmc_traffic(dom),
+                        frac=round(ach / HBM_PEAK_GBS, 4),
+                        traffic=pmc_traffic(args.config, dom),
+                        traffic_source=f"profiles/pmc/{args.config}.json",
                         bytes_per_launch=stored[dom][0], csr_bytes_per_launch=stored[dom][1],
                         csr_equiv_gbs=d["csr_gbs"], format=format_name(lay),
                         avg_ms=d["avg_ms"])
+
+    # The same workload on plain CSR (no offset masks, no value dictionary:
+    # 4-byte columns and 8-byte values streamed), timed in the same run: the
+    # north star's "CSR SpMV" roofline on SURVEY.md 8(d)'s bytes.
+    csr_rec = None
+    if not args.no_csr and (lay["mask_bits"] or lay["dict_values"]):
+        rc = run_system(args, cfg, mat, n, world, rank, local, comm, method, k,
+                        env={"KR_MASK": "0", "KR_VDICT": "0"})
+        kc, _ = kernel_table(rc["stats"], 0.0)
+        csr_rec = dict(value=round(iterations / rc["elapsed"], 3), unit="iterations/s",
+                       ms_per_step=round(rc["elapsed"] / args.steps * 1e3, 4),
+                       format=format_name(rc["lay"]), env="KR_MASK=0 KR_VDICT=0")
+        if kc:
+            dc = dominant(kc)
+            csr_rec.update(kernel=dc, avg_ms=kc[dc]["avg_ms"], achieved=kc[dc]["gbs"],
+                           frac=round(kc[dc]["gbs"] / HBM_PEAK_GBS, 4),
+                           traffic=pmc_traffic(args.config + "_csr", dc),
+                           traffic_source=f"profiles/pmc/{args.config}_csr.json",
+                           kernels=kc)
+
     base = None
+    parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "C4":
-        base = cpu_baseline(args.cpu_n_side, k, method)
+        base, ref_info = cpu_baseline(args.cpu_n_side, k, method, return_info=True)
+        if args.cpu_n_side == mat[1] and args.nz is None and mat[0] == "poisson":
+            parity = history_parity(run["history"], ref_info)
     if rank == 0:
         rec = {
             "metric": (HEADLINE_METRIC if args.config == "C4"
@@ -251,7 +344,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "ms_per_step": round(run["elapsed"] / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -264,11 +357,12 @@ def main():
                        "parallelism": f"row-partitioned x{world}, RCCL halo + Gram all-gather"},
             "roofline": roofline,
             "cpu_baseline": base,
+            "parity": parity,
+            "csr": csr_rec,
             "kernels": kernels,
-            "residual_tail": [float(v) for v in out.info["residual"][-3:-1]],
+            "residual_tail": [float(v) for v in run["history"]["residual"][-3:-1]],
         }
         print(json.dumps(rec))
-    sysm.close()
     if comm is not None:
         comm.close()
     if world > 1:

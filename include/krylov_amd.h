@@ -171,7 +171,12 @@ int kr_system_destroy(kr_system* sys);
  * row_begin[s]..row_begin[s+1], GLOBAL column indices, rowptr starting at
  * rowptr[0] (need not be 0). The caller keeps the buffers alive until
  * kr_system_destroy; column indices are rewritten IN PLACE to the shard's
- * local (halo-extended) numbering by kr_system_finalize. */
+ * local (halo-extended) numbering by kr_system_finalize.
+ * The matrix is FROZEN at kr_system_finalize: the SpMV kernels stream derived
+ * copies built there (offset masks from the columns, the value dictionary's
+ * codes and table, diagonal-offset values), so values changed in val_dev
+ * after finalize are seen by some kernels and not by others. To solve with
+ * new values, create (adopt, finalize) a new system. */
 int kr_system_adopt_csr(kr_system* sys, int shard, const void* rowptr_dev, int rowptr64,
                         int32_t* col_dev, const double* val_dev);
 
@@ -219,6 +224,13 @@ int kr_system_shard_layout(kr_system* sys, int shard, int* mask_bits, int* n_off
  * disables). Replaces nothing in the reference: the cuSPARSE csrmv behind
  * v3/gpu/common.py:119 always streams 8-byte values. */
 int kr_system_shard_values(kr_system* sys, int shard, int* dict_values);
+/* Launch geometry of shard s (after finalize): grid = workgroups of the
+ * elementwise kernels, spmv_grid = workgroups of the SpMV kernels. Together
+ * with the interior range of kr_system_shard_layout they fix the summation
+ * order of every dot product (oracle/gpu_order.py restates it
+ * for the bitwise GPU-order parity tests). Replaces nothing in the
+ * reference (cuBLAS ddot's order is internal). Pointers may be NULL. */
+int kr_system_shard_sched(kr_system* sys, int shard, int* grid, int* spmv_grid);
 
 /* Halo exchange plan (pure host arithmetic, no device; test hook and the
  * planner kr_system_finalize uses). part[0..nshards] is the global row
@@ -247,9 +259,17 @@ typedef struct {
   int method;      /* KR_METHOD_* */
   int k;           /* k-skip depth (ignored by CG/MrR) */
   double tol;      /* relative residual tolerance */
-  int64_t maxiter; /* <= 0: n_global (reference default, v3/gpu/common.py:35) */
+  int64_t maxiter; /* < 0: n_global (reference default for None,
+                      v3/gpu/common.py:35); 0 is honoured (CG / k-skip CG return
+                      the initial residual; the MrR family is refused: the
+                      reference raises IndexError there) */
   int profile;     /* N > 0: per-kernel HIP-event timing on every N-th outer
                      iteration (1 = all; events cost ~10 us per kernel) */
+  int nan_guard;   /* 1: stop at the first NaN/Inf residual entry (reported as
+                      not converged, kr_solve_result.diverged = 1). 0 (default):
+                      the reference's semantics -- a NaN never passes the tests
+                      `res < tol` / `res > pre_res`, so the loop runs on to
+                      maxiter (v3/cpu/kskipmrr.py:39-42, v3/common.py:17). */
 } kr_solve_params;
 
 typedef struct {
@@ -259,6 +279,7 @@ typedef struct {
   int converged;        /* residual < tol reached */
   int final_k;          /* adaptive: final k */
   double final_residual;
+  int diverged;         /* nan_guard stopped the loop at a non-finite residual */
 } kr_solve_result;
 
 /* Set up vectors, r0 = b - A x0 and ||b||; b_dev[s]/x0_dev[s] hold shard s's

@@ -1,0 +1,246 @@
+"""The engine's dot-product summation order, restated in numpy (TEST INFRASTRUCTURE ONLY).
+
+The oracle (oracle/v3cpu.py) is bitwise the reference given the reference's
+dot products (numpy/OpenBLAS order). The GPU path computes every SpMV row,
+vector update and scalar recurrence bitwise like the reference; ONLY the
+summation order of its dot products differs. For k-skip
+methods with large k the trajectory amplifies that rounding difference into
+a different history (adaptive k-skip MrR's rollbacks are rounding events), so
+a history check against the reference fixtures is only loose there.
+
+This module restates the engine's fixed summation order so that the oracle
+can run with EXACTLY the GPU's dot products: ``with gpu_order.patched(sched):
+v3cpu.adaptivekskipmrr(...)`` must then equal the GPU run bit for bit --
+nosl, khistory, every residual entry and x -- through every rollback.
+
+What is restated (single process; shards in shard order, RCCL ranks in rank
+order, as System::reduce and scalar_kernel sum them):
+
+* SpMV epilogue products (kr_spmv.h ``epi_products``): lane ``tid`` of
+  workgroup ``b`` owns rows ``rb*256 + tid`` of the row blocks RowSched gives
+  it (XCD-aware when the grid is a multiple of 8, kr_spmv.h RowSched::init)
+  and accumulates ``acc = acc + p[row]`` from 0.0 in visit order;
+  ``block_reduce_store`` folds each wave with the ``__shfl_down`` tree
+  (offsets 32..1) and the 4 waves as ``((w0 + w1) + w2) + w3``. A sharded
+  system splits each SpMV into an interior launch and one boundary launch that
+  ADDS its partials (kr_engine.cpp System::spmv).
+* Elementwise-kernel products (kr_kernels.hip ``ew_kernel``, 16-byte pairs):
+  thread ``t0`` adds ``p[2q]`` then ``p[2q+1]`` for q = t0, t0 + stride, ...;
+  an odd tail element goes to thread 0 of block 0 last.
+* Finalize (kr_kernels.hip ``block_slot_sum``): thread i sums partials
+  i, i+256, ... from 0.0, then the same wave tree and wave order; the host
+  adds the shards' totals to 0.0 in order.
+
+Which kernel computes which dot is a property of the method: in k-skip MrR,
+adaptive k-skip MrR and k-skip CG every dot after ||b|| comes from an SpMV
+epilogue (EPI_BMINUS, EPI_XY, EPI_HEAD_*, EPI_DUAL_*); ||b|| comes from
+EW_DOT. ``patched`` installs exactly that mapping.
+"""
+from __future__ import annotations
+
+import contextlib
+from dataclasses import dataclass
+
+import numpy as np
+
+BLOCK = 256  # kBlock (kr_internal.h)
+
+
+@dataclass
+class ShardSched:
+    """One shard's launch geometry (KrylovSystem.shard_sched)."""
+    n: int           # own rows
+    grid: int        # elementwise-kernel workgroups (default_grid)
+    spmv_grid: int   # SpMV workgroups (spmv_grid_for)
+    int_lo: int = 0  # interior rows [int_lo, int_hi) of the split SpMV
+    int_hi: int = 0
+
+
+def shard_scheds(A, part, cus: int = 256):
+    """The launch geometry kr_system_finalize gives the row blocks part[s]..
+    part[s+1] of A (kr_engine.cpp default_grid / spmv_grid_for / interior
+    rows; MI355X: 256 CUs x 8 workgroups). The GPU tests read the engine's
+    own values (KrylovSystem.shard_sched) and check them against this."""
+    import scipy.sparse as sp
+    A = sp.csr_matrix(A)
+    cap = cus * 8
+    out = []
+    for s in range(len(part) - 1):
+        r0, r1 = part[s], part[s + 1]
+        n = r1 - r0
+        blk = A[r0:r1]
+        rows = np.repeat(np.arange(n), np.diff(blk.indptr))
+        cols = blk.indices.astype(np.int64)
+        reach = int(np.max(np.abs(cols - (r0 + rows)))) if cols.size else 0
+        below = rows[cols < r0]
+        above = rows[cols > r1 - 1]
+        h0 = int(below.max()) + 1 if below.size else 0
+        h1 = int(above.min()) if above.size else n
+        int_lo = min(-(-h0 // BLOCK) * BLOCK, n)
+        int_hi = max(h1 // BLOCK * BLOCK, int_lo)
+        nrb = max(1, -(-n // BLOCK))
+        base = min(nrb, cap)
+        rb = -(-reach // BLOCK)
+        if rb * 8 <= base or rb * 8 > cap * 8 or rb * 8 > nrb:
+            g = base
+        else:
+            g = rb * 8
+            while g // 2 >= base and g > nrb // 16 and (g // 2) % 8 == 0:
+                g //= 2
+        out.append(ShardSched(n=n, grid=base, spmv_grid=g, int_lo=int_lo, int_hi=int_hi))
+    return out
+
+
+def _visits(rows: int, grid: int, gap_at: int = 0, gap: int = 0):
+    """Row blocks (launch-local) each workgroup visits, in order (RowSched)."""
+    nrb = -(-rows // BLOCK) - gap
+    out = []
+    for b in range(grid):
+        if grid % 8 == 0:
+            q, j0, jstep = b & 7, b >> 3, grid >> 3
+            chunk = (nrb + 7) // 8
+            base = q * chunk
+            jcount = max(0, min(nrb, base + chunk) - base)
+        else:
+            j0, jstep, jcount, base = b, grid, nrb, 0
+        vis = []
+        for v in range(j0, jcount, jstep):
+            r = base + v
+            vis.append(r if r < gap_at else r + gap)
+        out.append(vis)
+    return out
+
+
+def _wave_tree(v):
+    """Lane 0 after ``v += __shfl_down(v, off)`` for off = 32, 16, ..., 1."""
+    v = np.asarray(v, dtype=np.float64)
+    off = 32
+    while off >= 1:
+        v = v[:off] + v[off:2 * off]
+        off >>= 1
+    return v[0]
+
+
+def _block_total(acc):
+    """block_reduce_store / block_slot_sum: 4 wave trees, ((w0+w1)+w2)+w3."""
+    w = [_wave_tree(acc[64 * i:64 * (i + 1)]) for i in range(4)]
+    t = w[0]
+    t = t + w[1]
+    t = t + w[2]
+    t = t + w[3]
+    return np.float64(t)
+
+
+def _launch_partials(p, rows, grid, gap_at=0, gap=0):
+    """Per-workgroup partials of one SpMV launch over products p[0:rows]."""
+    out = np.zeros(grid, np.float64)
+    lanes = np.arange(BLOCK)
+    for b, vis in enumerate(_visits(rows, grid, gap_at, gap)):
+        acc = np.zeros(BLOCK, np.float64)
+        for rb in vis:
+            r = rb * BLOCK + lanes
+            act = r < rows
+            acc[act] = acc[act] + p[r[act]]
+        out[b] = _block_total(acc)
+    return out
+
+
+def finalize(partials):
+    """block_slot_sum over the slot's partials (fixed order)."""
+    acc = np.zeros(BLOCK, np.float64)
+    for i0 in range(0, len(partials), BLOCK):
+        chunk = np.asarray(partials[i0:i0 + BLOCK], dtype=np.float64)
+        acc[:chunk.size] = acc[:chunk.size] + chunk
+    return _block_total(acc)
+
+
+def spmv_shard_total(p, s: ShardSched, split: bool):
+    """One shard's total of the epilogue products p (length s.n)."""
+    if not split:
+        return finalize(_launch_partials(p, s.n, s.spmv_grid))
+    part = _launch_partials(p[s.int_lo:s.int_hi], s.int_hi - s.int_lo, s.spmv_grid)
+    nb_lo = s.int_lo // BLOCK
+    nb_gap = (s.int_hi - s.int_lo) // BLOCK
+    nb_all = -(-s.n // BLOCK)
+    if nb_all - nb_gap > 0:
+        g = min(s.spmv_grid, nb_all - nb_gap)
+        bnd = _launch_partials(p, s.n, g, nb_lo, nb_gap)
+        part[:g] = part[:g] + bnd
+    return finalize(part)
+
+
+def ew_shard_total(p, s: ShardSched):
+    """One shard's total of elementwise-kernel products (ew_kernel, pairs)."""
+    n = s.n
+    stride = s.grid * BLOCK
+    npairs = n // 2
+    acc = np.zeros((s.grid, BLOCK), np.float64).reshape(-1)
+    for q0 in range(0, npairs, stride):
+        q = np.arange(q0, min(q0 + stride, npairs))
+        t = q - q0
+        acc[t] = acc[t] + p[2 * q]
+        acc[t] = acc[t] + p[2 * q + 1]
+    if n & 1:
+        acc[0] = acc[0] + p[n - 1]
+    acc = acc.reshape(s.grid, BLOCK)
+    return finalize([_block_total(acc[b]) for b in range(s.grid)])
+
+
+class GpuOrder:
+    """Dot products summed like the engine over the given shards."""
+
+    def __init__(self, shards):
+        self.shards = list(shards)
+        self.split = len(self.shards) > 1 and all(s.int_lo < s.int_hi for s in self.shards)
+        self.bounds = np.cumsum([0] + [s.n for s in self.shards])
+
+    def _total(self, p, kind):
+        tot = np.float64(0.0)
+        for i, s in enumerate(self.shards):
+            seg = p[self.bounds[i]:self.bounds[i + 1]]
+            t = spmv_shard_total(seg, s, self.split) if kind == "spmv" else ew_shard_total(seg, s)
+            tot = tot + t
+        return np.float64(tot)
+
+    def spmv_dot(self, u, v):
+        return self._total(np.asarray(u, np.float64) * np.asarray(v, np.float64), "spmv")
+
+    def ew_dot(self, u, v):
+        return self._total(np.asarray(u, np.float64) * np.asarray(v, np.float64), "ew")
+
+
+SPMV_ONLY_METHODS = ("kskipmrr", "adaptivekskipmrr", "kskipcg")
+
+
+@contextlib.contextmanager
+def patched(order: GpuOrder):
+    """Run oracle.v3cpu's k-skip methods with the engine's dot order.
+
+    The first norm a solver takes is ||b|| (oracle _History), which the engine
+    computes with EW_DOT; every later dot and norm of the k-skip methods is an
+    SpMV epilogue product."""
+    from . import v3cpu
+    saved = (v3cpu._dot, v3cpu._norm)
+    state = {"first": True}
+
+    def norm(v):
+        if state["first"]:
+            state["first"] = False
+            return np.float64(np.sqrt(order.ew_dot(v, v)))
+        return np.float64(np.sqrt(order.spmv_dot(v, v)))
+
+    v3cpu._dot = order.spmv_dot
+    v3cpu._norm = norm
+    try:
+        yield
+    finally:
+        v3cpu._dot, v3cpu._norm = saved
+
+
+def run(method, A, b, shards, **kw):
+    """oracle.v3cpu.<method> with the engine's summation order."""
+    from . import v3cpu
+    if method not in SPMV_ONLY_METHODS:
+        raise ValueError(f"{method}: GPU-order emulation covers {SPMV_ONLY_METHODS}")
+    with patched(GpuOrder(shards)), np.errstate(all="ignore"):
+        return v3cpu.METHODS[method](A, b, **kw)

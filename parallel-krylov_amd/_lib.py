@@ -28,13 +28,15 @@ class KrylovError(RuntimeError):
 
 class SolveParams(ctypes.Structure):
     _fields_ = [("method", ctypes.c_int), ("k", ctypes.c_int), ("tol", ctypes.c_double),
-                ("maxiter", ctypes.c_int64), ("profile", ctypes.c_int)]
+                ("maxiter", ctypes.c_int64), ("profile", ctypes.c_int),
+                ("nan_guard", ctypes.c_int)]
 
 
 class SolveResult(ctypes.Structure):
     _fields_ = [("time_s", ctypes.c_double), ("iterations", ctypes.c_int64),
                 ("entries", ctypes.c_int64), ("converged", ctypes.c_int),
-                ("final_k", ctypes.c_int), ("final_residual", ctypes.c_double)]
+                ("final_k", ctypes.c_int), ("final_residual", ctypes.c_double),
+                ("diverged", ctypes.c_int)]
 
 
 class KernelStat(ctypes.Structure):
@@ -88,6 +90,7 @@ _SIGNATURES = {
     "kr_system_shard_info": [_P, _I, _PI64, _PI64, _PI64, _PI64],
     "kr_system_shard_layout": [_P, _I, _PI, _PI, _PI64, _PI64],
     "kr_system_shard_values": [_P, _I, _PI],
+    "kr_system_shard_sched": [_P, _I, _PI, _PI],
     "kr_fill_rhs": [_P, _I, _U64, _P],
     "kr_system_csr": [_P, _I, _PP, _PI, _PP, _PP, _PI64],
     "kr_system_spmv": [_PP, _PP, _PP],

@@ -635,6 +635,15 @@ int kr_system_shard_values(kr_system* sys, int shard, int* dict_values) {
   });
 }
 
+int kr_system_shard_sched(kr_system* sys, int shard, int* grid, int* spmv_grid) {
+  return guarded([&] {
+    KR_REQUIRE(sys && shard >= 0 && shard < (int)sys->shards.size(), "bad shard");
+    KR_REQUIRE(sys->finalized, "system not finalized");
+    if (grid) *grid = sys->shards[shard].grid;
+    if (spmv_grid) *spmv_grid = sys->shards[shard].spmv_grid;
+  });
+}
+
 int kr_system_csr(kr_system* sys, int shard, const void** rowptr, int* rowptr64,
                   const int32_t** col, const double** val, int64_t* pad) {
   return guarded([&] {
@@ -734,6 +743,7 @@ int kr_solve_end(kr_system* sys, double* const* x, kr_solve_result* res) {
       res->converged = ss.converged ? 1 : 0;
       res->final_k = ss.k;
       res->final_residual = ss.residual.empty() ? 0.0 : ss.residual[ss.index];
+      res->diverged = ss.diverged ? 1 : 0;
     }
     if (x) {
       const int id = ss.result_x();

@@ -312,27 +312,37 @@ void System::build_vdict(Shard& s) {
   std::sort(keys.begin(), keys.end());
   const int nk = (int)keys.size();
   // vcode (indexed like val) must be 8-byte aligned with readable bytes on
-  // both sides: windows start at (first entry) & ~7 and load 8 codes per lane
+  // both sides: windows start at (first entry) & ~7 and load 8 codes per lane.
+  // Either allocation failing (or a pattern the encode pass cannot find)
+  // leaves the shard on the 8-byte values, with nothing half built.
   const int64_t pre = 8 + (s.nz0 & 7);
-  uint8_t* code = nullptr;
-  if (hipMalloc(&code, (size_t)(pre + s.nnz + 16)) != hipSuccess) {
-    KR_HIP_CHECK(hipFree(gtab));
-    (void)hipGetLastError();
-    return;  // no room for the codes: keep the 8-byte values
-  }
-  s.owned.push_back(code);
   double* tab = nullptr;
-  KR_HIP_CHECK(hipMalloc(&tab, kVdMax * sizeof(double)));
-  s.owned.push_back(tab);
+  uint8_t* code = nullptr;
+  if (hipMalloc(&tab, kVdMax * sizeof(double)) != hipSuccess ||
+      hipMalloc(&code, (size_t)(pre + s.nnz + 16)) != hipSuccess) {
+    (void)hipGetLastError();
+    if (tab) (void)hipFree(tab);
+    (void)hipFree(gtab);
+    return;  // no room for the dictionary: keep the 8-byte values
+  }
   // the sorted keys (bit patterns) double as the value table
   KR_HIP_CHECK(hipMemcpyAsync(gtab, keys.data(), nk * sizeof(unsigned long long),
                               hipMemcpyHostToDevice, s.stream));
   KR_HIP_CHECK(hipMemcpyAsync(tab, keys.data(), nk * sizeof(unsigned long long),
                               hipMemcpyHostToDevice, s.stream));
   KR_HIP_CHECK(hipMemsetAsync(code, 0, (size_t)(pre + s.nnz + 16), s.stream));
-  launch_vdict_encode(s.val + s.nz0, s.nnz, gtab, nk, code + pre, s.stream);
+  launch_vdict_encode(s.val + s.nz0, s.nnz, gtab, nk, code + pre, flags, s.stream);
+  int miss = 0;
+  KR_HIP_CHECK(hipMemcpyAsync(&miss, flags, sizeof(int), hipMemcpyDeviceToHost, s.stream));
   KR_HIP_CHECK(hipStreamSynchronize(s.stream));
   KR_HIP_CHECK(hipFree(gtab));
+  if (miss) {  // a value outside the table: the codes would be wrong
+    (void)hipFree(code);
+    (void)hipFree(tab);
+    return;
+  }
+  s.owned.push_back(code);
+  s.owned.push_back(tab);
   s.vcode = code + pre - s.nz0;  // indexed like val
   s.vtab = tab;
   s.ntab = nk;
@@ -1117,7 +1127,7 @@ class CgSession : public Base {
     sys->spmv(EPI_BMINUS, X, -1, R, -1, -1, B, 0);  // r = b - A x
     gamma = sys->reduce(1)[0];                      // gamma = <r,r>
     sys->copy_own(P, R);                            // p = r.copy()
-    dev = sys->device_scalars();
+    dev = sys->device_scalars() && !prm.nan_guard;  // the guard tests every entry on the host
     if (dev) {
       thr = conv_threshold(bnorm, prm.tol);
       sys->scalar_state_init(gamma);
@@ -1139,6 +1149,7 @@ class CgSession : public Base {
       converged = true;
       return done = true;
     }
+    if (guard_stop(i)) return true;
     if (dev) {
       if (qpos >= q.size()) run_batch();
       gamma = q[qpos++];
@@ -1216,7 +1227,7 @@ class MrrSession : public Base {
     i = 1;
     index = 1;
     set_entry(1, 0.0);
-    dev = sys->device_scalars();
+    dev = sys->device_scalars() && !prm.nan_guard;  // the guard tests every entry on the host
     if (dev) {
       thr = conv_threshold(bnorm, prm.tol);
       sys->scalar_state_init(0.0);
@@ -1246,6 +1257,7 @@ class MrrSession : public Base {
         converged = true;
         return done = true;
       }
+      if (guard_stop(i)) return true;
       const double gamma = g[2] / g[1];  // nu / mu
       sys->ew(EW_MRR_S, gamma, 0, {AR, Y, R, -1, -1, -1}, 0);
       const auto h = sys->reduce(2);
@@ -1367,6 +1379,7 @@ class KskipMrrSession : public Base {
       converged = true;
       return done = true;
     }
+    if (guard_stop(index)) return true;
     // Gram -> (alpha, beta, delta) as the reference lays them out.
     std::vector<double> alpha(2 * k + 3, 0.0), beta(2 * k + 2, 0.0), delta(2 * k + 1, 0.0);
     alpha[0] = g[0];
@@ -1498,6 +1511,7 @@ class KskipCgSession : public Base {
       converged = true;
       return done = true;
     }
+    if (guard_stop(index)) return true;
     std::vector<double> a(2 * k + 2, 0.0), f(2 * k + 4, 0.0), c(2 * k + 2, 0.0);
     a[0] = g[0];
     f[0] = g[1];
@@ -1559,7 +1573,12 @@ std::unique_ptr<Session> make_session(System* sys, const kr_solve_params& p) {
   }
   s->sys = sys;
   s->prm = p;
-  if (s->prm.maxiter <= 0) s->prm.maxiter = sys->n_global;
+  if (s->prm.maxiter < 0) s->prm.maxiter = sys->n_global;  // None -> N (v3/cpu/common.py:29-30)
+  // maxiter = 0: CG and k-skip CG return the initial residual; the MrR family
+  // takes its first step unconditionally and writes nosl[1] of a length-1
+  // array, an IndexError in the reference (v3/cpu/mrr.py:31, kskipmrr.py:32)
+  KR_REQUIRE(s->prm.maxiter > 0 || p.method == KR_METHOD_CG || p.method == KR_METHOD_KSKIPCG,
+             "maxiter=0: the MrR family writes nosl[1] past its maxiter+1 entries (IndexError in the reference)");
   return s;
 }
 

@@ -2,6 +2,8 @@
 // the solver sessions. One host thread drives every shard the process owns.
 #pragma once
 
+#include <cmath>
+
 #include <rccl/rccl.h>
 
 #include <array>
@@ -198,7 +200,7 @@ class Session {
   int k = 0;
   double bnorm = 0;
   int64_t i = 0, index = 0;
-  bool done = false, converged = false;
+  bool done = false, converged = false, diverged = false;
   std::vector<double> residual;
   std::vector<int64_t> nosl, khist;
   bool track_k = false;
@@ -218,6 +220,15 @@ class Session {
     khist[idx] = v;
   }
   int64_t entries() const { return index + 1; }
+  // kr_solve_params::nan_guard: a non-finite residual entry ends the solve
+  // (reported not converged); off, NaN runs on to maxiter as in the reference.
+  bool guard_stop(int64_t idx) {
+    if (prm.nan_guard && !std::isfinite(residual[idx])) {
+      diverged = true;
+      done = true;
+    }
+    return diverged;
+  }
 };
 
 std::unique_ptr<Session> make_session(System* sys, const kr_solve_params& p);

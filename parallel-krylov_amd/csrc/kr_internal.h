@@ -290,7 +290,7 @@ constexpr int kVdGlobal = 1024;
 void launch_vdict_collect(const double* val, int64_t nnz, unsigned long long* gtab, int* flags,
                           hipStream_t s);
 void launch_vdict_encode(const double* val, int64_t nnz, const unsigned long long* keys, int nk,
-                         uint8_t* code, hipStream_t s);
+                         uint8_t* code, int* miss, hipStream_t s);
 // col[j] += delta for all stored entries of the block.
 void launch_col_shift(const void* rowptr, int rowptr64, int64_t n, int32_t* col,
                       int64_t delta, hipStream_t s);

@@ -1021,10 +1021,12 @@ __global__ __launch_bounds__(256) void vdict_collect_kernel(const unsigned long 
 }
 
 // code[j] = index of val[j]'s bit pattern in the ascending table keys[0, nk).
+// A pattern missing from the table (the collect pass must have seen every
+// one; this checks it) sets *miss, and the host then drops the dictionary.
 __global__ __launch_bounds__(256) void vdict_encode_kernel(const unsigned long long* val,
                                                            int64_t nnz,
                                                            const unsigned long long* keys,
-                                                           int nk, uint8_t* code) {
+                                                           int nk, uint8_t* code, int* miss) {
   __shared__ unsigned long long sk[kVdMax];
   for (int i = threadIdx.x; i < nk; i += blockDim.x) sk[i] = keys[i];
   __syncthreads();
@@ -1040,6 +1042,7 @@ __global__ __launch_bounds__(256) void vdict_encode_kernel(const unsigned long l
         hi = mid;
     }
     code[j] = (uint8_t)lo;
+    if (sk[lo] != key) *miss = 1;  // plain vector store: every writer stores 1
   }
 }
 }  // namespace
@@ -1056,11 +1059,12 @@ void launch_vdict_collect(const double* val, int64_t nnz, unsigned long long* gt
 }
 
 void launch_vdict_encode(const double* val, int64_t nnz, const unsigned long long* keys, int nk,
-                         uint8_t* code, hipStream_t s) {
+                         uint8_t* code, int* miss, hipStream_t s) {
+  KR_HIP_CHECK(hipMemsetAsync(miss, 0, sizeof(int), s));
   if (nnz <= 0) return;
   const unsigned g = std::min<unsigned>(blocks_for(nnz, 256), 8192);
   vdict_encode_kernel<<<g, 256, 0, s>>>(reinterpret_cast<const unsigned long long*>(val), nnz,
-                                        keys, nk, code);
+                                        keys, nk, code, miss);
   KR_HIP_CHECK(hipGetLastError());
 }
 

@@ -135,12 +135,15 @@ def gpu_ids_range():
 
 
 def local_device(rank: int) -> int:
-    """Device of this rank: LOCAL_RANK, else the first of GPU_IDS
-    (v3/gpu/mpi/common.py:77-83), else rank modulo the device count."""
-    if "LOCAL_RANK" in os.environ:  # more ranks than GPUs share them round-robin
+    """Device of this rank: the first id of GPU_IDS when it is set (the
+    reference's per-rank GPU range, v3/gpu/mpi/common.py:77-83: the launcher
+    sets it per process), else LOCAL_RANK (torchrun; more ranks than GPUs
+    share them round-robin), else rank modulo the device count."""
+    rng = gpu_ids_range()
+    if rng is not None:
+        return rng[0]
+    if "LOCAL_RANK" in os.environ:
         return int(os.environ["LOCAL_RANK"]) % max(_lib.device_count(), 1)
-    if os.environ.get("GPU_IDS"):
-        return int(os.environ["GPU_IDS"].split(",")[0])
     n = _lib.device_count()
     return rank % max(n, 1)
 
@@ -154,6 +157,14 @@ class SolveOutput:
     final_k: int
     final_residual: float
     kernel_stats: list = field(default_factory=list)
+    diverged: bool = False
+
+
+def nan_guard_default() -> bool:
+    """KRYLOV_AMD_NAN_GUARD=1: stop a solve at its first NaN/Inf residual
+    (Status: diverged). Off by default: the reference runs a NaN trajectory on
+    to maxiter (no test ever fires on NaN, v3/cpu/kskipmrr.py:39-42)."""
+    return os.environ.get("KRYLOV_AMD_NAN_GUARD", "0") not in ("", "0")
 
 
 class KrylovSystem:
@@ -274,6 +285,16 @@ class KrylovSystem:
         return dict(mask_bits=mb.value, n_offsets=no.value, interior_lo=lo.value,
                     interior_hi=hi.value, dict_values=dv.value)
 
+    def shard_sched(self, s: int) -> dict:
+        """Launch geometry of shard s: elementwise and SpMV grids plus the
+        interior rows of the split SpMV -- what fixes the engine's dot-product
+        summation order (oracle/gpu_order.py restates it for the tests)."""
+        g, sg = ctypes.c_int(), ctypes.c_int()
+        call("kr_system_shard_sched", self.handle, s, ctypes.byref(g), ctypes.byref(sg))
+        lay = self.shard_layout(s)
+        return dict(n=self.row_begin[s + 1] - self.row_begin[s], grid=g.value,
+                    spmv_grid=sg.value, int_lo=lay["interior_lo"], int_hi=lay["interior_hi"])
+
     def csr_pointers(self, s: int) -> dict:
         """Raw device CSR of shard s (local columns after finalize)."""
         rp, col, val = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
@@ -326,16 +347,20 @@ class KrylovSystem:
         return ys
 
     def solve(self, method: str, b_parts, x0_parts=None, tol=1e-5, maxiter=None, k=0,
-              profile=False, max_outer=None) -> SolveOutput:
-        """Run one solver to completion (or for ``max_outer`` outer steps)."""
+              profile=False, max_outer=None, nan_guard=None) -> SolveOutput:
+        """Run one solver to completion (or for ``max_outer`` outer steps).
+        nan_guard: stop at the first non-finite residual (default:
+        KRYLOV_AMD_NAN_GUARD, off = the reference's run-on semantics)."""
         torch = _torch()
         if not self._finalized:
             self.finalize()
         if method not in _lib.KR_METHOD:
             raise ValueError(f"unknown method {method!r}")
+        self._guard = nan_guard_default() if nan_guard is None else bool(nan_guard)
         prm = _lib.SolveParams(method=_lib.KR_METHOD[method], k=int(k or 0), tol=float(tol),
                                maxiter=-1 if maxiter is None else int(maxiter),
-                               profile=int(profile) if profile else 0)
+                               profile=int(profile) if profile else 0,
+                               nan_guard=int(self._guard))
         for s in range(self.nshards):
             torch.cuda.synchronize(self.device(s))
         b_arr = ptr_array([t.data_ptr() for t in b_parts])
@@ -347,13 +372,15 @@ class KrylovSystem:
         return self.finish(method)
 
     def begin(self, method, b_parts, x0_parts=None, tol=1e-5, maxiter=None, k=0,
-              profile=False) -> None:
+              profile=False, nan_guard=None) -> None:
         torch = _torch()
         if not self._finalized:
             self.finalize()
+        self._guard = nan_guard_default() if nan_guard is None else bool(nan_guard)
         prm = _lib.SolveParams(method=_lib.KR_METHOD[method], k=int(k or 0), tol=float(tol),
                                maxiter=-1 if maxiter is None else int(maxiter),
-                               profile=int(profile) if profile else 0)
+                               profile=int(profile) if profile else 0,
+                               nan_guard=int(self._guard))
         for s in range(self.nshards):
             torch.cuda.synchronize(self.device(s))
         b_arr = ptr_array([t.data_ptr() for t in b_parts])
@@ -387,10 +414,12 @@ class KrylovSystem:
         info = {"time": float(res.time_s), "nosl": nosl, "residual": residual}
         if method == "adaptivekskipmrr":
             info["khistory"] = khist
+        if getattr(self, "_guard", False):  # only with the (non-reference) guard on
+            info["diverged"] = bool(res.diverged)
         return SolveOutput(x=xs, info=info, converged=bool(res.converged),
                            iterations=int(res.iterations), final_k=int(res.final_k),
                            final_residual=float(res.final_residual),
-                           kernel_stats=self.kernel_stats())
+                           kernel_stats=self.kernel_stats(), diverged=bool(res.diverged))
 
     def reset_kernel_stats(self) -> None:
         call("kr_solve_kernel_stats_reset", self.handle)

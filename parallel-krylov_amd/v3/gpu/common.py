@@ -100,6 +100,20 @@ class MultiGpu:
         return cls.system.gather(cls.system.spmv(parts))
 
 
+MRR_FAMILY = ("mrr", "kskipmrr", "adaptivekskipmrr")
+
+
+def check_maxiter(method: str, maxiter) -> None:
+    """maxiter = 0 (not None): CG and k-skip CG return the initial residual;
+    the MrR family takes its first step unconditionally and writes
+    ``num_of_solution_updates[1]`` of a length-1 array, an IndexError in the
+    reference (v3/gpu/mrr.py, v3/cpu/mrr.py:31, kskipmrr.py:32). Raised here,
+    after the banner, as the reference raises it."""
+    if maxiter is not None and int(maxiter) == 0 and method in MRR_FAMILY:
+        raise IndexError("index 1 is out of bounds for axis 0 with size 1 "
+                         f"({method} with maxiter=0, as in the reference)")
+
+
 def run(method: str, banner: str, A, b, x=None, tol=1e-05, maxiter=None, k=None):
     """Shared body of the five v3/gpu solver functions.
 
@@ -119,6 +133,7 @@ def run(method: str, banner: str, A, b, x=None, tol=1e-05, maxiter=None, k=None)
         x0_parts = sysm.split(_host_vector(x)) if (isinstance(x, np.ndarray) or _is_tensor(x)) \
             else None
         _start(banner, k)
+        check_maxiter(method, maxiter)
         out = sysm.solve(method, b_parts, x0_parts, tol=tol, maxiter=maxiter, k=k or 0)
         final_k = out.final_k if method == "adaptivekskipmrr" else None
         _finish(out.info["time"], out.converged, out.iterations, out.final_residual, final_k)

@@ -21,7 +21,7 @@ import numpy as np
 
 from ....system import Communicator, KrylovSystem, balanced_partition, gpu_ids_range, local_device
 from ...common import _finish, _start
-from ..common import _host_vector, _is_tensor
+from ..common import _host_vector, _is_tensor, check_maxiter
 
 _COMMS = {}
 
@@ -144,6 +144,7 @@ def run(method, banner, comm, local_A, b, x=None, tol=1e-05, maxiter=None, k=Non
                         for r0, r1, dv in zip(rows[:-1], rows[1:], dev_of)]
         if d.rank == 0:
             _start(banner, k)
+        check_maxiter(method, maxiter)
         out = sysm.solve(method, b_parts, x0_parts, tol=tol, maxiter=maxiter, k=k or 0)
         x_local = torch.cat([xs.to(dev_of[0]) for xs in out.x])
         x_full = d.gather_x(x_local, counts)

@@ -1,7 +1,8 @@
 """bench.py pieces that run without a GPU: the headline metric string is
 BASELINE.json's, the configs match BASELINE.json's list, the CPU-baseline leg
 (the oracle, bitwise the reference's v3/cpu) produces the cpu_baseline object,
-and the PMC traffic lookup reads profiles/latest.json."""
+the PMC traffic lookup reads profiles/pmc/<config>.json keyed by (config,
+kernel), and the full-size parity check compares history entries."""
 import json
 import os
 
@@ -29,11 +30,31 @@ def test_cpu_baseline_object_small_sample():
 
 def test_pmc_traffic_from_committed_profile():
     import bench
-    with open(os.path.join(REPO, "profiles", "latest.json")) as f:
+    with open(os.path.join(REPO, "profiles", "pmc", "C4.json")) as f:
         prof = json.load(f)
-    t = bench.pmc_traffic("spmv2_gram_mrr")
-    assert t == prof["spmv2_gram_mrr"]["traffic_bytes"] and t > 1e9
-    assert bench.pmc_traffic("no_such_kernel") is None
+    assert prof["_meta"]["config"] == "C4"
+    t = bench.pmc_traffic("C4", "spmv2_gram_mrr")
+    assert t == prof["kernels"]["spmv2_gram_mrr"]["traffic_bytes"] and t > 1e9
+    assert bench.pmc_traffic("C4", "no_such_kernel") is None
+    # another config never borrows C4's bytes
+    assert bench.pmc_traffic("C1", "spmv2_gram_mrr") is None
+    assert bench.pmc_traffic("C5", "spmv2_gram_mrr") is None or \
+        bench.pmc_traffic("C5", "spmv2_gram_mrr") != t
+
+
+def test_history_parity_contract():
+    """bench `parity`: nosl equal and entries >= 1e-8 within 1e-12 relative."""
+    import numpy as np
+    import bench
+    ref = {"nosl": np.array([0, 1, 6]), "residual": np.array([1.0, 0.5, 0.25])}
+    gpu = {"nosl": np.array([0, 1, 6, 11]), "residual": np.array([1.0, 0.5 * (1 + 1e-13), 0.25, 0.1])}
+    p = bench.history_parity(gpu, ref)
+    assert p["ok"] and p["entries"] == 3 and p["max_rel"] < 1e-12
+    gpu["residual"][2] = 0.25 * (1 + 1e-10)
+    assert not bench.history_parity(gpu, ref)["ok"]
+    gpu["residual"][2] = 0.25
+    gpu["nosl"][2] = 5
+    assert not bench.history_parity(gpu, ref)["ok"]
 
 
 def test_stored_format_bytes():

@@ -205,3 +205,19 @@ def test_gpu_ids_range_rejects_descending(monkeypatch):
     monkeypatch.setenv("GPU_IDS", "3,1")
     with pytest.raises(ValueError):
         gpu_ids_range()
+
+
+def test_local_device_gpu_ids_wins_over_local_rank(monkeypatch):
+    """GPU_IDS (set per process by the launcher, as the reference's MPI family
+    reads it) picks the rank's device even under torchrun's LOCAL_RANK."""
+    from parallel_krylov_amd import system
+    monkeypatch.setattr(system._lib, "device_count", lambda: 8)
+    monkeypatch.setenv("LOCAL_RANK", "1")
+    monkeypatch.setenv("GPU_IDS", "3")
+    assert system.local_device(1) == 3
+    monkeypatch.setenv("GPU_IDS", "4,5")
+    assert system.local_device(0) == 4
+    monkeypatch.delenv("GPU_IDS")
+    assert system.local_device(0) == 1
+    monkeypatch.delenv("LOCAL_RANK")
+    assert system.local_device(10) == 2

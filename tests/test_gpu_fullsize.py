@@ -1,0 +1,77 @@
+"""Parity at BASELINE.json's full sizes (MI355X).
+
+C2 and C3 against the oracle on the SAME system (device generators =
+oracle/matrices.py integer for integer, b = the device counter hash =
+matrices.rhs bitwise), a few iterations each (the oracle needs ~5-40 s per
+case on the host): SURVEY.md §8(c) contract for CG / MrR -- nosl identical,
+every residual entry within 1e-12 relative, x within 1e-12 relative.
+
+C5 (N = 50M, 63 nnz/row; the oracle would need ~40 GB of host CSR) is checked
+through a size-independent property: after a few adaptive outer iterations the
+reported residual equals ||b - A x|| / ||b|| recomputed from the returned x.
+C4 at 512^3 is compared with the oracle inside bench.py (`parity` field of
+the headline line, from the same run as the CPU baseline).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _system(matrix):
+    from parallel_krylov_amd.system import KrylovSystem
+    if matrix[0] == "poisson":
+        n = matrix[1] ** matrix[2]
+        sysm = KrylovSystem(n, [0, n], [0])
+        sysm.gen_poisson(matrix[1], matrix[2])
+    else:
+        n = matrix[1]
+        sysm = KrylovSystem(n, [0, n], [0])
+        sysm.gen_banded(matrix[2], matrix[3], matrix[4])
+    sysm.finalize()
+    return sysm, n
+
+
+def _oracle_matrix(matrix):
+    from oracle import matrices
+    if matrix[0] == "poisson":
+        return matrices.poisson(matrix[1], matrix[2])
+    return matrices.banded(*matrix[1:])
+
+
+@pytest.mark.parametrize("name,method,matrix,maxiter", [
+    ("C2", "cg", ["poisson", 256, 3], 10),
+    ("C3", "mrr", ["banded", 10_000_000, 13, 64, 0], 5),
+])
+def test_fullsize_matches_oracle(name, method, matrix, maxiter):
+    from oracle import matrices, v3cpu
+    sysm, n = _system(matrix)
+    b = sysm.rhs(1)
+    out = sysm.solve(method, b, tol=0.0, maxiter=maxiter)
+    x = out.x[0].cpu().numpy()
+    info = out.info
+    sysm.close()
+    A = _oracle_matrix(matrix)
+    bh = matrices.rhs(n, 1)
+    np.testing.assert_array_equal(b[0].cpu().numpy(), bh)  # the same b
+    x_ref, ref = v3cpu.METHODS[method](A, bh, tol=0.0, maxiter=maxiter)
+    np.testing.assert_array_equal(info["nosl"], ref["nosl"])
+    rel = np.abs(info["residual"] - ref["residual"]) / np.abs(ref["residual"])
+    assert rel.max() <= 1e-12, (name, rel)
+    assert np.linalg.norm(x - x_ref) <= 1e-12 * np.linalg.norm(x_ref)
+
+
+def test_c5_fullsize_true_residual():
+    """C5: adaptive k-skip MrR k=4 on the N=50M, h=31 (63 nnz/row) banded
+    system for 3 outer iterations; the reported residual equals the true
+    relative residual of the returned x."""
+    sysm, n = _system(["banded", 50_000_000, 31, 256, 0])
+    b = sysm.rhs(1)
+    out = sysm.solve("adaptivekskipmrr", b, tol=0.0, maxiter=12, k=4)
+    assert list(out.info["nosl"]) == [0, 1, 6, 11, 16]
+    r = sysm.spmv(out.x)[0]
+    true_rel = float(((b[0] - r).norm() / b[0].norm()).item())
+    rep = float(out.info["residual"][-1])
+    assert rep < out.info["residual"][0]
+    assert abs(true_rel - rep) <= 1e-9 * rep
+    sysm.close()

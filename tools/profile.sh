@@ -4,8 +4,11 @@
 #   2.. one PMC group per pass            (TCC slots are scarce; separate runs)
 # then tools/pmc_summary.py writes gpurun_out/<tag>/summary.json.
 # Usage: bash tools/profile.sh <tag> [bench args...]
+# One config per call (kernel names must be unique per profile): the bench
+# args default to the C4 headline without its plain-CSR sub-run; profile the
+# CSR format with `KR_MASK=0 KR_VDICT=0 bash tools/profile.sh <tag>`.
 tag=${1:-prof}; shift
-args=${@:---steps 5 --warmup 1 --no-cpu-baseline}
+args=${@:---steps 5 --warmup 1 --no-cpu-baseline --no-csr}
 out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
