@@ -141,7 +141,10 @@ def stored_format_delta(nnz, n, lay, long_row=12.0):
     the bytes the shard's stored format streams for the same SpMV: offset
     masks replace the 4-byte columns by mw/8 bytes per row, a value
     dictionary the 8-byte values by 1-byte codes; long masked rows use the
-    diagonal-offset values (8 bytes per offset and row, no rowptr)."""
+    diagonal-offset values (8 bytes per offset and row, no rowptr); the
+    stencil SpMV streams one uint64 of codes per row and nothing else of A."""
+    if lay.get("stencil_walk"):
+        return 12.0 * nnz + 4.0 * (n + 1) - 8.0 * n
     mw = lay["mask_bits"]
     if mw and lay["dict_values"] == 0 and nnz >= long_row * n:  # DIA (KR_DIA=1)
         n_pad = -(-n // 256) * 256
@@ -155,6 +158,9 @@ def stored_format_delta(nnz, n, lay, long_row=12.0):
 
 
 def format_name(lay):
+    if lay.get("stencil_walk"):
+        return (f"stencil codes (8 x 1-byte dictionary codes per row, "
+                f"{lay['dict_values']}-entry table; walk {lay['stencil_walk']} blocks)")
     parts = [f"offset masks ({lay['mask_bits']}-bit)" if lay["mask_bits"] else "CSR columns"]
     parts.append(f"{lay['dict_values']}-entry value dictionary (1-byte codes)"
                  if lay["dict_values"] else "8-byte values")
@@ -205,6 +211,7 @@ def run_system(args, cfg, mat, n, world, rank, local, comm, method, k, env=None)
                 os.environ[key] = v
     info = sysm.shard_info(0)
     lay = sysm.shard_layout(0)
+    lay["stencil_walk"] = sysm.shard_sched(0)["stencil_walk"]
     b = sysm.rhs(1)
     per_step = (k + 1) if "kskip" in method else 1
     maxiter = (args.warmup + args.steps + 4) * per_step + 2
@@ -316,11 +323,11 @@ def main():
     csr_rec = None
     if not args.no_csr and (lay["mask_bits"] or lay["dict_values"]):
         rc = run_system(args, cfg, mat, n, world, rank, local, comm, method, k,
-                        env={"KR_MASK": "0", "KR_VDICT": "0"})
+                        env={"KR_MASK": "0", "KR_VDICT": "0", "KR_STENCIL": "0"})
         kc, _ = kernel_table(rc["stats"], 0.0)
         csr_rec = dict(value=round(iterations / rc["elapsed"], 3), unit="iterations/s",
                        ms_per_step=round(rc["elapsed"] / args.steps * 1e3, 4),
-                       format=format_name(rc["lay"]), env="KR_MASK=0 KR_VDICT=0")
+                       format=format_name(rc["lay"]), env="KR_MASK=0 KR_VDICT=0 KR_STENCIL=0")
         if kc:
             dc = dominant(kc)
             csr_rec.update(kernel=dc, avg_ms=kc[dc]["avg_ms"], achieved=kc[dc]["gbs"],

@@ -225,12 +225,16 @@ int kr_system_shard_layout(kr_system* sys, int shard, int* mask_bits, int* n_off
  * v3/gpu/common.py:119 always streams 8-byte values. */
 int kr_system_shard_values(kr_system* sys, int shard, int* dict_values);
 /* Launch geometry of shard s (after finalize): grid = workgroups of the
- * elementwise kernels, spmv_grid = workgroups of the SpMV kernels. Together
- * with the interior range of kr_system_shard_layout they fix the summation
- * order of every dot product (oracle/gpu_order.py restates it
- * for the bitwise GPU-order parity tests). Replaces nothing in the
- * reference (cuBLAS ddot's order is internal). Pointers may be NULL. */
-int kr_system_shard_sched(kr_system* sys, int shard, int* grid, int* spmv_grid);
+ * elementwise kernels, spmv_grid = workgroups of the SpMV kernels,
+ * stencil_walk = 0 for the row-walk SpMV (256-row blocks, one row per lane)
+ * or P > 0 for the stencil SpMV (512-row blocks, two rows per lane, walking
+ * P blocks per step). Together with the interior range of
+ * kr_system_shard_layout they fix the summation order of every dot product
+ * (oracle/gpu_order.py restates it for the bitwise GPU-order parity tests).
+ * Replaces nothing in the reference (cuBLAS ddot's order is internal).
+ * Pointers may be NULL. */
+int kr_system_shard_sched(kr_system* sys, int shard, int* grid, int* spmv_grid,
+                          int* stencil_walk);
 
 /* Halo exchange plan (pure host arithmetic, no device; test hook and the
  * planner kr_system_finalize uses). part[0..nshards] is the global row

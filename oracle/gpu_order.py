@@ -16,10 +16,14 @@ nosl, khistory, every residual entry and x -- through every rollback.
 What is restated (single process; shards in shard order, RCCL ranks in rank
 order, as System::reduce and scalar_kernel sum them):
 
-* SpMV epilogue products (kr_spmv.h ``epi_products``): lane ``tid`` of
-  workgroup ``b`` owns rows ``rb*256 + tid`` of the row blocks RowSched gives
-  it (XCD-aware when the grid is a multiple of 8, kr_spmv.h RowSched::init)
-  and accumulates ``acc = acc + p[row]`` from 0.0 in visit order;
+* SpMV epilogue products (kr_spmv.h ``epi_products``), row-walk kernels:
+  lane ``tid`` of workgroup ``b`` owns rows ``rb*256 + tid`` of the row
+  blocks RowSched gives it (XCD-aware when the grid is a multiple of 8,
+  kr_spmv.h RowSched::init) and accumulates ``acc = acc + p[row]`` from 0.0
+  in visit order. Stencil kernel (kr_stencil.h, shards with stencil codes):
+  512-row blocks, lane ``tid`` owns rows ``2 tid`` and ``2 tid + 1`` and
+  adds them in that order; workgroup (XCD q, plane segment s, position p)
+  visits the blocks z*P + p of its planes;
   ``block_reduce_store`` folds each wave with the ``__shfl_down`` tree
   (offsets 32..1) and the 4 waves as ``((w0 + w1) + w2) + w3``. A sharded
   system splits each SpMV into an interior launch and one boundary launch that
@@ -54,13 +58,46 @@ class ShardSched:
     spmv_grid: int   # SpMV workgroups (spmv_grid_for)
     int_lo: int = 0  # interior rows [int_lo, int_hi) of the split SpMV
     int_hi: int = 0
+    stencil_walk: int = 0  # P > 0: the stencil SpMV (512-row blocks), 0: row walk
+
+
+def _stencil_walk(blk, r0, nnz_row_mean):
+    """kr_engine.cpp build_masks / build_vdict / build_stencil: P of the
+    stencil SpMV for this row block, or 0 (row walk)."""
+    n = blk.shape[0]
+    if n < 2 or n % 2 or nnz_row_mean >= 12.0 or blk.nnz < 8:
+        return 0
+    rows = np.repeat(np.arange(n), np.diff(blk.indptr))
+    offs = np.unique(blk.indices.astype(np.int64) - (r0 + rows))
+    if offs.size == 0 or offs.size > 8:
+        return 0
+    if np.unique(blk.data.view(np.uint64)).size > 255:
+        return 0
+    W = max([int(o) for o in offs if o > 0 and o % 512 == 0 and -o in offs], default=0)
+    if W == 0:
+        return 0
+    far = [int(o) for o in offs if o not in (0, W, -W) and abs(o) > 2]
+    if len(far) > 4 or any(o % 2 for o in far):
+        return 0
+    return W // 512
+
+
+def stencil_grid(rows, P):
+    """kr_engine.cpp stencil_grid: 8 XCDs x P positions x Z plane segments."""
+    nrb = -(-rows // 512)
+    planes = -(-nrb // P)
+    Z = 1
+    while 8 * P * Z < 2048 and planes // (8 * Z * 2) >= 8:
+        Z *= 2
+    return 8 * P * Z
 
 
 def shard_scheds(A, part, cus: int = 256):
     """The launch geometry kr_system_finalize gives the row blocks part[s]..
-    part[s+1] of A (kr_engine.cpp default_grid / spmv_grid_for / interior
-    rows; MI355X: 256 CUs x 8 workgroups). The GPU tests read the engine's
-    own values (KrylovSystem.shard_sched) and check them against this."""
+    part[s+1] of A (kr_engine.cpp default_grid / spmv_grid_for /
+    stencil_grid / interior rows; MI355X: 256 CUs x 8 workgroups). The GPU
+    tests read the engine's own values (KrylovSystem.shard_sched) and check
+    them against this."""
     import scipy.sparse as sp
     A = sp.csr_matrix(A)
     cap = cus * 8
@@ -80,14 +117,21 @@ def shard_scheds(A, part, cus: int = 256):
         int_hi = max(h1 // BLOCK * BLOCK, int_lo)
         nrb = max(1, -(-n // BLOCK))
         base = min(nrb, cap)
-        rb = -(-reach // BLOCK)
-        if rb * 8 <= base or rb * 8 > cap * 8 or rb * 8 > nrb:
-            g = base
+        P = _stencil_walk(blk, r0, blk.nnz / max(n, 1))
+        if P:
+            int_lo = min(-(-int_lo // 512) * 512, n)
+            int_hi = max(int_hi // 512 * 512, int_lo)
+            g = stencil_grid(n, P)
         else:
-            g = rb * 8
-            while g // 2 >= base and g > nrb // 16 and (g // 2) % 8 == 0:
-                g //= 2
-        out.append(ShardSched(n=n, grid=base, spmv_grid=g, int_lo=int_lo, int_hi=int_hi))
+            rb = -(-reach // BLOCK)
+            if rb * 8 <= base or rb * 8 > cap * 8 or rb * 8 > nrb:
+                g = base
+            else:
+                g = rb * 8
+                while g // 2 >= base and g > nrb // 16 and (g // 2) % 8 == 0:
+                    g //= 2
+        out.append(ShardSched(n=n, grid=base, spmv_grid=g, int_lo=int_lo, int_hi=int_hi,
+                              stencil_walk=P))
     return out
 
 
@@ -131,10 +175,43 @@ def _block_total(acc):
     return np.float64(t)
 
 
-def _launch_partials(p, rows, grid, gap_at=0, gap=0):
+def _visits_stencil(rows: int, grid: int, P: int, gap_at: int = 0, gap: int = 0):
+    """512-row blocks each workgroup of the stencil SpMV visits, in order
+    (kr_stencil.h: XCD q = b & 7, position p and plane segment s of b >> 3)."""
+    nrb = -(-rows // 512) - gap
+    planes = -(-nrb // P)
+    Z = grid // (8 * P)
+    out = []
+    for b in range(grid):
+        q, w = b & 7, b >> 3
+        p, zs = w % P, w // P
+        pl0 = planes * q // 8
+        npl = planes * (q + 1) // 8 - pl0
+        z0, z1 = pl0 + npl * zs // Z, pl0 + npl * (zs + 1) // Z
+        vis = []
+        for z in range(z0, z1):
+            v = z * P + p
+            if v >= nrb:
+                break
+            vis.append(v if v < gap_at else v + gap)
+        out.append(vis)
+    return out
+
+
+def _launch_partials(p, rows, grid, gap_at=0, gap=0, P=0):
     """Per-workgroup partials of one SpMV launch over products p[0:rows]."""
     out = np.zeros(grid, np.float64)
     lanes = np.arange(BLOCK)
+    if P:
+        for b, vis in enumerate(_visits_stencil(rows, grid, P, gap_at, gap)):
+            acc = np.zeros(BLOCK, np.float64)
+            for rb in vis:
+                lo = rb * 512 + 2 * lanes
+                act = lo < rows  # rows is even: both rows of a pair or neither
+                acc[act] = acc[act] + p[lo[act]]
+                acc[act] = acc[act] + p[lo[act] + 1]
+            out[b] = _block_total(acc)
+        return out
     for b, vis in enumerate(_visits(rows, grid, gap_at, gap)):
         acc = np.zeros(BLOCK, np.float64)
         for rb in vis:
@@ -156,15 +233,17 @@ def finalize(partials):
 
 def spmv_shard_total(p, s: ShardSched, split: bool):
     """One shard's total of the epilogue products p (length s.n)."""
+    P = s.stencil_walk
     if not split:
-        return finalize(_launch_partials(p, s.n, s.spmv_grid))
-    part = _launch_partials(p[s.int_lo:s.int_hi], s.int_hi - s.int_lo, s.spmv_grid)
-    nb_lo = s.int_lo // BLOCK
-    nb_gap = (s.int_hi - s.int_lo) // BLOCK
-    nb_all = -(-s.n // BLOCK)
+        return finalize(_launch_partials(p, s.n, s.spmv_grid, P=P))
+    part = _launch_partials(p[s.int_lo:s.int_hi], s.int_hi - s.int_lo, s.spmv_grid, P=P)
+    rbs = 512 if P else BLOCK
+    nb_lo = s.int_lo // rbs
+    nb_gap = (s.int_hi - s.int_lo) // rbs
+    nb_all = -(-s.n // rbs)
     if nb_all - nb_gap > 0:
-        g = min(s.spmv_grid, nb_all - nb_gap)
-        bnd = _launch_partials(p, s.n, g, nb_lo, nb_gap)
+        g = 8 * P if P else min(s.spmv_grid, nb_all - nb_gap)
+        bnd = _launch_partials(p, s.n, g, nb_lo, nb_gap, P=P)
         part[:g] = part[:g] + bnd
     return finalize(part)
 

@@ -282,6 +282,84 @@ void System::build_masks(Shard& s) {
   s.moff = dM;
   s.nm = nm;
   s.mw = mw;
+  s.moff_h = M;
+}
+
+// Stencil codes (kr_stencil.h) for masked short-row blocks with a value
+// dictionary whose offsets hold a +-W pair with W a multiple of 512 rows
+// (3-D stencils: W = n^2), at most 8 offsets, other offsets within +-2 rows
+// (LDS line) or even (one 16-byte load each, at most 4), and an even number
+// of rows. Every row then streams 8 bytes (its codes); x[row - W] and x[row]
+// are carried along the walk. KR_STENCIL=0 keeps the row walk (A/B).
+void System::build_stencil(Shard& s) {
+  const char* env = getenv("KR_STENCIL");
+  if (env && atoi(env) == 0) return;
+  if (!s.mask || s.dia || !s.vcode || s.ntab > 255 || s.nm > 8 || s.n < 2 || (s.n & 1) ||
+      (s.pad & 1))
+    return;
+  const auto& M = s.moff_h;
+  int64_t W = 0;
+  for (int32_t o : M)
+    if (o > 0 && o % kStencilBlock == 0 && std::find(M.begin(), M.end(), -o) != M.end())
+      W = std::max<int64_t>(W, o);
+  if (W == 0) return;
+  int nfar = 0;
+  int32_t kind[8] = {}, far[4] = {};
+  for (int k = 0; k < s.nm; ++k) {
+    const int32_t o = M[k];
+    if (o == 0) {
+      kind[k] = 0;  // SK_CENTER
+    } else if (o == -W) {
+      kind[k] = 1;  // SK_PREV
+    } else if (o == W) {
+      kind[k] = 2;  // SK_NEXT
+    } else if (o >= -2 && o <= 2) {
+      kind[k] = 3;  // SK_NEAR (kSNear = 2)
+    } else {
+      if ((o & 1) || nfar == 4) return;
+      far[nfar] = o;
+      kind[k] = 4 + nfar++;  // SK_FAR + f
+    }
+  }
+  uint64_t* code = nullptr;
+  double* scratch = nullptr;
+  if (hipMalloc(&code, sizeof(uint64_t) * (size_t)s.n) != hipSuccess ||
+      hipMalloc(&scratch, 64 * sizeof(double)) != hipSuccess) {
+    (void)hipGetLastError();
+    if (code) (void)hipFree(code);
+    return;  // no room: keep the row walk
+  }
+  s.owned.push_back(code);
+  s.owned.push_back(scratch);
+  s.scratch = scratch;
+  launch_stencil_codes(s.rowptr, s.rowptr64, s.n, s.col, s.vcode, s.pad, s.moff, s.nm, code,
+                       s.stream);
+  KR_HIP_CHECK(hipStreamSynchronize(s.stream));
+  s.scode = code;
+  s.st_P = (int)(W / kStencilBlock);
+  s.st_nfar = nfar;
+  for (int k = 0; k < 8; ++k) s.st_kind[k] = kind[k];
+  for (int f = 0; f < 4; ++f) s.st_far[f] = far[f];
+  // the split SpMV's launches start on stencil row blocks
+  s.int_lo = std::min<int64_t>((s.int_lo + kStencilBlock - 1) / kStencilBlock * kStencilBlock, s.n);
+  s.int_hi = std::max<int64_t>(s.int_hi / kStencilBlock * kStencilBlock, s.int_lo);
+}
+
+// Stencil SpMV grid: 8 XCDs x P positions x Z plane segments (every
+// workgroup walks its position through a run of consecutive planes). More
+// segments give more workgroups but cost a reload of CENTER and PREV at each
+// segment start: at least 8 planes per segment, about 2048 workgroups.
+int stencil_grid(int64_t rows, int P) {
+  const int64_t nrb = (rows + kStencilBlock - 1) / kStencilBlock;
+  const int64_t planes = (nrb + P - 1) / P;
+  int64_t Z = 1;
+  const char* env = getenv("KR_STENCIL_Z");
+  if (env && atoi(env) > 0) {
+    Z = atoi(env);
+  } else {
+    while (8 * P * Z < 2048 && planes / (8 * Z * 2) >= 8) Z *= 2;
+  }
+  return (int)(8 * P * Z);
 }
 
 void System::build_vdict(Shard& s) {
@@ -474,13 +552,17 @@ void System::finalize() {
       // 6b. value dictionary for short-row blocks with <= 256 distinct values
       // (stencils): 1-byte codes instead of 8-byte values. KR_VDICT=0 disables.
       build_vdict(s);
+      // 6c. stencil codes (one uint64 per row) for 3-D-stencil blocks with a
+      // dictionary: the stencil SpMV (kr_stencil.h). KR_STENCIL=0 disables.
+      build_stencil(s);
     }
     // 7. reduction buffers
     s.grid = default_grid(s.n);
     // dense: one wave per row, 4 rows per workgroup
     s.spmv_grid = s.dense ? (int)std::max<int64_t>(1, std::min<int64_t>((s.n + 3) / 4,
                                                                          (int64_t)grid_cap() * 4))
-                          : spmv_grid_for(s.n, s.reach);
+                  : s.scode ? stencil_grid(s.n, s.st_P)
+                            : spmv_grid_for(s.n, s.reach);
     s.pstride = std::max(s.grid, s.spmv_grid);
     s.slot_n.fill(0);
     KR_HIP_CHECK(hipMalloc(&s.partials, sizeof(double) * (size_t)kMaxSlots * s.pstride));
@@ -767,6 +849,20 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
       a.vtab = s.vtab;
       a.ntab = s.ntab;
     }
+    if (s.scode) {
+      KR_REQUIRE(r_begin % kStencilBlock == 0, "stencil launch must start on a row block");
+      a.scode = s.scode + r_begin;
+      a.st_P = s.st_P;
+      a.st_nm = s.nm;
+      a.st_nfar = s.st_nfar;
+      for (int k = 0; k < 8; ++k) {
+        a.st_off[k] = k < s.nm ? s.moff_h[k] : 0;
+        a.st_kind[k] = s.st_kind[k];
+      }
+      for (int f = 0; f < 4; ++f) a.st_far[f] = s.st_far[f];
+      a.xlen = s.ld;
+      a.scratch = s.scratch;
+    }
     a.epi_late = epi_late;
     a.stop = dev_stop;
     a.nnz_total = s.nnz;
@@ -848,13 +944,16 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
     }
     // both boundary ranges in one launch: row blocks [0, int_lo/B) and
     // [int_hi/B, end) (interior bounds are whole blocks, see finalize)
-    const int64_t nb_lo = s.int_lo / kBlock, nb_gap = (s.int_hi - s.int_lo) / kBlock;
-    const int64_t nb_all = (s.n + kBlock - 1) / kBlock;
+    const int64_t rbs = s.scode ? kStencilBlock : kBlock;  // rows per row block
+    const int64_t nb_lo = s.int_lo / rbs, nb_gap = (s.int_hi - s.int_lo) / rbs;
+    const int64_t nb_all = (s.n + rbs - 1) / rbs;
     if (nb_all - nb_gap > 0) {
       SpmvArgs ab = args_for(s, 0, s.n, s.pstride, 1);
       ab.rb_gap_at = nb_lo;
       ab.rb_gap = nb_gap;
-      const int g = (int)std::min<int64_t>(s.spmv_grid, nb_all - nb_gap);
+      // stencil: one plane segment per XCD and position (8 * P workgroups)
+      const int g = s.scode ? 8 * s.st_P
+                            : (int)std::min<int64_t>(s.spmv_grid, nb_all - nb_gap);
       launch_spmv_grid(epi, ab, g, s.stream);
     }
     prof_end(s, nm, t0s[li], bytes_of(s));

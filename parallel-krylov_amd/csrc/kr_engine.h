@@ -88,6 +88,12 @@ struct Shard {
   double* vtab = nullptr;           // its table (<= kVdMax doubles), owned
   int ntab = 0;
   int64_t nz0 = 0;                  // rowptr[0]: index of the block's first stored entry
+  std::vector<int32_t> moff_h;      // host copy of the offset table (moff)
+  // stencil codes (SpmvArgs::scode, kr_stencil.h), owned; st_P = 0: not used
+  uint64_t* scode = nullptr;
+  double* scratch = nullptr;        // SpmvArgs::scratch (stencil SpMV), owned
+  int st_P = 0, st_nfar = 0;
+  int32_t st_kind[8] = {}, st_far[4] = {};
   hipStream_t comm_stream = nullptr;  // halo exchange, overlapped with interior rows
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   int grid = 1;                 // workgroups of the vector kernels
@@ -158,6 +164,7 @@ struct System {
   // Halo exchange of up to two vectors (ids), all shards.
   void build_masks(Shard& s);
   void build_vdict(Shard& s);
+  void build_stencil(Shard& s);
   void plan_window(Shard& s, const std::vector<int32_t>& M);
   void halo(int id1, int id2 = -1, int id3 = -1);
   // The same exchange on the shards' comm streams, ordered after ev_in and

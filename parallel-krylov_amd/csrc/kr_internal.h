@@ -139,7 +139,27 @@ struct SpmvArgs {
   const uint8_t* vcode = nullptr;
   const double* vtab = nullptr;
   int ntab = 0;
+  // Stencil codes (kr_stencil.h; optional, with vtab): scode[i] = the codes
+  // of row i's entries, byte k for offset st_off[k] (ascending), 0xFF = no
+  // entry. Rows are walked in 512-row blocks, st_P blocks per walk step
+  // (W = 512 * st_P rows = the +-W offsets); st_kind[k] = StencilKind of
+  // slot k; st_far[f] = the FAR offsets. Launch grids are multiples of
+  // 8 * st_P; rowptr, col, val, mask, vcode are not read.
+  const uint64_t* scode = nullptr;
+  int st_P = 0, st_nm = 0, st_nfar = 0;
+  int32_t st_off[8] = {};
+  int32_t st_kind[8] = {};
+  int32_t st_far[4] = {};
+  double* scratch = nullptr;  // >= 2 doubles, 16-byte aligned: stores of lanes past the last row
 };
+// Rows per row block of the stencil SpMV (2 per lane; kr_stencil.h).
+constexpr int kStencilBlock = 2 * kBlock;
+// Stencil codes of a masked CSR block (kr_stencil.h): out[i] = byte k =
+// vcode[j] of row i's entry at offset M[k] (local columns: base + i + M[k]),
+// 0xFF where row i has none. nm <= 8.
+void launch_stencil_codes(const void* rowptr, int rowptr64, int64_t n, const int32_t* col,
+                          const uint8_t* vcode, int64_t base, const int32_t* M, int nm,
+                          uint64_t* out, hipStream_t s);
 // Mean row length from which the product-then-sum SpMV is used.
 constexpr double kLongRow = 12.0;
 void launch_spmv(SpmvEpi epi, const SpmvArgs& a, hipStream_t s);

@@ -625,6 +625,29 @@ __global__ void dia_fill_kernel(const RP* rowptr, int64_t n, const int32_t* col,
   }
 }
 
+// Stencil codes (SpmvArgs::scode): byte k of out[i] = the dictionary code of
+// row i's entry at offset M[k], 0xFF where the row has none.
+template <typename RP>
+__global__ void stencil_codes_kernel(const RP* rowptr, int64_t n, const int32_t* col,
+                                     const uint8_t* vcode, int64_t base, const int32_t* M,
+                                     int nm, uint64_t* out) {
+  __shared__ int32_t sM[8];
+  if ((int)threadIdx.x < nm) sM[threadIdx.x] = M[threadIdx.x];
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t w = ~0ull;
+    for (int64_t j = (int64_t)rowptr[i]; j < (int64_t)rowptr[i + 1]; ++j) {
+      const int64_t off = (int64_t)col[j] - (base + i);
+      int b = 0;
+      while (b < nm - 1 && sM[b] != off) ++b;
+      w &= ~(0xFFull << (8 * b));
+      w |= (uint64_t)vcode[j] << (8 * b);
+    }
+    out[i] = w;
+  }
+}
+
 template <typename RP>
 __global__ void col_shift_kernel(const RP* rowptr, int64_t n, int32_t* col, int64_t delta) {
   const int64_t base = (int64_t)rowptr[0];
@@ -906,6 +929,21 @@ void launch_masks(const void* rowptr, int rowptr64, int64_t n, const int32_t* co
   else if (mw == 16) masks_typed<uint16_t>(rowptr, rowptr64, n, col, base, M, nm, mask, s);
   else if (mw == 32) masks_typed<uint32_t>(rowptr, rowptr64, n, col, base, M, nm, mask, s);
   else masks_typed<uint64_t>(rowptr, rowptr64, n, col, base, M, nm, mask, s);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_stencil_codes(const void* rowptr, int rowptr64, int64_t n, const int32_t* col,
+                          const uint8_t* vcode, int64_t base, const int32_t* M, int nm,
+                          uint64_t* out, hipStream_t s) {
+  KR_REQUIRE(nm >= 1 && nm <= 8, "stencil codes: 1..8 offsets");
+  if (n <= 0) return;
+  const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 65535);
+  if (rowptr64)
+    stencil_codes_kernel<int64_t><<<g, 256, 0, s>>>(static_cast<const int64_t*>(rowptr), n, col,
+                                                    vcode, base, M, nm, out);
+  else
+    stencil_codes_kernel<int32_t><<<g, 256, 0, s>>>(static_cast<const int32_t*>(rowptr), n, col,
+                                                    vcode, base, M, nm, out);
   KR_HIP_CHECK(hipGetLastError());
 }
 

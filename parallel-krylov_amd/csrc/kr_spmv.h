@@ -8,6 +8,7 @@
 #pragma once
 
 #include <cstdlib>
+#include <initializer_list>
 #include <type_traits>
 
 #include "kr_internal.h"
@@ -18,6 +19,8 @@ template <int E>
 void spmv_launch_epi(const SpmvArgs& a, int nblocks, hipStream_t s);
 
 namespace {
+
+typedef double dbl2v __attribute__((ext_vector_type(2)));
 
 // ---------------------------------------------------------------------------
 // Block-level deterministic reduction of NP per-thread accumulators into
@@ -220,14 +223,25 @@ __device__ __forceinline__ EpiIn epi_load(const SpmvArgs& a, int64_t row) {
   return in;
 }
 
+// The values one row's epilogue stores (statement for statement as above),
+// separated from the stores so the 2-rows-per-lane stencil kernel can store
+// row pairs as 16-byte accesses.
+struct EpiVals {
+  double y1 = 0, y2 = 0, u1 = 0, u2 = 0, ud = 0;
+};
 template <int EPI>
-__device__ __forceinline__ void epi_row_in(const SpmvArgs& a, int64_t row, double sum1,
-                                           double sum2, const double* __restrict__ x1,
-                                           const double* __restrict__ x2, const EpiIn& in,
-                                           double (&acc)[EpiTraits<EPI>::NP > 0
-                                                             ? EpiTraits<EPI>::NP
-                                                             : 1]) {
+constexpr bool epi_writes_ud() {
+  return EPI == EPI_STEP_MRR_X2 || EPI == EPI_STEP_MRR_X || EPI == EPI_STEP_MRR_FIRST2;
+}
+
+template <int EPI>
+__device__ __forceinline__ EpiVals epi_values(const SpmvArgs& a, double sum1, double sum2,
+                                              const EpiIn& in,
+                                              double (&acc)[EpiTraits<EPI>::NP > 0
+                                                                ? EpiTraits<EPI>::NP
+                                                                : 1]) {
   using T = EpiTraits<EPI>;
+  EpiVals o;
   if constexpr (EPI == EPI_STEP_MRR_FIRST2) {
     // step 0 at the own row (c0 = eta0, c1 = zeta0; x = r0, x2 = y0, e = Ar1,
     // u2 = z0), then step 1 (c2 = eta1, c3 = zeta1) with sum1 = (A r1)[row]
@@ -245,20 +259,20 @@ __device__ __forceinline__ void epi_row_in(const SpmvArgs& a, int64_t row, doubl
     const double s4 = a.c3 * r1;
     const double z2 = s3 - s4;
     const double xm = in.us - z1;  // x -= z of step 0, deferred
-    a.ud[row] = xm - z2;
-    a.u1[row] = y2;
-    a.u2[row] = z2;
-    a.y1[row] = r1 - y2;  // Ar0 of step 2
+    o.ud = xm - z2;
+    o.u1 = y2;
+    o.u2 = z2;
+    o.y1 = r1 - y2;  // Ar0 of step 2
   } else if constexpr (is_step<EPI>()) {
     const double xv = in.x;
     if constexpr (EPI == EPI_STEP_KCG) {  // x = Ap0, sum1 = Ap1; u1 = x, u2 = Ar0
       const double a0 = a.c0 * xv;
       const double a1 = a.c0 * sum1;
-      a.u1[row] = in.u1 + a0;
+      o.u1 = in.u1 + a0;
       const double r = in.u2 - a1;
-      a.u2[row] = r;
+      o.u2 = r;
       const double bp = a.c1 * xv;
-      a.y1[row] = r + bp;  // Ap0 of the next step
+      o.y1 = r + bp;  // Ap0 of the next step
     } else {  // x = Ar0, sum1 = Ar1; u1 = Ay0, u2 = z; c0 = eta, c1 = zeta
       const double t1 = a.c0 * in.u1;
       const double t2 = a.c1 * sum1;
@@ -268,21 +282,65 @@ __device__ __forceinline__ void epi_row_in(const SpmvArgs& a, int64_t row, doubl
       const double z = t3 - t4;
       if constexpr (EPI == EPI_STEP_MRR_X2) {
         const double xm = in.us - in.u2;  // the deferred x -= z of the previous step
-        a.ud[row] = xm - z;
+        o.ud = xm - z;
       } else if constexpr (EPI == EPI_STEP_MRR_X) {
-        a.ud[row] = in.us - z;
+        o.ud = in.us - z;
       }
-      a.u1[row] = y;
-      a.u2[row] = z;
-      a.y1[row] = xv - y;  // Ar0 of the next step
+      o.u1 = y;
+      o.u2 = z;
+      o.y1 = xv - y;  // Ar0 of the next step
     }
   } else {
     double y1 = sum1;
     if constexpr (EPI == EPI_BMINUS) y1 = in.e - sum1;
-    a.y1[row] = y1;
-    if constexpr (T::NV == 2) a.y2[row] = sum2;
+    o.y1 = y1;
+    if constexpr (T::NV == 2) o.y2 = sum2;
     if constexpr (T::NP > 0) epi_products<EPI>(in.x, in.x2, y1, sum2, in.e, acc);
   }
+  return o;
+}
+
+template <int EPI>
+__device__ __forceinline__ void epi_store_row(const SpmvArgs& a, int64_t row, const EpiVals& o) {
+  if constexpr (is_step<EPI>()) {
+    if constexpr (epi_writes_ud<EPI>()) a.ud[row] = o.ud;
+    a.u1[row] = o.u1;
+    a.u2[row] = o.u2;
+    a.y1[row] = o.y1;
+  } else {
+    a.y1[row] = o.y1;
+    if constexpr (EpiTraits<EPI>::NV == 2) a.y2[row] = o.y2;
+  }
+}
+
+// Rows row, row + 1 (row even: own-row vectors are 16-byte aligned there);
+// ok = false sends the pair to SpmvArgs::scratch instead (lanes past the
+// last row store unconditionally, see kr_stencil.h).
+template <int EPI>
+__device__ __forceinline__ void epi_store_pair(const SpmvArgs& a, int64_t row, const EpiVals& lo,
+                                               const EpiVals& hi, bool ok = true) {
+  auto st2 = [&](double* p, double u, double v) {
+    *reinterpret_cast<dbl2v*>(ok ? p + row : a.scratch) = dbl2v{u, v};
+  };
+  if constexpr (is_step<EPI>()) {
+    if constexpr (epi_writes_ud<EPI>()) st2(a.ud, lo.ud, hi.ud);
+    st2(a.u1, lo.u1, hi.u1);
+    st2(a.u2, lo.u2, hi.u2);
+    st2(a.y1, lo.y1, hi.y1);
+  } else {
+    st2(a.y1, lo.y1, hi.y1);
+    if constexpr (EpiTraits<EPI>::NV == 2) st2(a.y2, lo.y2, hi.y2);
+  }
+}
+
+template <int EPI>
+__device__ __forceinline__ void epi_row_in(const SpmvArgs& a, int64_t row, double sum1,
+                                           double sum2, const double* __restrict__ x1,
+                                           const double* __restrict__ x2, const EpiIn& in,
+                                           double (&acc)[EpiTraits<EPI>::NP > 0
+                                                             ? EpiTraits<EPI>::NP
+                                                             : 1]) {
+  epi_store_row<EPI>(a, row, epi_values<EPI>(a, sum1, sum2, in, acc));
 }
 
 template <int EPI>
@@ -307,7 +365,6 @@ __device__ __forceinline__ void epi_row(const SpmvArgs& a, int64_t row, double s
 //   Grid-stride over row blocks; reductions accumulate per lane across row
 //   blocks and are reduced once per workgroup at the end.
 // ---------------------------------------------------------------------------
-typedef double dbl2v __attribute__((ext_vector_type(2)));
 typedef int int4v __attribute__((ext_vector_type(4)));
 constexpr int kSlots = kWindow / (4 * kBlock);
 // x gathers in flight per lane: 7 = one batch for 7-point rows (8 issued a
@@ -1756,6 +1813,8 @@ void spmv_dispatch_epi(const SpmvArgs& a, int nblocks, hipStream_t s) {
   }
 }
 
+#include "kr_stencil.h"
+
 }  // namespace
 
 // One epilogue's launcher: explicitly instantiated, one epilogue per object
@@ -1763,6 +1822,11 @@ void spmv_dispatch_epi(const SpmvArgs& a, int nblocks, hipStream_t s) {
 // parallel.
 template <int E>
 void spmv_launch_epi(const SpmvArgs& a, int nblocks, hipStream_t s) {
+  if (a.scode) {  // stencil codes (kr_stencil.h): 3-D stencils with a value dictionary
+    KR_REQUIRE(nblocks % (8 * a.st_P) == 0, "stencil SpMV: grid must be a multiple of 8 * P");
+    spmv_stencil_launch<E>(a, nblocks, s);
+    return;
+  }
   if (use_dia<E>(a)) {
     spmv_dia_launch<E>(a, nblocks, s);
     return;

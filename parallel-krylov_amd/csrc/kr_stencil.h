@@ -1,0 +1,410 @@
+// Stencil SpMV (gfx950): the short-row kernel for offset-structured matrices
+// with a value dictionary -- 3-D stencils such as the 512^3 / 256^3 Poisson
+// systems of C4 / C2. Included by kr_spmv.h (inside kr::{anon}).
+//
+// Why a second short-row kernel. The row walk (spmv_kernel2) is bound by
+// vector-memory ADDRESS work, not bytes (profiles/r01f/sq_ta_counters.txt:
+// TA busy ~83 %, 42 % issue stalls): per row it issues 7 8-byte x gathers
+// per input vector, two row-pointer loads, a mask and a code load, plus the
+// own-row operands. This kernel issues, per PAIR of rows and input vector,
+// about three 16-byte loads:
+//
+//  * Storage (SpmvArgs::scode): one uint64 per row = the dictionary codes of
+//    the row's entries, byte k for offset M[k] (M ascending), 0xFF = no entry.
+//    8 B/row instead of rowptr + mask + codes (12-13 B/row); no LDS staging.
+//  * 2 rows per lane, 512-row blocks: every own-row access (codes, x, y, the
+//    epilogue operands) is one 16-byte load/store per lane.
+//  * Walk: workgroup (XCD q, plane segment s, position p) visits the blocks
+//    p, p + P, p + 2P, ... of its planes (P = st_P blocks = W / 512 rows,
+//    W = the stencil's largest offset, +-n^2 for a 3-D stencil). The rows
+//    one walk step apart are the +-W neighbours, so x[row - W] (PREV) and
+//    x[row] (CENTER) are the CENTER and NEXT values of the previous visit,
+//    carried in registers: per visit only x[row + W] (NEXT) is new.
+//  * Offsets |o| <= kSNear (+-1) are read from an LDS line of the block's
+//    CENTER values (+ 2 edge values each side); any other offset (FAR: +-n)
+//    is one 16-byte load per lane (even offsets only; the host checks).
+//  * Software pipeline: the next visit's loads are issued before this
+//    visit's sums (vector loads complete in order, see spmv_kernel2), one
+//    workgroup barrier per visit (double-buffered line).
+//
+// Numerics: each row sums its entries in stored order (ascending offset =
+// ascending column) from 0.0 with separately rounded products: bitwise
+// scipy's csr_matvec, like every SpMV kernel here. The epilogue statements
+// are epi_values (shared with the row walks). Dot-product partials: lane t
+// adds row 2t's products, then row 2t+1's, visit after visit
+// (oracle/gpu_order.py restates this order).
+#pragma once
+
+constexpr int kSBlock = kStencilBlock;  // rows per stencil row block (2 per lane)
+constexpr int kSNear = 2;            // LDS line halo (offsets 0 < |o| <= kSNear)
+constexpr int kSLine = kSBlock + 2 * kSNear;
+constexpr int kSFarMax = 4;          // FAR offsets (one 16-byte load each)
+
+// Slot kinds (SpmvArgs::st_kind): the source of x[row + M[k]].
+enum StencilKind : int {
+  SK_CENTER = 0,  // o == 0: carried
+  SK_PREV = 1,    // o == -W: carried
+  SK_NEXT = 2,    // o == +W: loaded, carried to the next visit as CENTER
+  SK_NEAR = 3,    // 0 < |o| <= kSNear: LDS line
+  SK_FAR = 4,     // SK_FAR + f: FAR load f
+};
+
+// 16-byte load of x[i], x[i+1] (i even), clamped into [0, xlen - 2]: lanes
+// past the last row and neighbours past the vector ends read a valid pair
+// that is never used (their codes say 0xFF / the row is inactive).
+__device__ __forceinline__ dbl2v st_ld2(const double* __restrict__ x, int64_t i, int64_t xlen) {
+  i = min(max(i, (int64_t)0), xlen - 2);
+  return *reinterpret_cast<const dbl2v*>(x + i);
+}
+
+// x at (row + o) for both rows of the lane.
+struct SPair {
+  double lo, hi;
+};
+
+// One visit's prefetched loads.
+template <int NX, int NFAR>
+struct SStage {
+  uint64_t clo, chi;          // codes of rows 2t, 2t+1
+  dbl2v nxt[NX];              // x[row + W]
+  dbl2v far[NFAR > 0 ? NFAR : 1][NX];
+  dbl2v u1, u2, us, e;        // own-row epilogue operands (as the EPI needs)
+  dbl2v cen[NX], prv[NX];     // RELOAD: x[row], x[row - W]
+  dbl2v el[NX], er[NX];       // the line's edges x[r0-2..r0-1], x[r0+512..r0+513] (uniform)
+};
+
+// Uniform 16-byte load through the scalar cache (s_load_dwordx4: counted by
+// lgkmcnt, so it never lengthens a vector-memory wait). x is read-only while
+// the kernel runs. i even, clamped like st_ld2.
+__device__ __forceinline__ dbl2v st_ld2_uniform(const double* x, int64_t i, int64_t xlen) {
+  i = min(max(i, (int64_t)0), xlen - 2);
+  return load_uniform(reinterpret_cast<const dbl2v*>(x), i >> 1);
+}
+
+template <int EPI, bool RELOAD, int NX, int NFAR>
+__device__ __forceinline__ void st_issue(SStage<NX, NFAR>& st, const SpmvArgs& a,
+                                         const double* const (&xs)[3], int64_t row0, int64_t rr,
+                                         int tid) {
+  using T = EpiTraits<EPI>;
+  (void)tid;
+  const uint64_t* cp = a.scode + rr;
+  const auto c = *reinterpret_cast<const __attribute__((ext_vector_type(2))) uint64_t*>(cp);
+  st.clo = c.x;
+  st.chi = c.y;
+  const int64_t xi = a.xoff + rr;
+  const int64_t W = (int64_t)a.st_P * kSBlock;
+#pragma unroll
+  for (int v = 0; v < NX; ++v) st.nxt[v] = st_ld2(xs[v], xi + W, a.xlen);
+#pragma unroll
+  for (int f = 0; f < NFAR; ++f)
+#pragma unroll
+    for (int v = 0; v < NX; ++v) st.far[f][v] = st_ld2(xs[v], xi + a.st_far[f], a.xlen);
+  if constexpr (is_step<EPI>()) {
+    st.u1 = *reinterpret_cast<const dbl2v*>(a.u1 + rr);
+    st.u2 = *reinterpret_cast<const dbl2v*>(a.u2 + rr);
+    if constexpr (EPI == EPI_STEP_MRR_X2 || EPI == EPI_STEP_MRR_X || EPI == EPI_STEP_MRR_FIRST2)
+      st.us = *reinterpret_cast<const dbl2v*>(a.us + rr);
+  } else if constexpr (EPI == EPI_BMINUS) {
+    st.e = *reinterpret_cast<const dbl2v*>(a.b + rr);
+  } else if constexpr (T::kE) {
+    st.e = *reinterpret_cast<const dbl2v*>(a.e + rr);
+  }
+  if constexpr (RELOAD) {
+#pragma unroll
+    for (int v = 0; v < NX; ++v) {
+      st.cen[v] = st_ld2(xs[v], xi, a.xlen);
+      st.prv[v] = st_ld2(xs[v], xi - W, a.xlen);
+    }
+  }
+}
+
+// The line's edge pairs (uniform: scalar loads, counted by lgkmcnt). Issued
+// after the visit's barrier, whose lgkmcnt(0) would otherwise wait for them.
+template <int NX, int NFAR>
+__device__ __forceinline__ void st_issue_edges(SStage<NX, NFAR>& st, const SpmvArgs& a,
+                                               const double* const (&xs)[3], int64_t row0) {
+#pragma unroll
+  for (int v = 0; v < NX; ++v) {
+    st.el[v] = st_ld2_uniform(xs[v], a.xoff + row0 - kSNear, a.xlen);
+    st.er[v] = st_ld2_uniform(xs[v], a.xoff + row0 + kSBlock, a.xlen);
+  }
+}
+
+// Own-row epilogue of one row from the carried centers (x, x2 / r0, y0, Ar1)
+// and the staged operands: the values epi_row_in stores, without the loads.
+template <int EPI>
+__device__ __forceinline__ EpiIn st_epi_in(double c0, double c1, double c2, double u1, double u2,
+                                           double us, double e) {
+  EpiIn in;
+  in.x = c0;
+  in.x2 = c1;
+  if constexpr (is_step<EPI>()) {
+    in.u1 = u1;
+    in.u2 = u2;
+    in.us = us;
+    if constexpr (EPI == EPI_STEP_MRR_FIRST2) in.e = c2;
+  } else {
+    in.e = e;
+  }
+  return in;
+}
+
+// Slot-kind patterns known at compile time (PAT != 0): 4 bits per slot,
+// the slot count in bits 28-31. The 3-D 7-point stencil (offsets -W, -n, -1,
+// 0, +1, +n, +W) is the C2 / C4 pattern; any other offset set runs the
+// kernel with PAT = 0, which reads st_kind at run time.
+constexpr uint32_t st_pat(int nm, std::initializer_list<int> kinds) {
+  uint32_t p = (uint32_t)nm << 28;
+  int k = 0;
+  for (int v : kinds) p |= (uint32_t)v << (4 * k++);
+  return p;
+}
+constexpr uint32_t kPat7 =
+    st_pat(7, {SK_PREV, SK_FAR + 0, SK_NEAR, SK_CENTER, SK_NEAR, SK_FAR + 1, SK_NEXT});
+
+// RELOAD: every visit loads its CENTER and PREV (launches whose walk crosses
+// a row-block gap: the boundary launch of a split SpMV); otherwise they are
+// loaded once per plane segment, before the loop, and carried.
+template <int EPI, int NFAR, uint32_t PAT, bool RELOAD>
+__global__ __launch_bounds__(kBlock) void spmv_stencil_kernel(SpmvArgs a) {
+  if (a.stop && *a.stop != 0.0) return;  // converged (device-resident scalars)
+  using T = EpiTraits<EPI>;
+  constexpr int NP = T::NP;
+  constexpr int NV = T::NV;                    // sums (input vectors of the SpMV)
+  constexpr bool VIRT = is_virtual<EPI>();     // operand r1 formed from x1, x2, x3
+  constexpr int NX = VIRT ? 3 : NV;            // physical input vectors
+  __shared__ double s_red[(NP > 0 ? NP : 1) * 4];
+  __shared__ double s_tab[kVdMax];
+  __shared__ __attribute__((aligned(16))) double s_line[2][NV][kSLine];
+  const int tid = threadIdx.x;
+  if (tid < a.ntab) s_tab[tid] = a.vtab[tid];
+
+  double acc[NP > 0 ? NP : 1];
+#pragma unroll
+  for (int q = 0; q < (NP > 0 ? NP : 1); ++q) acc[q] = 0.0;
+
+  // ---- the walk: blocks v = z * P + p for the planes z of this segment
+  const int64_t P = a.st_P;
+  const int64_t W = P * kSBlock;
+  const int64_t nrb = (a.n + kSBlock - 1) / kSBlock - a.rb_gap;
+  const int64_t planes = (nrb + P - 1) / P;
+  const int64_t Z = gridDim.x / (8 * P);
+  const int64_t q = blockIdx.x & 7;
+  const int64_t w = blockIdx.x >> 3;
+  const int64_t p = w % P, zs = w / P;
+  const int64_t pl0 = planes * q / 8, npl = planes * (q + 1) / 8 - pl0;
+  const int64_t z0 = pl0 + npl * zs / Z, z1 = pl0 + npl * (zs + 1) / Z;
+  auto phys = [&](int64_t v) { return v < a.rb_gap_at ? v : v + a.rb_gap; };
+  auto visit_ok = [&](int64_t z) { return z < z1 && z * P + p < nrb; };
+  constexpr int NM_C = PAT ? (int)(PAT >> 28) : 8;
+  const int nm = PAT ? NM_C : a.st_nm;
+
+  const double* const xs[3] = {a.x1, a.x2, a.x3};
+  dbl2v cen[NX], prv[NX];  // carried: x at the rows, x at the rows - W
+  SStage<NX, NFAR> sA, sB;
+  int buf = 0;
+  auto issue = [&](SStage<NX, NFAR>& st, int64_t z) {
+    const int64_t rb = phys(z * P + p);
+    const int64_t rl = rb * kSBlock + 2 * tid;
+    st_issue<EPI, RELOAD>(st, a, xs, rb * kSBlock, rl < a.n ? rl : a.n - 2, tid);
+  };
+  auto issue_edges = [&](SStage<NX, NFAR>& st, int64_t z) {
+    st_issue_edges(st, a, xs, phys(z * P + p) * kSBlock);
+  };
+
+  // One visit: `cur` holds its loads (issued one visit earlier); the next
+  // visit's loads go to `nxs` before anything here waits. The loop below
+  // alternates the two stage register sets, so nothing copies a register a
+  // load is still writing (a copy would wait for it).
+  auto visit = [&](SStage<NX, NFAR>& cur, SStage<NX, NFAR>& nxs, int64_t z) {
+    const int64_t rb = phys(z * P + p);
+    const int64_t row0 = rb * kSBlock;
+    const int64_t rl = row0 + 2 * tid;
+    // Lanes past the last row (n is even: both rows or neither) run the same
+    // instructions on clamped addresses; their products are dropped and they
+    // store into SpmvArgs::scratch. No branch around any memory operation: a
+    // branch there makes the compiler's wait counts assume the shorter path.
+    const bool active = rl < a.n;
+    const int lp = tid;
+    if constexpr (RELOAD) {
+#pragma unroll
+      for (int v = 0; v < NX; ++v) {
+        cen[v] = cur.cen[v];
+        prv[v] = cur.prv[v];
+      }
+    }
+    // (1) the next visit's loads, in flight across this visit's work. Issued
+    // unconditionally (the last visit re-reads its own rows): a load under a
+    // branch makes the compiler's wait counts assume the shorter path.
+    const int64_t zn = visit_ok(z + 1) ? z + 1 : z;
+    issue(nxs, zn);
+    // (2) operand values at the rows: centers, the previous plane's centers
+    dbl2v opc[NV], opp[NV];
+    if constexpr (VIRT) {
+      opc[0] = dbl2v{virtual_r1(a.c0, a.c1, cen[0].x, cen[1].x, cen[2].x),
+                     virtual_r1(a.c0, a.c1, cen[0].y, cen[1].y, cen[2].y)};
+      opp[0] = dbl2v{virtual_r1(a.c0, a.c1, prv[0].x, prv[1].x, prv[2].x),
+                     virtual_r1(a.c0, a.c1, prv[0].y, prv[1].y, prv[2].y)};
+    } else {
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        opc[v] = cen[v];
+        opp[v] = prv[v];
+      }
+    }
+    // (3) the LDS line: this block's centers and the edge pairs
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+      reinterpret_cast<dbl2v*>(&s_line[buf][v][kSNear])[tid] = opc[v];
+    if (tid < 2) {
+      double* dst = &s_line[buf][0][tid == 0 ? 0 : kSNear + kSBlock];
+      const dbl2v* e = tid == 0 ? cur.el : cur.er;
+      if constexpr (VIRT) {
+        *reinterpret_cast<dbl2v*>(dst) =
+            dbl2v{virtual_r1(a.c0, a.c1, e[0].x, e[1].x, e[2].x),
+                  virtual_r1(a.c0, a.c1, e[0].y, e[1].y, e[2].y)};
+      } else {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) *reinterpret_cast<dbl2v*>(dst + v * kSLine) = e[v];
+      }
+    }
+    __syncthreads();
+    issue_edges(nxs, zn);
+    // (4) the two rows' sums, slot by slot in ascending offset order
+    double slo[NV], shi[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) slo[v] = shi[v] = 0.0;
+#pragma unroll
+    for (int k = 0; k < NM_C; ++k) {
+      if (k >= nm) break;
+      const int kind = PAT ? (int)((PAT >> (4 * k)) & 0xFu) : a.st_kind[k];
+      const unsigned clo = (unsigned)(cur.clo >> (8 * k)) & 0xFFu;
+      const unsigned chi = (unsigned)(cur.chi >> (8 * k)) & 0xFFu;
+      const double vlo = s_tab[clo == 0xFFu ? 0u : clo];
+      const double vhi = s_tab[chi == 0xFFu ? 0u : chi];
+      double xlo[NV], xhi[NV];
+      if (kind == SK_CENTER) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) { xlo[v] = opc[v].x; xhi[v] = opc[v].y; }
+      } else if (kind == SK_PREV) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) { xlo[v] = opp[v].x; xhi[v] = opp[v].y; }
+      } else if (kind == SK_NEAR) {
+        const int o = a.st_off[k];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          xlo[v] = s_line[buf][v][kSNear + 2 * lp + o];
+          xhi[v] = s_line[buf][v][kSNear + 2 * lp + 1 + o];
+        }
+      } else {
+        // NEXT or FAR f: a staged pair
+        dbl2v g[NX];
+#pragma unroll
+        for (int v = 0; v < NX; ++v) g[v] = cur.nxt[v];
+#pragma unroll
+        for (int f = 0; f < NFAR; ++f)
+          if (kind == SK_FAR + f) {
+#pragma unroll
+            for (int v = 0; v < NX; ++v) g[v] = cur.far[f][v];
+          }
+        if constexpr (VIRT) {
+          xlo[0] = virtual_r1(a.c0, a.c1, g[0].x, g[1].x, g[2].x);
+          xhi[0] = virtual_r1(a.c0, a.c1, g[0].y, g[1].y, g[2].y);
+        } else {
+#pragma unroll
+          for (int v = 0; v < NV; ++v) { xlo[v] = g[v].x; xhi[v] = g[v].y; }
+        }
+      }
+      if (clo != 0xFFu) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) slo[v] = slo[v] + vlo * xlo[v];
+      }
+      if (chi != 0xFFu) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) shi[v] = shi[v] + vhi * xhi[v];
+      }
+    }
+    // (5) epilogue: row 2t, then row 2t+1 (products in that order)
+    {
+      const EpiIn ilo = st_epi_in<EPI>(cen[0].x, NX > 1 ? cen[NX > 1 ? 1 : 0].x : 0.0,
+                                       NX > 2 ? cen[NX > 2 ? 2 : 0].x : 0.0, cur.u1.x, cur.u2.x,
+                                       cur.us.x, cur.e.x);
+      const EpiIn ihi = st_epi_in<EPI>(cen[0].y, NX > 1 ? cen[NX > 1 ? 1 : 0].y : 0.0,
+                                       NX > 2 ? cen[NX > 2 ? 2 : 0].y : 0.0, cur.u1.y, cur.u2.y,
+                                       cur.us.y, cur.e.y);
+      double tmp[NP > 0 ? NP : 1];
+#pragma unroll
+      for (int q = 0; q < (NP > 0 ? NP : 1); ++q) tmp[q] = acc[q];
+      const EpiVals olo = epi_values<EPI>(a, slo[0], NV == 2 ? slo[NV - 1] : 0.0, ilo, tmp);
+      const EpiVals ohi = epi_values<EPI>(a, shi[0], NV == 2 ? shi[NV - 1] : 0.0, ihi, tmp);
+#pragma unroll
+      for (int q = 0; q < (NP > 0 ? NP : 1); ++q) acc[q] = active ? tmp[q] : acc[q];
+      epi_store_pair<EPI>(a, rl, olo, ohi, active);
+    }
+    // (6) carry along the walk: this visit's centers are the next one's PREV
+    if constexpr (!RELOAD) {
+#pragma unroll
+      for (int v = 0; v < NX; ++v) {
+        prv[v] = cen[v];
+        cen[v] = cur.nxt[v];
+      }
+    }
+    buf ^= 1;
+  };
+
+  int64_t z = z0;
+  if (visit_ok(z)) {
+    issue(sA, z);
+    issue_edges(sA, z);
+    if constexpr (!RELOAD) {  // CENTER and PREV of the segment's first visit
+      const int64_t rl = phys(z * P + p) * kSBlock + 2 * tid;
+      const int64_t xi = a.xoff + (rl < a.n ? rl : a.n - 2);
+#pragma unroll
+      for (int v = 0; v < NX; ++v) {
+        cen[v] = st_ld2(xs[v], xi, a.xlen);
+        prv[v] = st_ld2(xs[v], xi - W, a.xlen);
+      }
+    }
+  }
+  // Drain the prologue's loads (once per segment): the loop's wait counts
+  // then start from an empty queue on every path into it.
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  __syncthreads();  // s_tab
+  for (;;) {
+    if (!visit_ok(z)) break;
+    visit(sA, sB, z);
+    ++z;
+    if (!visit_ok(z)) break;
+    visit(sB, sA, z);
+    ++z;
+  }
+  __syncthreads();
+  block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
+}
+
+template <int E, bool RELOAD>
+void spmv_stencil_launch_r(const SpmvArgs& a, int nblocks, hipStream_t s) {
+  bool pat7 = a.st_nm == 7 && a.st_nfar == 2;
+  for (int k = 0; k < 7 && pat7; ++k) pat7 = a.st_kind[k] == (int)((kPat7 >> (4 * k)) & 0xFu);
+  if (pat7) {
+    spmv_stencil_kernel<E, 2, kPat7, RELOAD><<<nblocks, kBlock, 0, s>>>(a);
+    return;
+  }
+  switch (a.st_nfar) {
+    case 0: spmv_stencil_kernel<E, 0, 0, RELOAD><<<nblocks, kBlock, 0, s>>>(a); return;
+    case 1: spmv_stencil_kernel<E, 1, 0, RELOAD><<<nblocks, kBlock, 0, s>>>(a); return;
+    case 2: spmv_stencil_kernel<E, 2, 0, RELOAD><<<nblocks, kBlock, 0, s>>>(a); return;
+    case 3: spmv_stencil_kernel<E, 3, 0, RELOAD><<<nblocks, kBlock, 0, s>>>(a); return;
+    default: spmv_stencil_kernel<E, 4, 0, RELOAD><<<nblocks, kBlock, 0, s>>>(a); return;
+  }
+}
+
+// Launches with a row-block gap (the boundary launch of a split SpMV) reload
+// CENTER and PREV at every visit; all others carry them.
+template <int E>
+void spmv_stencil_launch(const SpmvArgs& a, int nblocks, hipStream_t s) {
+  if (a.rb_gap > 0)
+    spmv_stencil_launch_r<E, true>(a, nblocks, s);
+  else
+    spmv_stencil_launch_r<E, false>(a, nblocks, s);
+}

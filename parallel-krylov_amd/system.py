@@ -289,11 +289,13 @@ class KrylovSystem:
         """Launch geometry of shard s: elementwise and SpMV grids plus the
         interior rows of the split SpMV -- what fixes the engine's dot-product
         summation order (oracle/gpu_order.py restates it for the tests)."""
-        g, sg = ctypes.c_int(), ctypes.c_int()
-        call("kr_system_shard_sched", self.handle, s, ctypes.byref(g), ctypes.byref(sg))
+        g, sg, sw = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        call("kr_system_shard_sched", self.handle, s, ctypes.byref(g), ctypes.byref(sg),
+             ctypes.byref(sw))
         lay = self.shard_layout(s)
         return dict(n=self.row_begin[s + 1] - self.row_begin[s], grid=g.value,
-                    spmv_grid=sg.value, int_lo=lay["interior_lo"], int_hi=lay["interior_hi"])
+                    spmv_grid=sg.value, int_lo=lay["interior_lo"], int_hi=lay["interior_hi"],
+                    stencil_walk=sw.value)
 
     def csr_pointers(self, s: int) -> dict:
         """Raw device CSR of shard s (local columns after finalize)."""

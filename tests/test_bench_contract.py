@@ -73,3 +73,6 @@ def test_stored_format_bytes():
     assert bench.stored_format_delta(nnz_long, n, dia) == (
         12.0 * nnz_long + 4.0 * (n + 1) - (8.0 * 27 * 1024 + 4.0 * n))
     assert "dictionary" in bench.format_name(both) and "masks" in bench.format_name(both)
+    st = dict(mask_bits=8, n_offsets=7, dict_values=2, stencil_walk=512)
+    assert bench.stored_format_delta(nnz, n, st) == 12.0 * nnz + 4.0 * (n + 1) - 8.0 * n
+    assert "stencil" in bench.format_name(st)

@@ -1,0 +1,224 @@
+"""The stencil SpMV (kr_stencil.h): 512-row blocks, two rows per lane, the
+walk carrying x[row - W] and x[row] in registers, +-1 neighbours from an LDS
+line, one uint64 of dictionary codes per row.
+
+It serves masked short-row shards with a value dictionary whose offsets hold
+a +-W pair (W a multiple of 512: 3-D stencils with n^2 % 512 == 0, 2-D ones
+with n % 512 == 0), up to 8 offsets, others within +-2 or even (<= 4).
+CPU tests pin which matrices qualify (oracle/gpu_order.py restates the
+engine's decision); ``-m gpu`` tests check it bit for bit:
+
+* y = A x equals scipy's csr_matvec BITWISE (every row summed in stored
+  order) -- cubes, boxes with partial last planes / blocks, 2-D, banded
+  stencils with FAR offsets, 1-3 shards (split SpMV with a row-block gap);
+* the solver histories equal the oracle run in the engine's summation order
+  bit for bit (kr_stencil.h's lane/visit order, oracle/gpu_order.py),
+  including adaptive rollbacks, on 1-3 shards;
+* fused k-skip steps (EPI_STEP_*, steps 0+1 in one SpMV) equal the unfused
+  ones bit for bit on the stencil kernel;
+* KR_STENCIL=0 (the row walk) gives the same y bitwise.
+"""
+import contextlib
+import importlib
+import io
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from conftest import golden_matrix
+from oracle import gpu_order
+
+
+def box(nx, ny, nz=None):
+    """7-point (5-point without nz) Poisson on an nx x ny (x nz) grid, x fastest."""
+    def T(m):
+        return sp.diags([-1.0, 2.0, -1.0], [-1, 0, 1], shape=(m, m))
+    K = sp.kronsum(T(nx), T(ny))
+    if nz is not None:
+        K = sp.kronsum(K, T(nz))
+    K = sp.csr_matrix(K)
+    K.sort_indices()
+    return K
+
+
+def stencil_band(n, offs, seed=0):
+    """Symmetric banded SPD matrix with the given positive offsets (few
+    distinct values: a dictionary applies)."""
+    rng = np.random.default_rng(seed)
+    vals = {o: -float(rng.integers(1, 4)) / 4 for o in offs}
+    diags = [np.full(n - o, vals[o]) for o in offs]
+    A = sp.diags(diags + diags + [np.full(n, 2.0 * sum(-v for v in vals.values()) + 1.0)],
+                 list(offs) + [-o for o in offs] + [0], shape=(n, n))
+    A = sp.csr_matrix(A)
+    A.sort_indices()
+    return A
+
+
+def _bal(n, p):
+    q, r = divmod(n, p)
+    out = [0]
+    for i in range(p):
+        out.append(out[-1] + q + (1 if i < r else 0))
+    return out
+
+
+MATRICES = {
+    "p3d32": lambda: golden_matrix(["poisson", 32, 3]),
+    "p3d64": lambda: golden_matrix(["poisson", 64, 3]),
+    "box32x32x7": lambda: box(32, 32, 7),        # 7168 rows: 14 blocks, 7 planes of 2
+    "box64x16x9": lambda: box(64, 16, 9),        # W = 1024: P = 2
+    "box48x32x5": lambda: box(48, 32, 5),        # W = 1536: P = 3, n % 512 == 0
+    "box32x32x3": lambda: box(32, 32, 3),        # 3 planes only
+    "p2d512x6": lambda: box(512, 6),             # 2-D: W = 512 = the line
+    "band_far": lambda: stencil_band(6144, [1, 6, 512]),
+    "band_far2": lambda: stencil_band(5120, [2, 14, 1024]),
+}
+# expected stencil walk P (0: the row walk serves the matrix)
+EXPECT_P = {"p3d32": 2, "p3d64": 8, "box32x32x7": 2, "box64x16x9": 2, "box48x32x5": 3,
+            "box32x32x3": 2, "p2d512x6": 1, "band_far": 1, "band_far2": 2}
+NOT_STENCIL = {
+    "p3d24": lambda: golden_matrix(["poisson", 24, 3]),      # 576 % 512 != 0
+    "p3d16": lambda: golden_matrix(["poisson", 16, 3]),
+    "odd_rows": lambda: box(32, 32, 7)[:7167, :7167],        # odd n
+    "odd_far": lambda: stencil_band(4096, [3, 512]),         # FAR offset 3 is odd
+    "nine_offsets": lambda: stencil_band(6000, [1, 6, 40, 512]),
+    "band27": lambda: golden_matrix(["banded", 3000, 13, 64, 0]),  # long rows (DIA)
+}
+
+
+# ------------------------------------------------------------------ CPU
+@pytest.mark.parametrize("name", sorted(MATRICES))
+def test_stencil_kernel_is_chosen(name):
+    A = MATRICES[name]()
+    sc = gpu_order.shard_scheds(A, [0, A.shape[0]])[0]
+    assert sc.stencil_walk == EXPECT_P[name]
+    assert sc.spmv_grid % (8 * sc.stencil_walk) == 0
+
+
+@pytest.mark.parametrize("name", sorted(NOT_STENCIL))
+def test_row_walk_keeps_the_rest(name):
+    A = NOT_STENCIL[name]()
+    assert gpu_order.shard_scheds(A, [0, A.shape[0]])[0].stencil_walk == 0
+
+
+def test_stencil_sharded_interior_on_512_blocks():
+    A = MATRICES["p3d64"]()
+    for s in gpu_order.shard_scheds(A, _bal(A.shape[0], 4)):
+        assert s.stencil_walk == 8
+        assert s.int_lo % 512 == 0 and s.int_hi % 512 == 0 and s.int_lo < s.int_hi
+    # 262144 rows over 3 shards: 87382 (even: stencil) + 2 x 87381 (odd: row walk)
+    assert [s.stencil_walk for s in gpu_order.shard_scheds(A, _bal(A.shape[0], 3))] == [8, 0, 0]
+
+
+# ------------------------------------------------------------------ GPU
+def _system(A, shards, env=None, monkeypatch=None):
+    from parallel_krylov_amd.system import KrylovSystem, balanced_partition
+    for k, v in (env or {}).items():
+        monkeypatch.setenv(k, v)
+    n = A.shape[0]
+    sysm = KrylovSystem(n, balanced_partition(n, shards), [0] * shards)
+    sysm.set_matrix(A)
+    sysm.finalize()
+    return sysm
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shards", [1, 2, 3])
+@pytest.mark.parametrize("name", sorted(MATRICES))
+def test_stencil_spmv_bitwise_scipy(monkeypatch, name, shards):
+    A = MATRICES[name]()
+    n = A.shape[0]
+    sysm = _system(A, shards)
+    sc = [sysm.shard_sched(s) for s in range(shards)]
+    assert [s["stencil_walk"] for s in sc] == \
+        [s.stencil_walk for s in gpu_order.shard_scheds(A, _bal(n, shards))]
+    assert sc[0]["stencil_walk"] > 0 or shards > 1
+    x = np.random.default_rng(5).standard_normal(n)
+    y = sysm.gather(sysm.spmv(sysm.split(x))).cpu().numpy()
+    sysm.close()
+    np.testing.assert_array_equal(y, A @ x)
+    # the row walk agrees bit for bit
+    sysm = _system(A, shards, {"KR_STENCIL": "0"}, monkeypatch)
+    assert all(sysm.shard_sched(s)["stencil_walk"] == 0 for s in range(shards))
+    y0 = sysm.gather(sysm.spmv(sysm.split(x))).cpu().numpy()
+    sysm.close()
+    np.testing.assert_array_equal(y0, y)
+
+
+def _solver(method):
+    mod = importlib.import_module(f"parallel_krylov_amd.v3.gpu.{method}")
+    return getattr(mod, method)
+
+
+CASES = [
+    ("adaptivekskipmrr", "p3d32", 12, 1), ("adaptivekskipmrr", "p3d32", 12, 3),
+    ("adaptivekskipmrr", "box32x32x7", 8, 2), ("kskipmrr", "p3d32", 4, 1),
+    ("kskipmrr", "box64x16x9", 3, 2), ("kskipcg", "p3d32", 3, 1), ("kskipcg", "band_far", 2, 3),
+    ("kskipmrr", "band_far2", 5, 1), ("adaptivekskipmrr", "p2d512x6", 6, 1),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method,name,k,shards", CASES)
+def test_stencil_solvers_bitwise_gpu_order_oracle(monkeypatch, method, name, k, shards):
+    A = MATRICES[name]()
+    n = A.shape[0]
+    b = np.random.default_rng(1).standard_normal(n)
+    sysm = _system(A, shards)
+    sc = [gpu_order.ShardSched(**sysm.shard_sched(s)) for s in range(shards)]
+    sysm.close()
+    assert sc == gpu_order.shard_scheds(A, _bal(n, shards))
+    monkeypatch.setenv("KRYLOV_AMD_SHARDS", ",".join(["0"] * shards))
+    kw = dict(tol=1e-10, k=k, maxiter=600)
+    with contextlib.redirect_stdout(io.StringIO()):
+        x, info = _solver(method)(A, b, **kw)
+    x_ref, ref = gpu_order.run(method, A, b, sc, **kw)
+    np.testing.assert_array_equal(info["nosl"], ref["nosl"])
+    if "khistory" in ref:
+        np.testing.assert_array_equal(info["khistory"], ref["khistory"])
+    np.testing.assert_array_equal(info["residual"], ref["residual"])
+    np.testing.assert_array_equal(x.cpu().numpy(), x_ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shards", ["0", "0,0,0"])
+@pytest.mark.parametrize("method,name,k", [("kskipmrr", "p3d32", 1), ("kskipmrr", "p3d32", 4),
+                                           ("kskipmrr", "box32x32x7", 3),
+                                           ("kskipcg", "p3d64", 3),
+                                           ("adaptivekskipmrr", "p3d32", 6),
+                                           ("kskipmrr", "band_far", 2)])
+def test_stencil_fused_steps_bitwise_equal_unfused(monkeypatch, shards, method, name, k):
+    A = MATRICES[name]()
+    b = np.random.default_rng(3).standard_normal(A.shape[0])
+    kw = dict(tol=1e-10, maxiter=300, k=k)
+    out = []
+    for env in ({"KR_FUSE": "0"}, {"KR_FUSE": "1", "KR_FUSE_FIRST": "1"},
+                {"KR_FUSE": "1", "KR_FUSE_FIRST": "0"}):
+        monkeypatch.setenv("KRYLOV_AMD_SHARDS", shards)
+        for kk, vv in env.items():
+            monkeypatch.setenv(kk, vv)
+        with contextlib.redirect_stdout(io.StringIO()):
+            x, info = _solver(method)(A, b, **kw)
+        out.append((x.cpu().numpy(), info))
+    for x1, i1 in out[1:]:
+        np.testing.assert_array_equal(i1["nosl"], out[0][1]["nosl"])
+        np.testing.assert_array_equal(i1["residual"], out[0][1]["residual"])
+        np.testing.assert_array_equal(x1, out[0][0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method", ["cg", "mrr"])
+def test_stencil_cg_mrr_match_reference_contract(method):
+    """CG / MrR (head-less epilogues EPI_XY, EPI_MRR_LOOP, EPI_BMINUS on the
+    stencil kernel) against the oracle: SURVEY.md 8(c) contract."""
+    from oracle import v3cpu
+    A = MATRICES["p3d32"]()
+    b = np.random.default_rng(1).standard_normal(A.shape[0])
+    with contextlib.redirect_stdout(io.StringIO()):
+        x, info = _solver(method)(A, b, tol=1e-10)
+    x_ref, ref = v3cpu.METHODS[method](A, b, tol=1e-10)
+    np.testing.assert_array_equal(info["nosl"], ref["nosl"])
+    rel = np.abs(info["residual"] - ref["residual"]) / ref["residual"]
+    assert rel.max() <= 1e-12
+    assert np.linalg.norm(x.cpu().numpy() - x_ref) <= 1e-11 * np.linalg.norm(x_ref)

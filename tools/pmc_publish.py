@@ -12,7 +12,7 @@ Writes profiles/pmc/<config>.json:
                                         "write_bytes", "avg_ms", ...}}}
 
 Kernel names are the engine's (kr_engine.cpp epi_name / ew_name), the names
-bench.py's per-kernel table uses: pmc_summary's "_dia" / "_dense" / "_rp64"
+bench.py's per-kernel table uses: pmc_summary's "_dia" / "_dense" / "_stencil" / "_rp64"
 variant suffixes are folded (one config runs one variant of a kernel).
 bench.pmc_traffic(config, kernel) returns null for any other pair.
 """
@@ -25,7 +25,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def engine_name(name):
-    return re.sub(r"(_rp64)?(_dia|_dense)?$", "", name)
+    return re.sub(r"(_rp64)?(_dia|_dense|_stencil)?$", "", name)
 
 
 def main(d, config, source=None):

@@ -6,7 +6,7 @@
 # Usage: bash tools/profile.sh <tag> [bench args...]
 # One config per call (kernel names must be unique per profile): the bench
 # args default to the C4 headline without its plain-CSR sub-run; profile the
-# CSR format with `KR_MASK=0 KR_VDICT=0 bash tools/profile.sh <tag>`.
+# CSR format with `KR_MASK=0 KR_VDICT=0 KR_STENCIL=0 bash tools/profile.sh <tag>`.
 tag=${1:-prof}; shift
 args=${@:---steps 5 --warmup 1 --no-cpu-baseline --no-csr}
 out=gpurun_out/$tag
