@@ -81,17 +81,19 @@ __device__ __forceinline__ dbl2v st_ld2_uniform(const double* x, int64_t i, int6
   return load_uniform(reinterpret_cast<const dbl2v*>(x), i >> 1);
 }
 
+// rl: the lane's first row (launch-relative, may lie past the last own row:
+// x loads use it as is -- rows past the own rows are halo rows, which the
+// +-1 neighbours of the last own rows need -- clamped only to the vector);
+// rr: rl clamped to the own rows (codes and own-row operands).
 template <int EPI, bool RELOAD, int NX, int NFAR>
 __device__ __forceinline__ void st_issue(SStage<NX, NFAR>& st, const SpmvArgs& a,
-                                         const double* const (&xs)[3], int64_t row0, int64_t rr,
-                                         int tid) {
+                                         const double* const (&xs)[3], int64_t rl, int64_t rr) {
   using T = EpiTraits<EPI>;
-  (void)tid;
   const uint64_t* cp = a.scode + rr;
   const auto c = *reinterpret_cast<const __attribute__((ext_vector_type(2))) uint64_t*>(cp);
   st.clo = c.x;
   st.chi = c.y;
-  const int64_t xi = a.xoff + rr;
+  const int64_t xi = a.xoff + rl;
   const int64_t W = (int64_t)a.st_P * kSBlock;
 #pragma unroll
   for (int v = 0; v < NX; ++v) st.nxt[v] = st_ld2(xs[v], xi + W, a.xlen);
@@ -204,9 +206,8 @@ __global__ __launch_bounds__(kBlock) void spmv_stencil_kernel(SpmvArgs a) {
   SStage<NX, NFAR> sA, sB;
   int buf = 0;
   auto issue = [&](SStage<NX, NFAR>& st, int64_t z) {
-    const int64_t rb = phys(z * P + p);
-    const int64_t rl = rb * kSBlock + 2 * tid;
-    st_issue<EPI, RELOAD>(st, a, xs, rb * kSBlock, rl < a.n ? rl : a.n - 2, tid);
+    const int64_t rl = phys(z * P + p) * kSBlock + 2 * tid;
+    st_issue<EPI, RELOAD>(st, a, xs, rl, rl < a.n ? rl : a.n - 2);
   };
   auto issue_edges = [&](SStage<NX, NFAR>& st, int64_t z) {
     st_issue_edges(st, a, xs, phys(z * P + p) * kSBlock);
@@ -221,9 +222,11 @@ __global__ __launch_bounds__(kBlock) void spmv_stencil_kernel(SpmvArgs a) {
     const int64_t row0 = rb * kSBlock;
     const int64_t rl = row0 + 2 * tid;
     // Lanes past the last row (n is even: both rows or neither) run the same
-    // instructions on clamped addresses; their products are dropped and they
-    // store into SpmvArgs::scratch. No branch around any memory operation: a
-    // branch there makes the compiler's wait counts assume the shorter path.
+    // instructions; they load x at their true rows (halo rows: the line needs
+    // them for the +1 neighbour of the last own row), their products are
+    // dropped and they store into SpmvArgs::scratch. No branch around any
+    // memory operation: a branch there makes the compiler's wait counts
+    // assume the shorter path.
     const bool active = rl < a.n;
     const int lp = tid;
     if constexpr (RELOAD) {
@@ -357,8 +360,7 @@ __global__ __launch_bounds__(kBlock) void spmv_stencil_kernel(SpmvArgs a) {
     issue(sA, z);
     issue_edges(sA, z);
     if constexpr (!RELOAD) {  // CENTER and PREV of the segment's first visit
-      const int64_t rl = phys(z * P + p) * kSBlock + 2 * tid;
-      const int64_t xi = a.xoff + (rl < a.n ? rl : a.n - 2);
+      const int64_t xi = a.xoff + phys(z * P + p) * kSBlock + 2 * tid;
 #pragma unroll
       for (int v = 0; v < NX; ++v) {
         cen[v] = st_ld2(xs[v], xi, a.xlen);
