@@ -316,11 +316,15 @@ __device__ __forceinline__ void epi_store_row(const SpmvArgs& a, int64_t row, co
 // Rows row, row + 1 (row even: own-row vectors are 16-byte aligned there);
 // ok = false sends the pair to SpmvArgs::scratch instead (lanes past the
 // last row store unconditionally, see kr_stencil.h).
-template <int EPI>
+template <int EPI, bool NT = false>
 __device__ __forceinline__ void epi_store_pair(const SpmvArgs& a, int64_t row, const EpiVals& lo,
                                                const EpiVals& hi, bool ok = true) {
   auto st2 = [&](double* p, double u, double v) {
-    *reinterpret_cast<dbl2v*>(ok ? p + row : a.scratch) = dbl2v{u, v};
+    dbl2v* d = reinterpret_cast<dbl2v*>(ok ? p + row : a.scratch);
+    if constexpr (NT)
+      __builtin_nontemporal_store(dbl2v{u, v}, d);
+    else
+      *d = dbl2v{u, v};
   };
   if constexpr (is_step<EPI>()) {
     if constexpr (epi_writes_ud<EPI>()) st2(a.ud, lo.ud, hi.ud);

@@ -85,12 +85,17 @@ __device__ __forceinline__ dbl2v st_ld2_uniform(const double* x, int64_t i, int6
 // x loads use it as is -- rows past the own rows are halo rows, which the
 // +-1 neighbours of the last own rows need -- clamped only to the vector);
 // rr: rl clamped to the own rows (codes and own-row operands).
-template <int EPI, bool RELOAD, int NX, int NFAR>
+template <int EPI, bool RELOAD, int NTM, int NX, int NFAR>
 __device__ __forceinline__ void st_issue(SStage<NX, NFAR>& st, const SpmvArgs& a,
                                          const double* const (&xs)[3], int64_t rl, int64_t rr) {
   using T = EpiTraits<EPI>;
   const uint64_t* cp = a.scode + rr;
-  const auto c = *reinterpret_cast<const __attribute__((ext_vector_type(2))) uint64_t*>(cp);
+  typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+  u64x2 c;
+  if constexpr (NTM & 1)  // codes: streamed once (non-temporal)
+    c = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(cp));
+  else
+    c = *reinterpret_cast<const u64x2*>(cp);
   st.clo = c.x;
   st.chi = c.y;
   const int64_t xi = a.xoff + rl;
@@ -167,7 +172,9 @@ constexpr uint32_t kPat7 =
 // RELOAD: every visit loads its CENTER and PREV (launches whose walk crosses
 // a row-block gap: the boundary launch of a split SpMV); otherwise they are
 // loaded once per plane segment, before the loop, and carried.
-template <int EPI, int NFAR, uint32_t PAT, bool RELOAD>
+// NTM: bit 0 = non-temporal code loads, bit 1 = non-temporal result stores
+// (A/B, KR_STENCIL_NT).
+template <int EPI, int NFAR, uint32_t PAT, bool RELOAD, int NTM = 3>
 __global__ __launch_bounds__(kBlock) void spmv_stencil_kernel(SpmvArgs a) {
   if (a.stop && *a.stop != 0.0) return;  // converged (device-resident scalars)
   using T = EpiTraits<EPI>;
@@ -207,7 +214,7 @@ __global__ __launch_bounds__(kBlock) void spmv_stencil_kernel(SpmvArgs a) {
   int buf = 0;
   auto issue = [&](SStage<NX, NFAR>& st, int64_t z) {
     const int64_t rl = phys(z * P + p) * kSBlock + 2 * tid;
-    st_issue<EPI, RELOAD>(st, a, xs, rl, rl < a.n ? rl : a.n - 2);
+    st_issue<EPI, RELOAD, NTM>(st, a, xs, rl, rl < a.n ? rl : a.n - 2);
   };
   auto issue_edges = [&](SStage<NX, NFAR>& st, int64_t z) {
     st_issue_edges(st, a, xs, phys(z * P + p) * kSBlock);
@@ -342,7 +349,7 @@ __global__ __launch_bounds__(kBlock) void spmv_stencil_kernel(SpmvArgs a) {
       const EpiVals ohi = epi_values<EPI>(a, shi[0], NV == 2 ? shi[NV - 1] : 0.0, ihi, tmp);
 #pragma unroll
       for (int q = 0; q < (NP > 0 ? NP : 1); ++q) acc[q] = active ? tmp[q] : acc[q];
-      epi_store_pair<EPI>(a, rl, olo, ohi, active);
+      epi_store_pair<EPI, (NTM & 2) != 0>(a, rl, olo, ohi, active);
     }
     // (6) carry along the walk: this visit's centers are the next one's PREV
     if constexpr (!RELOAD) {
@@ -388,16 +395,32 @@ template <int E, bool RELOAD>
 void spmv_stencil_launch_r(const SpmvArgs& a, int nblocks, hipStream_t s) {
   bool pat7 = a.st_nm == 7 && a.st_nfar == 2;
   for (int k = 0; k < 7 && pat7; ++k) pat7 = a.st_kind[k] == (int)((kPat7 >> (4 * k)) & 0xFu);
+  // Non-temporal code loads and result stores (NTM = 3): the streamed-once
+  // bytes stop displacing the x lines neighbouring workgroups re-read from
+  // L2 (C4 +4-7 %). KR_STENCIL_NT=0..2 (A/B; 7-point pattern). KR_STENCIL_LDS
+  // (A/B): extra LDS per workgroup, i.e. fewer resident workgroups per CU.
+  const char* env = getenv("KR_STENCIL_NT");
+  const int ntm = env ? atoi(env) : 3;
+  const char* lenv = getenv("KR_STENCIL_LDS");
+  const size_t lds = lenv ? (size_t)atoi(lenv) : 0;
   if (pat7) {
-    spmv_stencil_kernel<E, 2, kPat7, RELOAD><<<nblocks, kBlock, 0, s>>>(a);
+    if constexpr (!RELOAD) {
+      switch (ntm) {
+        case 0: spmv_stencil_kernel<E, 2, kPat7, RELOAD, 0><<<nblocks, kBlock, lds, s>>>(a); return;
+        case 1: spmv_stencil_kernel<E, 2, kPat7, RELOAD, 1><<<nblocks, kBlock, lds, s>>>(a); return;
+        case 2: spmv_stencil_kernel<E, 2, kPat7, RELOAD, 2><<<nblocks, kBlock, lds, s>>>(a); return;
+        default: break;
+      }
+    }
+    spmv_stencil_kernel<E, 2, kPat7, RELOAD, 3><<<nblocks, kBlock, lds, s>>>(a);
     return;
   }
   switch (a.st_nfar) {
-    case 0: spmv_stencil_kernel<E, 0, 0, RELOAD><<<nblocks, kBlock, 0, s>>>(a); return;
-    case 1: spmv_stencil_kernel<E, 1, 0, RELOAD><<<nblocks, kBlock, 0, s>>>(a); return;
-    case 2: spmv_stencil_kernel<E, 2, 0, RELOAD><<<nblocks, kBlock, 0, s>>>(a); return;
-    case 3: spmv_stencil_kernel<E, 3, 0, RELOAD><<<nblocks, kBlock, 0, s>>>(a); return;
-    default: spmv_stencil_kernel<E, 4, 0, RELOAD><<<nblocks, kBlock, 0, s>>>(a); return;
+    case 0: spmv_stencil_kernel<E, 0, 0, RELOAD, 3><<<nblocks, kBlock, 0, s>>>(a); return;
+    case 1: spmv_stencil_kernel<E, 1, 0, RELOAD, 3><<<nblocks, kBlock, 0, s>>>(a); return;
+    case 2: spmv_stencil_kernel<E, 2, 0, RELOAD, 3><<<nblocks, kBlock, 0, s>>>(a); return;
+    case 3: spmv_stencil_kernel<E, 3, 0, RELOAD, 3><<<nblocks, kBlock, 0, s>>>(a); return;
+    default: spmv_stencil_kernel<E, 4, 0, RELOAD, 3><<<nblocks, kBlock, 0, s>>>(a); return;
   }
 }
 
