@@ -232,9 +232,14 @@ int kr_system_shard_values(kr_system* sys, int shard, int* dict_values);
  * kr_system_shard_layout they fix the summation order of every dot product
  * (oracle/gpu_order.py restates it for the bitwise GPU-order parity tests).
  * Replaces nothing in the reference (cuBLAS ddot's order is internal).
- * Pointers may be NULL. */
+ * format = KR_FORMAT_*. Pointers may be NULL. */
 int kr_system_shard_sched(kr_system* sys, int shard, int* grid, int* spmv_grid,
-                          int* stencil_walk);
+                          int* stencil_walk, int* format);
+/* kr_system_shard_sched format: the SpMV kernel family serving the shard. */
+#define KR_FORMAT_CSR 0     /* row walk over CSR (offset masks / dictionary optional) */
+#define KR_FORMAT_STENCIL 1 /* stencil codes (kr_stencil.h) */
+#define KR_FORMAT_DIA 2     /* diagonal-offset values (long masked rows) */
+#define KR_FORMAT_DENSE 3   /* dense row block (GEMV) */
 
 /* Halo exchange plan (pure host arithmetic, no device; test hook and the
  * planner kr_system_finalize uses). part[0..nshards] is the global row

@@ -16,6 +16,7 @@ _lock = threading.Lock()
 _lib = None
 
 KR_METHOD = {"cg": 0, "mrr": 1, "kskipcg": 2, "kskipmrr": 3, "adaptivekskipmrr": 4}
+KR_FORMAT = {0: "csr", 1: "stencil", 2: "dia", 3: "dense"}  # kr_system_shard_sched
 
 
 class KrylovError(RuntimeError):
@@ -90,7 +91,7 @@ _SIGNATURES = {
     "kr_system_shard_info": [_P, _I, _PI64, _PI64, _PI64, _PI64],
     "kr_system_shard_layout": [_P, _I, _PI, _PI, _PI64, _PI64],
     "kr_system_shard_values": [_P, _I, _PI],
-    "kr_system_shard_sched": [_P, _I, _PI, _PI, _PI],
+    "kr_system_shard_sched": [_P, _I, _PI, _PI, _PI, _PI],
     "kr_fill_rhs": [_P, _I, _U64, _P],
     "kr_system_csr": [_P, _I, _PP, _PI, _PP, _PP, _PI64],
     "kr_system_spmv": [_PP, _PP, _PP],

@@ -636,13 +636,17 @@ int kr_system_shard_values(kr_system* sys, int shard, int* dict_values) {
 }
 
 int kr_system_shard_sched(kr_system* sys, int shard, int* grid, int* spmv_grid,
-                          int* stencil_walk) {
+                          int* stencil_walk, int* format) {
   return guarded([&] {
     KR_REQUIRE(sys && shard >= 0 && shard < (int)sys->shards.size(), "bad shard");
     KR_REQUIRE(sys->finalized, "system not finalized");
     if (grid) *grid = sys->shards[shard].grid;
     if (spmv_grid) *spmv_grid = sys->shards[shard].spmv_grid;
-    if (stencil_walk) *stencil_walk = sys->shards[shard].scode ? sys->shards[shard].st_P : 0;
+    const Shard& s = sys->shards[shard];
+    if (stencil_walk) *stencil_walk = s.scode ? s.st_P : 0;
+    if (format)
+      *format = s.dense ? KR_FORMAT_DENSE : s.scode ? KR_FORMAT_STENCIL
+                                                     : s.dia ? KR_FORMAT_DIA : KR_FORMAT_CSR;
   });
 }
 

@@ -4,15 +4,22 @@ The reference's MPI drivers hand each rank a row block read from ``.npz``
 (scipy sparse) or ``.npy`` (dense) files (``v3/gpu/mpi/common.py:123-129``;
 the files themselves are gitignored, ``.gitignore:14-17``). Here:
 
-* ``read_csr_rows(path, r0, r1)`` returns rows [r0, r1) of a stored matrix as
-  (indptr, indices, data, n_cols) with GLOBAL columns. For an uncompressed
+* ``read_rows(path, r0, r1)`` returns rows [r0, r1) of a stored matrix as
+  the reference would hold them: a ``.npz`` (scipy CSR) block as
+  (indptr, indices, data, n_cols) with GLOBAL columns, a ``.npy`` block as a
+  DENSE float64 ndarray -- the reference keeps dense row blocks dense
+  (``v3/gpu/mpi/common.py:123-125``, cupy dgemv), so they run the GEMV kernel
+  here too (8 B per entry streamed, no index stream). For an uncompressed
   ``.npz`` (``scipy.sparse.save_npz(..., compressed=False)``) or a ``.npy``,
   the arrays are memory-mapped, so a rank touches only its own block's bytes;
-  a compressed ``.npz`` is inflated once.
+  a compressed ``.npz`` is inflated once. ``read_csr_rows`` is the CSR view
+  of either (a ``.npy`` block converted).
 * ``load_system(path, devices=None)`` builds a single-process
-  ``KrylovSystem`` (one shard per device) from a file.
+  ``KrylovSystem`` (one shard per device) from a file: CSR shards for a
+  ``.npz``, dense shards for a ``.npy``.
 * ``load_local_block(path, comm)`` is the MPI-family helper: this rank's
-  balanced row block, ready for ``v3.gpu.mpi.<method>(comm, local_A, b)``.
+  balanced row block (scipy CSR, or a dense ndarray for a ``.npy``), ready
+  for ``v3.gpu.mpi.<method>(comm, local_A, b)``.
 
 Files are read with ``allow_pickle=False`` only.
 """
@@ -69,8 +76,18 @@ def matrix_shape(path) -> tuple:
         return tuple(int(v) for v in z["shape"])
 
 
+def read_rows(path: str, r0: int, r1: int):
+    """Rows [r0, r1) of a stored matrix: a dense float64 ndarray for a .npy,
+    else (indptr from 0, indices, data, n_cols) of the CSR block."""
+    if path.endswith(".npy"):
+        dense = np.load(path, mmap_mode="r", allow_pickle=False)
+        return np.ascontiguousarray(dense[r0:r1], dtype=np.float64)
+    return read_csr_rows(path, r0, r1)
+
+
 def read_csr_rows(path: str, r0: int, r1: int):
-    """Rows [r0, r1) of a stored matrix: (indptr from 0, indices, data, n_cols)."""
+    """Rows [r0, r1) of a stored matrix as CSR: (indptr from 0, indices, data,
+    n_cols); a .npy block is converted (its nonzero entries)."""
     if path.endswith(".npy"):
         dense = np.load(path, mmap_mode="r", allow_pickle=False)
         blk = np.asarray(dense[r0:r1], dtype=np.float64)
@@ -98,15 +115,21 @@ def load_system(path: str, devices=None) -> KrylovSystem:
     sysm = KrylovSystem(n, balanced_partition(n, len(devices)), devices)
     for s in range(sysm.nshards):
         r0, r1 = sysm.shard_rows(s)
-        indptr, indices, data, _ = read_csr_rows(path, r0, r1)
-        sysm.adopt_csr(s, (indptr, indices, data))
+        blk = read_rows(path, r0, r1)
+        if isinstance(blk, np.ndarray):  # .npy: dense row block, GEMV
+            sysm.adopt_dense(s, blk)
+        else:
+            indptr, indices, data, _ = blk
+            sysm.adopt_csr(s, (indptr, indices, data))
     sysm.finalize()
     return sysm
 
 
 def load_local_block(path: str, comm=None):
-    """This rank's balanced row block as a scipy CSR matrix (global columns),
-    for the MPI family: ``x, info = kskipmrr(comm, load_local_block(p, comm), b)``."""
+    """This rank's balanced row block for the MPI family, as the reference
+    holds it: a scipy CSR matrix (global columns) for a .npz, a dense ndarray
+    for a .npy (v3/gpu/mpi/common.py:123-125):
+    ``x, info = kskipmrr(comm, load_local_block(p, comm), b)``."""
     import scipy.sparse as sp
     if comm is not None and hasattr(comm, "Get_rank"):
         rank, size = comm.Get_rank(), comm.Get_size()
@@ -115,7 +138,10 @@ def load_local_block(path: str, comm=None):
         rank, size = dist.get_rank(comm), dist.get_world_size(comm)
     n, m = matrix_shape(path)
     part = balanced_partition(n, size)
-    indptr, indices, data, ncols = read_csr_rows(path, part[rank], part[rank + 1])
+    blk = read_rows(path, part[rank], part[rank + 1])
+    if isinstance(blk, np.ndarray):
+        return blk
+    indptr, indices, data, ncols = blk
     return sp.csr_matrix((data, indices, indptr), shape=(part[rank + 1] - part[rank], ncols))
 
 

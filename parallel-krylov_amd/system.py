@@ -289,13 +289,20 @@ class KrylovSystem:
         """Launch geometry of shard s: elementwise and SpMV grids plus the
         interior rows of the split SpMV -- what fixes the engine's dot-product
         summation order (oracle/gpu_order.py restates it for the tests)."""
-        g, sg, sw = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        g, sg, sw, fm = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         call("kr_system_shard_sched", self.handle, s, ctypes.byref(g), ctypes.byref(sg),
-             ctypes.byref(sw))
+             ctypes.byref(sw), ctypes.byref(fm))
         lay = self.shard_layout(s)
         return dict(n=self.row_begin[s + 1] - self.row_begin[s], grid=g.value,
                     spmv_grid=sg.value, int_lo=lay["interior_lo"], int_hi=lay["interior_hi"],
                     stencil_walk=sw.value)
+
+    def shard_format(self, s: int) -> str:
+        """The SpMV kernel family serving shard s: "csr" (row walk), "stencil",
+        "dia" (diagonal-offset values) or "dense" (GEMV)."""
+        fm = ctypes.c_int()
+        call("kr_system_shard_sched", self.handle, s, None, None, None, ctypes.byref(fm))
+        return _lib.KR_FORMAT[fm.value]
 
     def csr_pointers(self, s: int) -> dict:
         """Raw device CSR of shard s (local columns after finalize)."""

@@ -134,6 +134,8 @@ def test_stencil_spmv_bitwise_scipy(monkeypatch, name, shards):
     assert [s["stencil_walk"] for s in sc] == \
         [s.stencil_walk for s in gpu_order.shard_scheds(A, _bal(n, shards))]
     assert sc[0]["stencil_walk"] > 0 or shards > 1
+    assert [sysm.shard_format(s) for s in range(shards)] == \
+        ["stencil" if s_["stencil_walk"] else "csr" for s_ in sc]
     x = np.random.default_rng(5).standard_normal(n)
     y = sysm.gather(sysm.spmv(sysm.split(x))).cpu().numpy()
     sysm.close()
