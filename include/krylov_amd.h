@@ -156,13 +156,20 @@ int kr_halo_exchange_f64(kr_comm* comm, double* x_dev, const int64_t* recv, int 
 /* ------------------------------------------------------------------------
  * Distributed system: A and every vector row-partitioned into contiguous
  * shards (replaces MultiGpu.init/alloc, v3/gpu/common.py:62-109 and
- * v3/gpu/mpi/common.py:73-134). A process owns `nshards` shards; with a
- * communicator it owns exactly one and its peers own the rest.
+ * v3/gpu/mpi/common.py:73-134). A process owns `nshards` shards. Without a
+ * communicator they are the whole system; with one, every rank owns its
+ * shards (1..16, e.g. the GPU_IDS range of MultiGpu.alloc,
+ * v3/gpu/mpi/common.py:100-118), global shards are numbered rank after rank,
+ * halo pieces between two shards of one rank are device copies and the
+ * others RCCL send/recv; dot products are summed in global shard order
+ * either way, so a partition gives the same bits in one process or over
+ * ranks.
  * ------------------------------------------------------------------------ */
 typedef struct kr_system kr_system;
 
 /* row_begin[0..nshards] are GLOBAL row offsets of this process's shards
- * (contiguous, increasing). devices[s] is the HIP device of shard s. */
+ * (contiguous, increasing; with a communicator, rank r's block follows rank
+ * r-1's). devices[s] is the HIP device of shard s. Collective over `comm`. */
 int kr_system_create(kr_system** sys, int64_t n_global, int nshards, const int* devices,
                      const int64_t* row_begin, kr_comm* comm);
 int kr_system_destroy(kr_system* sys);

@@ -418,7 +418,7 @@ int kr_system_create(kr_system** out, int64_t n_global, int nshards, const int* 
                      const int64_t* row_begin, kr_comm* comm) {
   return guarded([&] {
     KR_REQUIRE(out && devices && row_begin && nshards >= 1 && n_global >= 0, "bad arguments");
-    if (comm) KR_REQUIRE(nshards == 1, "with a communicator a process owns one shard");
+    if (comm) KR_REQUIRE(nshards <= kMaxLocal, "too many local shards for one rank");
     for (int s = 0; s < nshards; ++s)
       KR_REQUIRE(row_begin[s] <= row_begin[s + 1], "row_begin must be non-decreasing");
     auto sys = std::make_unique<kr_system>();
@@ -434,34 +434,51 @@ int kr_system_create(kr_system** out, int64_t n_global, int nshards, const int* 
       KR_HIP_CHECK(hipStreamCreateWithFlags(&sh.stream, hipStreamNonBlocking));
     }
     if (comm) {
-      // global partition from every rank's [row0, row1)
+      // global partition from every rank's local shards: record = [count,
+      // boundaries...], kMaxLocal + 2 int64 per rank, in rank order
       Shard& sh = sys->shards[0];
-      const int P = comm->nranks;
+      const int R = comm->nranks;
+      constexpr int W = kMaxLocal + 2;
       int64_t* d = nullptr;
-      KR_HIP_CHECK(hipMalloc(&d, sizeof(int64_t) * (2 + 2 * P)));
-      int64_t mine[2] = {sh.row0, sh.row0 + sh.n};
-      KR_HIP_CHECK(hipMemcpy(d, mine, sizeof(mine), hipMemcpyHostToDevice));
-      KR_NCCL_CHECK(ncclAllGather(d, d + 2, 2, ncclInt64, comm->nccl, sh.stream));
-      std::vector<int64_t> all(2 * P);
-      KR_HIP_CHECK(hipMemcpyAsync(all.data(), d + 2, sizeof(int64_t) * 2 * P,
+      KR_HIP_CHECK(hipSetDevice(sh.dev));
+      KR_HIP_CHECK(hipMalloc(&d, sizeof(int64_t) * W * (1 + R)));
+      std::vector<int64_t> mine(W, 0);
+      mine[0] = nshards;
+      for (int s = 0; s <= nshards; ++s) mine[1 + s] = row_begin[s];
+      KR_HIP_CHECK(hipMemcpy(d, mine.data(), sizeof(int64_t) * W, hipMemcpyHostToDevice));
+      KR_NCCL_CHECK(ncclAllGather(d, d + W, W, ncclInt64, comm->nccl, sh.stream));
+      std::vector<int64_t> all((size_t)W * R);
+      KR_HIP_CHECK(hipMemcpyAsync(all.data(), d + W, sizeof(int64_t) * W * R,
                                   hipMemcpyDeviceToHost, sh.stream));
       KR_HIP_CHECK(hipStreamSynchronize(sh.stream));
       KR_HIP_CHECK(hipFree(d));
-      sys->part.assign(P + 1, 0);
-      for (int r = 0; r < P; ++r) {
-        KR_REQUIRE(all[2 * r] == (r == 0 ? 0 : all[2 * r - 1]),
+      sys->part.assign(1, 0);
+      sys->rank_first.assign(1, 0);
+      sys->owner.clear();
+      for (int r = 0; r < R; ++r) {
+        const int64_t* rec = &all[(size_t)W * r];
+        const int cnt = (int)rec[0];
+        KR_REQUIRE(cnt >= 1 && cnt <= kMaxLocal, "bad local shard count of a rank");
+        KR_REQUIRE(rec[1] == sys->part.back(),
                    "rank row blocks must be contiguous and in rank order");
-        sys->part[r] = all[2 * r];
+        for (int s = 0; s < cnt; ++s) {
+          sys->part.push_back(rec[2 + s]);
+          sys->owner.push_back(r);
+        }
+        sys->rank_first.push_back((int)sys->owner.size());
       }
-      sys->part[P] = all[2 * P - 1];
-      KR_REQUIRE(sys->part[P] == n_global, "rank row blocks must cover n_global");
-      sys->first_global = comm->rank;
+      KR_REQUIRE(sys->part.back() == n_global, "rank row blocks must cover n_global");
+      sys->first_global = sys->rank_first[comm->rank];
     } else {
       KR_REQUIRE(row_begin[0] == 0 && row_begin[nshards] == n_global,
                  "in-process shards must cover [0, n_global)");
       sys->part.assign(row_begin, row_begin + nshards + 1);
       sys->first_global = 0;
-      // peer access between distinct devices (best effort)
+    }
+    {
+      // peer access between the distinct devices of the local shards (best
+      // effort; halo copies and, with a communicator, the RCCL transfers of
+      // shards on other devices than the first go through it)
       for (int a = 0; a < nshards; ++a)
         for (int b = 0; b < nshards; ++b) {
           const int da = devices[a], db = devices[b];

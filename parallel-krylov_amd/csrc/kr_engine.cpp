@@ -151,6 +151,10 @@ void plan_halo(int P, const int64_t* part, const int64_t* need_lo, const int64_t
 
 System::~System() {
   session.reset();
+  if (hy_send) (void)hipFree(hy_send);
+  if (hy_recv) (void)hipFree(hy_recv);
+  if (hy_host) (void)hipHostFree(hy_host);
+  if (hy_ev) (void)hipEventDestroy(hy_ev);
   for (auto& s : shards) {
     (void)hipSetDevice(s.dev);
     if (s.stream) (void)hipStreamSynchronize(s.stream);
@@ -473,20 +477,29 @@ void System::finalize() {
   // 2. everybody's needed range [lo, hi]
   std::vector<int64_t> lo(P), hi(P);
   if (comm) {
+    // every rank's local shards, kMaxLocal (lo, hi) pairs per rank
     Shard& s = shards[0];
+    const int R = comm->nranks;
+    constexpr int W = 2 * kMaxLocal;
+    KR_HIP_CHECK(hipSetDevice(s.dev));
     int64_t* d = nullptr;
-    KR_HIP_CHECK(hipMalloc(&d, (size_t)(2 + 2 * P) * sizeof(int64_t)));
-    int64_t mine[2] = {s.col_lo, s.col_hi};
-    KR_HIP_CHECK(hipMemcpy(d, mine, sizeof(mine), hipMemcpyHostToDevice));
-    KR_NCCL_CHECK(ncclAllGather(d, d + 2, 2, ncclInt64, comm->nccl, s.stream));
-    std::vector<int64_t> all(2 * P);
-    KR_HIP_CHECK(hipMemcpyAsync(all.data(), d + 2, all.size() * 8, hipMemcpyDeviceToHost,
+    KR_HIP_CHECK(hipMalloc(&d, (size_t)W * (1 + R) * sizeof(int64_t)));
+    std::vector<int64_t> mine(W, 0);
+    for (size_t li = 0; li < shards.size(); ++li) {
+      mine[2 * li] = shards[li].col_lo;
+      mine[2 * li + 1] = shards[li].col_hi;
+    }
+    KR_HIP_CHECK(hipMemcpy(d, mine.data(), W * sizeof(int64_t), hipMemcpyHostToDevice));
+    KR_NCCL_CHECK(ncclAllGather(d, d + W, W, ncclInt64, comm->nccl, s.stream));
+    std::vector<int64_t> all((size_t)W * R);
+    KR_HIP_CHECK(hipMemcpyAsync(all.data(), d + W, all.size() * 8, hipMemcpyDeviceToHost,
                                 s.stream));
     KR_HIP_CHECK(hipStreamSynchronize(s.stream));
     KR_HIP_CHECK(hipFree(d));
     for (int t = 0; t < P; ++t) {
-      lo[t] = all[2 * t];
-      hi[t] = all[2 * t + 1];
+      const int r = owner[t], l = t - rank_first[r];
+      lo[t] = all[(size_t)W * r + 2 * l];
+      hi[t] = all[(size_t)W * r + 2 * l + 1];
     }
   } else {
     for (int t = 0; t < P; ++t) {
@@ -509,6 +522,8 @@ void System::finalize() {
       for (auto& p : s.recv) p.peer -= first_global;
       s.send.clear();
     }
+    // with a communicator the peers stay global shard indices: a peer owned
+    // by this rank is a device copy (halo_hybrid), any other RCCL
     // 4. interior rows (every column owned), computed on global columns
     KR_HIP_CHECK(hipSetDevice(s.dev));
     if (s.dense) {  // no interior rows when there are other shards
@@ -569,11 +584,42 @@ void System::finalize() {
     KR_HIP_CHECK(hipMemsetAsync(s.partials, 0, sizeof(double) * (size_t)kMaxSlots * s.pstride,
                                 s.stream));
     KR_HIP_CHECK(hipMalloc(&s.slots, sizeof(double) * kMaxSlots));
-    KR_HIP_CHECK(hipMalloc(&s.gather, sizeof(double) * kMaxSlots * nranks));
+    // RCCL ranks' (or, on the first shard, in-process shards') slot totals
+    KR_HIP_CHECK(hipMalloc(&s.gather,
+                           sizeof(double) * kMaxSlots * std::max<size_t>(nranks, shards.size())));
     KR_HIP_CHECK(hipHostMalloc(&s.host, sizeof(double) * kMaxSlots * nranks, 0));
     if (!s.ev_a) KR_HIP_CHECK(hipEventCreateWithFlags(&s.ev_a, hipEventDisableTiming));
     if (!s.ev_b) KR_HIP_CHECK(hipEventCreateWithFlags(&s.ev_b, hipEventDisableTiming));
     KR_HIP_CHECK(hipStreamSynchronize(s.stream));
+  }
+  if (hybrid()) {  // reduce(): the local slot totals, gathered over the ranks
+    Shard& s0 = shards[0];
+    KR_HIP_CHECK(hipSetDevice(s0.dev));
+    KR_HIP_CHECK(hipMalloc(&hy_send, sizeof(double) * kMaxLocal * kMaxSlots));
+    KR_HIP_CHECK(hipMemset(hy_send, 0, sizeof(double) * kMaxLocal * kMaxSlots));
+    KR_HIP_CHECK(hipMalloc(&hy_recv, sizeof(double) * kMaxLocal * kMaxSlots * nranks));
+    KR_HIP_CHECK(hipHostMalloc(&hy_host, sizeof(double) * kMaxLocal * kMaxSlots * nranks, 0));
+    if (!hy_ev) KR_HIP_CHECK(hipEventCreateWithFlags(&hy_ev, hipEventDisableTiming));
+  }
+  // The split SpMV needs interior rows on every shard; with RCCL ranks the
+  // decision is global, so the summation order (interior + boundary partials)
+  // is the one of the same partition in one process (oracle/gpu_order.py).
+  all_interior = true;
+  for (auto& s : shards) all_interior = all_interior && s.int_lo < s.int_hi;
+  if (comm && comm->nranks > 1) {
+    Shard& s0 = shards[0];
+    KR_HIP_CHECK(hipSetDevice(s0.dev));
+    int64_t* d = nullptr;
+    KR_HIP_CHECK(hipMalloc(&d, sizeof(int64_t) * (1 + nranks)));
+    const int64_t mine = all_interior ? 1 : 0;
+    KR_HIP_CHECK(hipMemcpy(d, &mine, sizeof(int64_t), hipMemcpyHostToDevice));
+    KR_NCCL_CHECK(ncclAllGather(d, d + 1, 1, ncclInt64, comm->nccl, s0.stream));
+    std::vector<int64_t> all(nranks);
+    KR_HIP_CHECK(hipMemcpyAsync(all.data(), d + 1, sizeof(int64_t) * nranks,
+                                hipMemcpyDeviceToHost, s0.stream));
+    KR_HIP_CHECK(hipStreamSynchronize(s0.stream));
+    KR_HIP_CHECK(hipFree(d));
+    for (int64_t f : all) all_interior = all_interior && f != 0;
   }
   {
     const char* env = getenv("KR_OVERLAP");  // 0 disables the split SpMV (A/B)
@@ -675,7 +721,103 @@ void System::harvest_profile() {
   }
 }
 
+// Several local shards with a communicator: halo pieces from a shard of this
+// rank are device copies (as in-process), the others RCCL send/recv, all of
+// them on the first local shard's stream (one RCCL rank per process). Both
+// sides of a rank pair list their transfers in one order -- vector, then
+// receiving global shard, then sending global shard -- so the RCCL
+// send/recv pairs match.
+void System::halo_hybrid(int id1, int id2, int id3, bool async) {
+  Shard& s0 = shards[0];
+  auto stream_of = [&](Shard& s) { return async ? s.comm_stream : s.stream; };
+  const int me = comm->rank;
+  for (auto& s : shards) {
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    if (!async) KR_HIP_CHECK(hipEventRecord(s.ev_a, s.stream));
+  }
+  auto ready = [&](Shard& s) { return async ? s.ev_in : s.ev_a; };
+  // local pieces: device copies on the receiving shard's stream
+  for (auto& s : shards) {
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    hipStream_t st = stream_of(s);
+    if (async) KR_HIP_CHECK(hipStreamWaitEvent(st, s.ev_in, 0));
+    for (auto& p : s.recv) {
+      if (owner[p.peer] != me) continue;
+      Shard& t = shards[p.peer - first_global];
+      KR_HIP_CHECK(hipStreamWaitEvent(st, ready(t), 0));
+      for (int id : {id1, id2, id3}) {
+        if (id < 0) continue;
+        double* dst = s.vec[id] + s.local_index(p.g0);
+        const double* src = t.vec[id] + t.local_index(p.g0);
+        if (s.dev == t.dev)
+          KR_HIP_CHECK(hipMemcpyAsync(dst, src, 8 * (size_t)p.count, hipMemcpyDeviceToDevice, st));
+        else
+          KR_HIP_CHECK(hipMemcpyPeerAsync(dst, s.dev, src, t.dev, 8 * (size_t)p.count, st));
+      }
+    }
+    KR_HIP_CHECK(hipEventRecord(async ? s.ev_out : s.ev_b, st));
+  }
+  // remote pieces: one RCCL group on the first shard's stream
+  struct Xfer {
+    int recv_shard, send_shard, peer_rank;
+    double* ptr;
+    int64_t count;
+  };
+  std::vector<Xfer> sends, recvs;
+  for (size_t li = 0; li < shards.size(); ++li) {
+    Shard& s = shards[li];
+    const int g = first_global + (int)li;
+    for (auto& p : s.send)
+      if (owner[p.peer] != me) sends.push_back({p.peer, g, owner[p.peer], nullptr, p.count});
+    for (auto& p : s.recv)
+      if (owner[p.peer] != me) recvs.push_back({g, p.peer, owner[p.peer], nullptr, p.count});
+  }
+  auto by_pair = [](const Xfer& a, const Xfer& b) {
+    return a.recv_shard != b.recv_shard ? a.recv_shard < b.recv_shard
+                                        : a.send_shard < b.send_shard;
+  };
+  std::sort(sends.begin(), sends.end(), by_pair);
+  std::sort(recvs.begin(), recvs.end(), by_pair);
+  KR_HIP_CHECK(hipSetDevice(s0.dev));
+  hipStream_t st0 = stream_of(s0);
+  if (!sends.empty() || !recvs.empty()) {
+    for (auto& s : shards) KR_HIP_CHECK(hipStreamWaitEvent(st0, ready(s), 0));
+    KR_NCCL_CHECK(ncclGroupStart());
+    for (int id : {id1, id2, id3}) {
+      if (id < 0) continue;
+      for (auto& x : sends) {
+        Shard& s = shards[x.send_shard - first_global];
+        auto it = std::find_if(s.send.begin(), s.send.end(),
+                               [&](const HaloPiece& p) { return p.peer == x.recv_shard; });
+        KR_NCCL_CHECK(ncclSend(s.vec[id] + s.local_index(it->g0), (size_t)it->count, ncclFloat64,
+                               x.peer_rank, comm->nccl, st0));
+      }
+      for (auto& x : recvs) {
+        Shard& s = shards[x.recv_shard - first_global];
+        for (auto& p : s.recv)
+          if (p.peer == x.send_shard)
+            KR_NCCL_CHECK(ncclRecv(s.vec[id] + s.local_index(p.g0), (size_t)p.count, ncclFloat64,
+                                   x.peer_rank, comm->nccl, st0));
+      }
+    }
+    KR_NCCL_CHECK(ncclGroupEnd());
+  }
+  KR_HIP_CHECK(hipEventRecord(hy_ev, st0));
+  if (async) return;  // spmv() makes every shard wait for every ev_out and hy_ev
+  // Nobody reads or overwrites a vector before every transfer is done.
+  for (auto& t : shards) {
+    KR_HIP_CHECK(hipSetDevice(t.dev));
+    KR_HIP_CHECK(hipStreamWaitEvent(t.stream, hy_ev, 0));
+    for (auto& s : shards)
+      if (&s != &t) KR_HIP_CHECK(hipStreamWaitEvent(t.stream, s.ev_b, 0));
+  }
+}
+
 void System::halo(int id1, int id2, int id3) {
+  if (hybrid()) {
+    halo_hybrid(id1, id2, id3, false);
+    return;
+  }
   if (comm) {
     Shard& s = shards[0];
     if (s.recv.empty() && s.send.empty()) return;
@@ -733,6 +875,10 @@ void System::halo(int id1, int id2, int id3) {
 }
 
 void System::halo_async(int id1, int id2, int id3) {
+  if (hybrid()) {
+    halo_hybrid(id1, id2, id3, true);
+    return;
+  }
   if (comm) {
     Shard& s = shards[0];
     KR_HIP_CHECK(hipSetDevice(s.dev));
@@ -791,15 +937,14 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
   const int hx2 = (dual || virt) ? in2 : -1;  // vectors whose halo the SpMV reads
   const int hx3 = virt ? st->x3 : -1;
   KR_REQUIRE(slot0 + spmv_products(epi) <= kMaxSlots, "reduction slots exhausted");
-  const bool exchange =
-      comm ? !(shards[0].recv.empty() && shards[0].send.empty()) : shards.size() > 1;
+  // one decision for every shard of every rank (the same summation order as
+  // the partition in one process), even where a shard has no halo piece
+  const bool exchange = nglobal_shards() > 1;
   // Split SpMV: the halo exchange runs on a side stream while the interior
   // rows (no halo column) are multiplied; the boundary rows follow it. The
   // boundary launches ADD their reduction partials to the interior launch's
   // (same stream, fixed order: deterministic).
-  bool split = exchange && overlap;
-  for (auto& s : shards)
-    if (s.int_lo >= s.int_hi) split = false;
+  const bool split = exchange && overlap && all_interior;
   const char* nm = epi_name(epi);
 
   auto args_for = [&](Shard& s, int64_t r_begin, int64_t rows, int grid, int acc) {
@@ -864,7 +1009,7 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
       a.scratch = s.scratch;
     }
     a.epi_late = epi_late;
-    a.stop = dev_stop;
+    a.stop = dev_stop ? s.st + ST_STOP : nullptr;
     a.nnz_total = s.nnz;
     if (s.dense) {
       a.dense = 1;
@@ -936,11 +1081,12 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
   for (size_t li = 0; li < shards.size(); ++li) {
     Shard& s = shards[li];
     KR_HIP_CHECK(hipSetDevice(s.dev));
-    if (comm) {
+    if (comm && !hybrid()) {
       KR_HIP_CHECK(hipStreamWaitEvent(s.stream, s.ev_out, 0));
     } else {
       // own halo copied, and every reader done with this shard's rows
       for (auto& t : shards) KR_HIP_CHECK(hipStreamWaitEvent(s.stream, t.ev_out, 0));
+      if (comm) KR_HIP_CHECK(hipStreamWaitEvent(s.stream, hy_ev, 0));  // RCCL pieces
     }
     // both boundary ranges in one launch: row blocks [0, int_lo/B) and
     // [int_hi/B, end) (interior bounds are whole blocks, see finalize)
@@ -984,40 +1130,50 @@ void System::ew(EwOp op, double c0, double c1, std::array<int, 6> ids, int slot0
 bool System::device_scalars() const {
   const char* env = getenv("KR_DEVICE_SCALARS");  // 0: one host sync per reduction (A/B)
   if (env && atoi(env) == 0) return false;
-  return shards.size() == 1;  // one shard, alone or one RCCL rank of several
+  // one shard per RCCL rank, or any number of shards in one process
+  return comm ? !hybrid() : true;
 }
 
 void System::scalar_state_init(double gamma) {
-  Shard& s = shards[0];
-  KR_HIP_CHECK(hipSetDevice(s.dev));
-  if (!s.st) {
-    KR_HIP_CHECK(hipMalloc(&s.st, sizeof(double) * kScalarState));
-    KR_HIP_CHECK(hipHostMalloc(&s.hst, sizeof(double) * kScalarState, 0));
+  Shard& s0 = shards[0];
+  for (auto& s : shards) {
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    if (!s.st) KR_HIP_CHECK(hipMalloc(&s.st, sizeof(double) * kScalarState));
   }
-  KR_HIP_CHECK(hipStreamSynchronize(s.stream));  // hst is free
-  for (int q = 0; q < kScalarState; ++q) s.hst[q] = 0.0;
-  s.hst[ST_GAMMA] = gamma;
-  KR_HIP_CHECK(hipMemcpyAsync(s.st, s.hst, sizeof(double) * kScalarState,
-                              hipMemcpyHostToDevice, s.stream));
+  KR_HIP_CHECK(hipSetDevice(s0.dev));
+  if (!s0.hst) KR_HIP_CHECK(hipHostMalloc(&s0.hst, sizeof(double) * kScalarState, 0));
+  KR_HIP_CHECK(hipStreamSynchronize(s0.stream));  // hst is free
+  for (int q = 0; q < kScalarState; ++q) s0.hst[q] = 0.0;
+  s0.hst[ST_GAMMA] = gamma;
+  for (auto& s : shards) {
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    KR_HIP_CHECK(hipMemcpyAsync(s.st, s0.hst, sizeof(double) * kScalarState,
+                                hipMemcpyHostToDevice, s.stream));
+  }
+  KR_HIP_CHECK(hipSetDevice(s0.dev));
+  KR_HIP_CHECK(hipStreamSynchronize(s0.stream));  // hst is rewritten by the next init
+  for (auto& s : shards) KR_HIP_CHECK(hipStreamSynchronize(s.stream));
 }
 
 void System::ew_dev(EwOp op, int coef, std::array<int, 6> ids, int slot0) {
   KR_REQUIRE(slot0 + ew_products(op) <= kMaxSlots, "reduction slots exhausted");
-  Shard& s = shards[0];
-  EwArgs a;
-  for (int q = 0; q < 6; ++q) a.p[q] = ids[q] >= 0 ? s.own(ids[q]) : nullptr;
-  a.n = s.n;
-  a.partials = s.partials + (size_t)slot0 * s.pstride;
-  a.grid = s.grid;
-  a.stride = s.pstride;
-  a.cdev = s.st + coef;
-  a.stop = dev_stop;
-  for (int p = 0; p < ew_products(op); ++p) s.slot_n[slot0 + p] = s.grid;
-  hipEvent_t t0 = nullptr;
-  const char* nm = ew_name(op);
-  prof_begin(s, nm, t0);
-  launch_ew(op, a, s.stream);
-  prof_end(s, nm, t0, 8.0 * ew_vectors(op) * s.n);
+  for (auto& s : shards) {
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    EwArgs a;
+    for (int q = 0; q < 6; ++q) a.p[q] = ids[q] >= 0 ? s.own(ids[q]) : nullptr;
+    a.n = s.n;
+    a.partials = s.partials + (size_t)slot0 * s.pstride;
+    a.grid = s.grid;
+    a.stride = s.pstride;
+    a.cdev = s.st + coef;
+    a.stop = dev_stop ? s.st + ST_STOP : nullptr;
+    for (int p = 0; p < ew_products(op); ++p) s.slot_n[slot0 + p] = s.grid;
+    hipEvent_t t0 = nullptr;
+    const char* nm = ew_name(op);
+    prof_begin(s, nm, t0);
+    launch_ew(op, a, s.stream);
+    prof_end(s, nm, t0, 8.0 * ew_vectors(op) * s.n);
+  }
 }
 
 void System::scalar(ScalarOp op, int need, int64_t it, int h, double thr, int check) {
@@ -1033,13 +1189,12 @@ void System::scalar(ScalarOp op, int need, int64_t it, int h, double thr, int ch
   a.h = h;
   a.check = check;
   a.thr = thr;
-  hipEvent_t t0 = nullptr;
-  prof_begin(s, "scalar", t0);
+  const int nslots = 32 - __builtin_clz((unsigned)need);
   if (comm) {
     // every rank: its slot totals (finalize order), all-gathered on the
     // compute stream (after this SpMV's halo, before the next one's: one
     // RCCL order on every rank), then the same scalar step everywhere
-    const int nslots = 32 - __builtin_clz((unsigned)need);
+    KR_HIP_CHECK(hipSetDevice(s.dev));
     SlotCounts cnt{};
     for (int q = 0; q < nslots; ++q) cnt.n[q] = s.slot_n[q];
     launch_finalize_counts(s.partials, s.pstride, cnt, nslots, s.slots, s.stream);
@@ -1048,9 +1203,44 @@ void System::scalar(ScalarOp op, int need, int64_t it, int h, double thr, int ch
     a.gathered = s.gather;
     a.nranks = comm->nranks;
     a.gstride = nslots;
+  } else if (shards.size() > 1) {
+    // in-process shards: each one's slot totals (finalize order) side by
+    // side on the first shard, summed there in shard order like reduce()
+    for (auto& t : shards) {
+      KR_HIP_CHECK(hipSetDevice(t.dev));
+      SlotCounts cnt{};
+      for (int q = 0; q < nslots; ++q) cnt.n[q] = t.slot_n[q];
+      launch_finalize_counts(t.partials, t.pstride, cnt, nslots, t.slots, t.stream);
+      KR_HIP_CHECK(hipEventRecord(t.ev_a, t.stream));
+    }
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    for (size_t li = 0; li < shards.size(); ++li) {
+      Shard& t = shards[li];
+      KR_HIP_CHECK(hipStreamWaitEvent(s.stream, t.ev_a, 0));
+      KR_HIP_CHECK(hipMemcpyPeerAsync(s.gather + li * nslots, s.dev, t.slots, t.dev,
+                                      sizeof(double) * nslots, s.stream));
+    }
+    a.gathered = s.gather;
+    a.nranks = (int)shards.size();
+    a.gstride = nslots;
   }
+  KR_HIP_CHECK(hipSetDevice(s.dev));
+  hipEvent_t t0 = nullptr;
+  prof_begin(s, "scalar", t0);
   launch_scalar(a, s.stream);
   prof_end(s, "scalar", t0, 8.0 * s.pstride * __builtin_popcount(need));
+  if (!comm && shards.size() > 1) {
+    // the coefficients and the stop flag to every other shard (its vector
+    // kernels read its own copy); st[ST_HIST...] stays on the first shard
+    KR_HIP_CHECK(hipEventRecord(s.ev_b, s.stream));
+    for (size_t li = 1; li < shards.size(); ++li) {
+      Shard& t = shards[li];
+      KR_HIP_CHECK(hipSetDevice(t.dev));
+      KR_HIP_CHECK(hipStreamWaitEvent(t.stream, s.ev_b, 0));
+      KR_HIP_CHECK(hipMemcpyPeerAsync(t.st, t.dev, s.st, s.dev, sizeof(double) * ST_HIST,
+                                      t.stream));
+    }
+  }
 }
 
 void System::scalar_state_read() {
@@ -1105,7 +1295,10 @@ std::vector<double> System::reduce(int nslots) {
     SlotCounts cnt{};
     for (int q = 0; q < nslots; ++q) cnt.n[q] = s.slot_n[q];
     launch_finalize_counts(s.partials, s.pstride, cnt, nslots, s.slots, s.stream);
-    if (comm) {
+    if (hybrid()) {
+      // gathered below, from the first shard's stream
+      KR_HIP_CHECK(hipEventRecord(s.ev_a, s.stream));
+    } else if (comm) {
       KR_NCCL_CHECK(ncclAllGather(s.slots, s.gather, (size_t)nslots, ncclFloat64, comm->nccl,
                                   s.stream));
       KR_HIP_CHECK(hipMemcpyAsync(s.host, s.gather, sizeof(double) * nslots * comm->nranks,
@@ -1116,12 +1309,33 @@ std::vector<double> System::reduce(int nslots) {
     }
     prof_end(s, "reduce", t0, 8.0 * nslots * s.pstride);
   }
+  if (hybrid()) {
+    // every local shard's slots side by side (kMaxLocal x nslots), one
+    // all-gather for the rank; the stride stays fixed so any rank can index
+    Shard& s0 = shards[0];
+    KR_HIP_CHECK(hipSetDevice(s0.dev));
+    for (size_t li = 0; li < shards.size(); ++li) {
+      Shard& s = shards[li];
+      KR_HIP_CHECK(hipStreamWaitEvent(s0.stream, s.ev_a, 0));
+      KR_HIP_CHECK(hipMemcpyPeerAsync(hy_send + li * nslots, s0.dev, s.slots, s.dev,
+                                      sizeof(double) * nslots, s0.stream));
+    }
+    const size_t per = (size_t)kMaxLocal * nslots;
+    KR_NCCL_CHECK(ncclAllGather(hy_send, hy_recv, per, ncclFloat64, comm->nccl, s0.stream));
+    KR_HIP_CHECK(hipMemcpyAsync(hy_host, hy_recv, sizeof(double) * per * comm->nranks,
+                                hipMemcpyDeviceToHost, s0.stream));
+  }
   for (auto& s : shards) {
     KR_HIP_CHECK(hipSetDevice(s.dev));
     KR_HIP_CHECK(hipStreamSynchronize(s.stream));
   }
   // Fixed order: global shard 0, 1, ... (identical for in-process and RCCL).
-  if (comm) {
+  if (hybrid()) {
+    const size_t per = (size_t)kMaxLocal * nslots;
+    for (int r = 0; r < comm->nranks; ++r)
+      for (int l = 0; l < rank_first[r + 1] - rank_first[r]; ++l)
+        for (int q = 0; q < nslots; ++q) tot[q] = tot[q] + hy_host[r * per + l * nslots + q];
+  } else if (comm) {
     const double* h = shards[0].host;
     for (int r = 0; r < comm->nranks; ++r)
       for (int q = 0; q < nslots; ++q) tot[q] = tot[q] + h[r * nslots + q];
@@ -1192,7 +1406,7 @@ class CgSession : public Base {
   void run_batch() {
     const int64_t m = std::min<int64_t>({(int64_t)scalar_batch(), std::max<int64_t>(hint, 1),
                                          prm.maxiter - i});
-    sys->dev_stop = sys->shards[0].st + ST_STOP;
+    sys->dev_stop = true;
     for (int64_t j = 0; j < m; ++j) {
       if (j > 0) sys->prof_active = (sys->prof_tick++ % sys->profile_every) == 0;
       sys->spmv(EPI_XY, P, -1, V, -1, -1, -1, 0);              // v = A p ; sigma
@@ -1201,7 +1415,7 @@ class CgSession : public Base {
       sys->scalar(SC_CG_BETA, 1 << 0, i + j, (int)j, thr);      // beta, gamma, test
       sys->ew_dev(EW_CG_P, ST_C2, {P, R, -1, -1, -1, -1}, 0);  // p = r + b p
     }
-    sys->dev_stop = nullptr;
+    sys->dev_stop = false;
     sys->scalar_state_read();
     const double* h = sys->shards[0].hst;
     q.assign(h + ST_HIST, h + ST_HIST + m);
@@ -1284,7 +1498,7 @@ class MrrSession : public Base {
   void run_batch() {
     const int64_t m = std::min<int64_t>({(int64_t)scalar_batch(), std::max<int64_t>(hint, 1),
                                          prm.maxiter - i});
-    sys->dev_stop = sys->shards[0].st + ST_STOP;
+    sys->dev_stop = true;
     for (int64_t j = 0; j < m; ++j) {
       if (j > 0) sys->prof_active = (sys->prof_tick++ % sys->profile_every) == 0;
       sys->spmv(EPI_MRR_LOOP, R, -1, AR, -1, Y, -1, 0);            // Ar = A r ; <r,r> mu nu
@@ -1293,7 +1507,7 @@ class MrrSession : public Base {
       sys->scalar(SC_MRR_ZETA, 0x18, i + j, (int)j, thr);          // zeta, eta
       sys->ew_dev(EW_MRR, ST_C2, {Y, AR, Z, R, X, X}, 0);
     }
-    sys->dev_stop = nullptr;
+    sys->dev_stop = false;
     sys->scalar_state_read();
     const double* h = sys->shards[0].hst;
     q.assign(h + ST_HIST, h + ST_HIST + m);

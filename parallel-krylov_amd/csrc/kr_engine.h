@@ -26,6 +26,8 @@ struct Comm {
   ncclComm_t nccl = nullptr;
   int rank = 0, nranks = 1, device = 0;
 };
+// Local shards per rank with a communicator (kr_system_create).
+constexpr int kMaxLocal = 16;
 
 #define KR_NCCL_CHECK(expr)                                                              \
   do {                                                                                   \
@@ -143,6 +145,21 @@ struct System {
   int64_t n_global = 0;
   std::vector<Shard> shards;
   Comm* comm = nullptr;             // null: single process
+  // With a communicator, a rank may own several shards (a GPU range,
+  // v3/gpu/mpi/common.py:77-134): global shards are numbered rank after
+  // rank, local shards in order; rank_first[r] = rank r's first global shard.
+  // Halo pieces between two local shards are device copies, the others RCCL
+  // send/recv on the first local shard's stream (one RCCL rank per process).
+  std::vector<int> owner;           // comm: rank of every global shard
+  std::vector<int> rank_first;      // comm: size nranks + 1
+  double* hy_send = nullptr;        // several local shards: slot totals [kMaxLocal][kMaxSlots]
+  double* hy_recv = nullptr;        // [nranks][kMaxLocal][kMaxSlots]
+  double* hy_host = nullptr;        // pinned copy of hy_recv
+  hipEvent_t hy_ev = nullptr;       // the RCCL group of the exchange is done (shards[0] streams)
+  // some rank holds several shards (then every rank takes the hybrid paths,
+  // so the RCCL call sequence is the same everywhere)
+  bool hybrid() const { return comm && nglobal_shards() != comm->nranks; }
+  void halo_hybrid(int id1, int id2, int id3, bool async);
   std::vector<int64_t> part;        // global partition, size P+1
   int first_global = 0;             // global index of shards[0]
   bool finalized = false;
@@ -151,6 +168,7 @@ struct System {
   int64_t prof_tick = 0;
   bool prof_active = true;
   bool overlap = true;              // split SpMV: interior rows || halo exchange
+  bool all_interior = false;        // every shard (all ranks) has interior rows
   bool fuse_steps = true;           // k-skip steps fused into the SpMV epilogue
   bool fuse_first = true;           // k-skip MrR steps 0+1 in one SpMV (EPI_STEP_MRR_FIRST2)
   int epi_late = 0;                 // SpmvArgs::epi_late (A/B knob)
@@ -173,16 +191,19 @@ struct System {
   void spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int b, int slot0,
             const StepOps* st = nullptr);
   void ew(EwOp op, double c0, double c1, std::array<int, 6> ids, int slot0);
-  // Device-resident scalars (single shard, no communicator): the vector
-  // kernel takes c0, c1 from st[coef], st[coef + 1]; scalar() runs one
-  // scalar_kernel step over the reductions in slots `need`. While dev_stop is
-  // set, every SpMV / vector kernel skips itself once the test has fired.
+  // Device-resident scalars (one shard per rank, or every shard in this
+  // process): the vector kernel takes c0, c1 from st[coef], st[coef + 1];
+  // scalar() runs one scalar_kernel step over the reductions in slots `need`
+  // on the first shard (in-process shards: their slot totals gathered there
+  // in shard order) and copies the control part of st to the other shards.
+  // While dev_stop is set, every SpMV / vector kernel skips itself once the
+  // test has fired (each shard reads its own st[ST_STOP]).
   bool device_scalars() const;
   void scalar_state_init(double gamma);
   void ew_dev(EwOp op, int coef, std::array<int, 6> ids, int slot0);
   void scalar(ScalarOp op, int need, int64_t it, int h, double thr, int check = 1);
   void scalar_state_read();  // st -> hst, synchronises the stream
-  const double* dev_stop = nullptr;
+  bool dev_stop = false;
   // Device->host of the summed slots [0, nslots): the one host sync point.
   std::vector<double> reduce(int nslots);
   void copy_own(int dst, int src);

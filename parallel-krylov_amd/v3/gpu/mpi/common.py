@@ -14,12 +14,14 @@ group) or an mpi4py-style communicator (``Get_rank``/``Get_size``/``bcast``/
 """
 from __future__ import annotations
 
+import os
 import sys
 import time
 
 import numpy as np
 
-from ....system import Communicator, KrylovSystem, balanced_partition, gpu_ids_range, local_device
+from ....system import (Communicator, KrylovSystem, balanced_partition, gpu_ids_range,
+                        local_device)
 from ...common import _finish, _start
 from ..common import _host_vector, _is_tensor, check_maxiter
 
@@ -89,6 +91,20 @@ class _Dist:
         return torch.cat([o[:c] for o, c in zip(out, counts)]).to(x_local.device)
 
 
+def rank_devices(rank):
+    """Devices of this rank's local shards: the GPU_IDS range (the reference's
+    per-rank GPU list, v3/gpu/mpi/common.py:77-83), else one GPU
+    (local_device). ``KRYLOV_AMD_RANK_SHARDS="0,0"`` overrides it (several
+    shards may share a device: the multi-GPU-per-rank path on one GPU)."""
+    env = os.environ.get("KRYLOV_AMD_RANK_SHARDS")
+    if env:
+        return [int(t) for t in env.split(",") if t.strip() != ""]
+    gpu_range = gpu_ids_range()
+    if gpu_range is not None and len(gpu_range) > 1:
+        return gpu_range
+    return [local_device(rank)]
+
+
 def run(method, banner, comm, local_A, b, x=None, tol=1e-05, maxiter=None, k=None,
         exit_nonroot=False):
     """Shared body of the five v3/gpu/mpi solver functions.
@@ -109,20 +125,12 @@ def run(method, banner, comm, local_A, b, x=None, tol=1e-05, maxiter=None, k=Non
     if sum(counts) != N:
         raise ValueError(f"row blocks cover {sum(counts)} rows but b has {N}")
     row0 = sum(counts[: d.rank])
-    gpu_range = gpu_ids_range()
-    if gpu_range is not None and len(gpu_range) > 1:
-        # GPU_IDS=first,...,last: the rank splits its row block over that range
-        # (MultiGpu.alloc, v3/gpu/mpi/common.py:100-118). Supported for a single
-        # rank (in-process shards); with several ranks each rank owns one GPU.
-        if d.size > 1:
-            raise NotImplementedError(
-                "GPU_IDS with several GPUs per rank needs one rank: launch one rank per "
-                "GPU instead (torchrun --nproc-per-node G, LOCAL_RANK picks the GPU)")
-        devices = gpu_range
-        comm_h = None
-    else:
-        devices = [local_device(d.rank)]
-        comm_h = d.communicator(devices[0])
+    devices = rank_devices(d.rank)
+    # one RCCL rank per process: a rank with several GPUs (GPU_IDS range,
+    # MultiGpu.alloc, v3/gpu/mpi/common.py:100-118) keeps them as local
+    # shards -- device copies between them, RCCL to the other ranks (a lone
+    # rank with several GPUs is the in-process system)
+    comm_h = None if (d.size == 1 and len(devices) > 1) else d.communicator(devices[0])
     torch.cuda.set_device(devices[0])
     rows = [row0 + r for r in balanced_partition(local_n, len(devices))]
     sysm = KrylovSystem(N, rows, devices, comm=comm_h)

@@ -240,20 +240,24 @@ def test_fused_steps_bitwise_equal_unfused(monkeypatch, shards, method, matrix, 
     ("cg", ["banded", 3000, 13, 64, 0], 1e-10, 400), ("mrr", ["poisson", 16, 2], 1e-10, 400),
     ("mrr", ["poisson", 12, 3], 1e-8, 9), ("mrr", ["banded", 3000, 13, 64, 0], 1e-9, 400),
     ("cg", ["poisson", 8, 2], 0.0, 40), ("mrr", ["poisson", 8, 2], 0.5, 40)])
-def test_device_scalars_bitwise_equal_host(monkeypatch, method, matrix, tol, maxiter):
+@pytest.mark.parametrize("shards", ["0", "0,0,0"])
+def test_device_scalars_bitwise_equal_host(monkeypatch, shards, method, matrix, tol, maxiter):
     """CG / MrR with device-resident scalars (batches of iterations, the
     convergence test on the device, one host sync per batch) perform the same
     operations in the same order as the host-scalar path (one sync per
     reduction): x and the whole history are bitwise identical, for batches of
     1, 3 and 32 iterations, convergence inside a batch, maxiter truncation,
-    tol = 0 and a test that fires at the first check."""
+    tol = 0 and a test that fires at the first check -- on one shard and on
+    three in-process shards (slot totals gathered on the first shard, summed
+    in shard order; coefficients and stop flag copied to the others)."""
     A = golden_matrix(matrix)
     b = np.random.default_rng(11).standard_normal(A.shape[0])
     kw = dict(tol=tol, maxiter=maxiter)
-    x0, i0 = _run_env(monkeypatch, {"KR_DEVICE_SCALARS": "0"}, method, A, b, **kw)
+    base = {"KRYLOV_AMD_SHARDS": shards}
+    x0, i0 = _run_env(monkeypatch, {**base, "KR_DEVICE_SCALARS": "0"}, method, A, b, **kw)
     for batch in ("1", "3", "32"):
-        x1, i1 = _run_env(monkeypatch, {"KR_DEVICE_SCALARS": "1", "KR_SCALAR_BATCH": batch},
-                          method, A, b, **kw)
+        x1, i1 = _run_env(monkeypatch, {**base, "KR_DEVICE_SCALARS": "1",
+                                        "KR_SCALAR_BATCH": batch}, method, A, b, **kw)
         np.testing.assert_array_equal(i1["nosl"], i0["nosl"])
         np.testing.assert_array_equal(i1["residual"], i0["residual"])
         np.testing.assert_array_equal(x1, x0)
