@@ -1163,7 +1163,10 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
     const int64_t off = bs - ws;
     const int js = active ? (int)max((int64_t)rlo - bs + off, (int64_t)0) : 0;
     const int je = active ? (int)min((int64_t)rhi - bs + off, (int64_t)kWindow) : 0;
-    const int64_t xrow = a.xoff + r0 + tid;
+    // lanes past the block's last row gather at row r0 (their products are
+    // dropped): x + xoff + r0 + tid may lie past the vector's end when the
+    // shard has no halo above it
+    const int64_t xrow = a.xoff + r0 + (active ? tid : 0);
 
     // (1) first gather batch of this window
     double v[G], p1[G], p2[G], p3[VIRT ? G : 1];

@@ -73,7 +73,10 @@ def main():
     dist.init_process_group("gloo")
     world = dist.get_world_size()
     failures = []
+    only = os.environ.get("KR_WORKER_CASES")  # diagnostics: e.g. "poisson:kskipcg"
     for mat, method, k in (CASES_LOCAL if counts else CASES):
+        if only and f"{mat}:{method}" not in only.split(","):
+            continue
         A = matrix(mat)
         n = A.shape[0]
         b = np.random.default_rng(5).standard_normal(n)
@@ -84,11 +87,11 @@ def main():
         if k:
             kw["k"] = k
         same = None
-        if counts and RANK == 0:
-            part = [0]
-            for r in range(world):
-                part += [rows[r] + t for t in balanced_partition(rows[r + 1] - rows[r],
-                                                                 counts[r])[1:]]
+        part = [0]
+        for r in range(world):
+            part += [rows[r] + t for t in balanced_partition(rows[r + 1] - rows[r],
+                                                             counts[r] if counts else 1)[1:]]
+        if counts and RANK == 0 and os.environ.get("KR_WORKER_INPROC", "1") != "0":
             same = in_process(A, b, part, method, kw)
         runs = []
         for dev_scalars in (("1", "0") if method in ("cg", "mrr") else ("1",)):

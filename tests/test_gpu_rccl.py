@@ -40,8 +40,11 @@ def test_mpi_family_several_shards_per_rank(shards):
            os.path.join(REPO, "tests", "rccl_2rank_worker.py"), "--shards", shards]
     p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=110)
     out = "\n".join(l for l in (p.stdout + p.stderr).splitlines() if "WARN" not in l)
-    assert p.returncode == 0, out[-3000:]
-    assert out.count("-> ok") == 9, out[-3000:]
+    # the solver lines and every rank's error, not torchrun's own traceback
+    brief = "\n".join(l for l in out.splitlines()
+                      if "nosl" in l or "Error" in l or l.startswith("[rank"))
+    assert p.returncode == 0, brief[-4000:]
+    assert out.count("-> ok") == 9, brief[-4000:]
 
 
 def test_bench_two_ranks_json_line():
