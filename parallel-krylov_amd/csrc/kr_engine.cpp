@@ -1243,6 +1243,41 @@ void System::scalar(ScalarOp op, int need, int64_t it, int h, double thr, int ch
   }
 }
 
+bool System::fused_scalars() const {
+  const char* env = getenv("KR_FUSE_SCALAR");
+  if (env && atoi(env) == 0) return false;
+  return !comm && shards.size() == 1;
+}
+
+void System::ew_pro(EwOp op, ScalarOp sop, std::array<int, 6> ids, int slot0, int64_t it, int h,
+                    int par, double thr) {
+  KR_REQUIRE(slot0 + ew_products(op) <= kMaxSlots, "reduction slots exhausted");
+  Shard& s = shards[0];
+  KR_HIP_CHECK(hipSetDevice(s.dev));
+  EwArgs a;
+  for (int q = 0; q < 6; ++q) a.p[q] = ids[q] >= 0 ? s.own(ids[q]) : nullptr;
+  a.n = s.n;
+  a.partials = s.partials + (size_t)slot0 * s.pstride;
+  a.grid = s.grid;
+  a.stride = s.pstride;
+  a.stop = dev_stop ? s.st + ST_STOP : nullptr;
+  a.pro = (int)sop + 1;
+  a.pro_part = s.partials;
+  a.pro_stride = s.pstride;
+  for (int q = 0; q < 5; ++q) a.pro_cnt[q] = s.slot_n[q];
+  a.st = s.st;
+  a.pro_it = it;
+  a.pro_h = h;
+  a.pro_par = par;
+  a.pro_thr = thr;
+  for (int p = 0; p < ew_products(op); ++p) s.slot_n[slot0 + p] = s.grid;
+  hipEvent_t t0 = nullptr;
+  const char* nm = ew_name(op);
+  prof_begin(s, nm, t0);
+  launch_ew(op, a, s.stream);
+  prof_end(s, nm, t0, 8.0 * ew_vectors(op) * s.n);
+}
+
 void System::scalar_state_read() {
   Shard& s = shards[0];
   KR_HIP_CHECK(hipMemcpyAsync(s.hst, s.st, sizeof(double) * kScalarState,
@@ -1407,9 +1442,16 @@ class CgSession : public Base {
     const int64_t m = std::min<int64_t>({(int64_t)scalar_batch(), std::max<int64_t>(hint, 1),
                                          prm.maxiter - i});
     sys->dev_stop = true;
+    const bool fused = sys->fused_scalars();
     for (int64_t j = 0; j < m; ++j) {
       if (j > 0) sys->prof_active = (sys->prof_tick++ % sys->profile_every) == 0;
       sys->spmv(EPI_XY, P, -1, V, -1, -1, -1, 0);              // v = A p ; sigma
+      if (fused) {  // the scalar steps inside the vector kernels: 3 launches
+        const int par = (int)((i + j) & 1);
+        sys->ew_pro(EW_CG, SC_CG_ALPHA, {X, P, R, V, -1, -1}, 0, i + j, (int)j, par, thr);
+        sys->ew_pro(EW_CG_P, SC_CG_BETA, {P, R, -1, -1, -1, -1}, 0, i + j, (int)j, par, thr);
+        continue;
+      }
       sys->scalar(SC_CG_ALPHA, 1 << 1, i + j, (int)j, thr);     // alpha = gamma / sigma
       sys->ew_dev(EW_CG, ST_C0, {X, P, R, V, -1, -1}, 0);       // x += a p ; r -= a v
       sys->scalar(SC_CG_BETA, 1 << 0, i + j, (int)j, thr);      // beta, gamma, test
@@ -1499,9 +1541,15 @@ class MrrSession : public Base {
     const int64_t m = std::min<int64_t>({(int64_t)scalar_batch(), std::max<int64_t>(hint, 1),
                                          prm.maxiter - i});
     sys->dev_stop = true;
+    const bool fused = sys->fused_scalars();
     for (int64_t j = 0; j < m; ++j) {
       if (j > 0) sys->prof_active = (sys->prof_tick++ % sys->profile_every) == 0;
       sys->spmv(EPI_MRR_LOOP, R, -1, AR, -1, Y, -1, 0);            // Ar = A r ; <r,r> mu nu
+      if (fused) {  // the scalar steps inside the vector kernels: 3 launches
+        sys->ew_pro(EW_MRR_S, SC_MRR_GAMMA, {AR, Y, R, -1, -1, -1}, 3, i + j, (int)j, 0, thr);
+        sys->ew_pro(EW_MRR, SC_MRR_ZETA, {Y, AR, Z, R, X, X}, 0, i + j, (int)j, 0, thr);
+        continue;
+      }
       sys->scalar(SC_MRR_GAMMA, 0x7, i + j, (int)j, thr);          // test ; gamma = nu / mu
       sys->ew_dev(EW_MRR_S, ST_C0, {AR, Y, R, -1, -1, -1}, 3);     // s ; <r,s> <s,s>
       sys->scalar(SC_MRR_ZETA, 0x18, i + j, (int)j, thr);          // zeta, eta

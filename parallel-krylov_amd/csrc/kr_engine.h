@@ -203,6 +203,12 @@ struct System {
   void ew_dev(EwOp op, int coef, std::array<int, 6> ids, int slot0);
   void scalar(ScalarOp op, int need, int64_t it, int h, double thr, int check = 1);
   void scalar_state_read();  // st -> hst, synchronises the stream
+  // One shard, no communicator: the scalar step runs inside the vector
+  // kernel that consumes it (EwArgs::pro) instead of its own launch.
+  // KR_FUSE_SCALAR=0 keeps the separate scalar kernel (A/B).
+  bool fused_scalars() const;
+  void ew_pro(EwOp op, ScalarOp sop, std::array<int, 6> ids, int slot0, int64_t it, int h,
+              int par, double thr);
   bool dev_stop = false;
   // Device->host of the summed slots [0, nslots): the one host sync point.
   std::vector<double> reduce(int nslots);

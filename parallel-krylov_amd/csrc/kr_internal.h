@@ -192,6 +192,21 @@ struct EwArgs {
   int stride = 0;                  // partial stride per slot (0: grid)
   const double* cdev = nullptr;    // device-resident c0, c1 (cdev[0], cdev[1]) if set
   const double* stop = nullptr;    // skip the launch when *stop != 0 (converged)
+  // Fused scalar step (device scalars on one shard): every workgroup first
+  // runs the scalar_kernel statement `pro - 1` (a ScalarOp) itself, from the
+  // reduction partials pro_part[q * pro_stride + 0 .. pro_cnt[q]) summed in
+  // the finalize order, and takes c0, c1 from it; workgroup 0 writes the
+  // state (st). Saves the one-workgroup scalar launch between two kernels.
+  int pro = 0;
+  const double* pro_part = nullptr;
+  int pro_stride = 0;
+  int pro_cnt[5] = {};
+  double* st = nullptr;
+  int64_t pro_it = 0;              // iteration number (ST_STOP_AT)
+  int pro_h = 0;                   // ST_HIST index
+  int pro_par = 0;                 // CG: gamma of this iteration in st[gamma_slot(par)]
+  int pro_check = 1;
+  double pro_thr = 0;
 };
 void launch_ew(EwOp op, const EwArgs& a, hipStream_t s);
 
@@ -204,8 +219,12 @@ enum ScalarState : int {
   ST_C3 = 4,
   ST_STOP = 5,     // 1.0 once the convergence test fired
   ST_STOP_AT = 6,  // iteration at whose top it fired
+  ST_GAMMA_ALT = 7,  // fused CG steps: gamma of odd iterations (even: ST_GAMMA)
   ST_HIST = 8,     // ring of reduced norms, one per iteration of a batch
 };
+// Fused CG steps read this iteration's gamma while workgroup 0 writes the
+// next one: two slots, alternating with the iteration's parity.
+inline __host__ __device__ int gamma_slot(int par) { return par ? ST_GAMMA_ALT : ST_GAMMA; }
 constexpr int kScalarBatch = 64;  // iterations per host sync (ring size)
 constexpr int kScalarState = ST_HIST + kScalarBatch;
 enum ScalarOp : int { SC_CG_ALPHA = 0, SC_CG_BETA, SC_MRR_GAMMA, SC_MRR_ZETA };

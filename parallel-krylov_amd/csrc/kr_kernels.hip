@@ -150,6 +150,69 @@ __device__ __forceinline__ void ew_elem(double c0, double c1, double (&v)[6],
   }
 }
 
+__device__ double block_slot_sum(const double* __restrict__ part, int cnt, double* s_red);
+
+// The scalar_kernel statement a.pro - 1 run by a whole workgroup of the
+// vector kernel that consumes it (EwArgs::pro): the same sums (0.0 + the
+// finalize order), the same IEEE statements, so the coefficients are
+// bitwise the scalar kernel's. Returns false when the convergence test fired
+// (the workgroup then skips its vector work, as the separate vector kernel
+// skipped itself on st[ST_STOP]). Only workgroup 0 writes the state; no
+// workgroup reads a state entry this launch writes (CG's gamma alternates).
+__device__ bool ew_prologue(const EwArgs& a, double* s_red, double& c0, double& c1) {
+  double* st = a.st;
+  const bool w0 = blockIdx.x == 0 && threadIdx.x == 0;
+  auto slot = [&](int q) {
+    return 0.0 + block_slot_sum(a.pro_part + (int64_t)q * a.pro_stride, a.pro_cnt[q], s_red);
+  };
+  auto converged = [&](double g) { return a.pro_check && g >= 0.0 && g < a.pro_thr; };
+  c1 = 0.0;
+  switch (a.pro - 1) {
+    case SC_CG_ALPHA: {  // alpha = gamma / sigma  (v3/gpu/cg.py:33)
+      const double sigma = slot(1);
+      c0 = st[gamma_slot(a.pro_par)] / sigma;
+      return true;
+    }
+    case SC_CG_BETA: {  // beta = gnew / gamma; gamma = gnew  (v3/gpu/cg.py:36-38)
+      const double gnew = slot(0);
+      c0 = gnew / st[gamma_slot(a.pro_par)];
+      const bool conv = converged(gnew);
+      if (w0) {
+        st[ST_HIST + a.pro_h] = gnew;
+        st[gamma_slot(a.pro_par ^ 1)] = gnew;
+        if (conv) {  // the test at the top of the next iteration
+          st[ST_STOP_AT] = (double)(a.pro_it + 1);
+          st[ST_STOP] = 1.0;
+        }
+      }
+      return !conv;
+    }
+    case SC_MRR_GAMMA: {  // <r,r>, mu, nu -> test; gamma = nu / mu  (v3/gpu/mrr.py:40-46)
+      const double rr = slot(0), mu = slot(1), nu = slot(2);
+      const bool conv = converged(rr);
+      c0 = nu / mu;
+      if (w0) {
+        st[ST_HIST + a.pro_h] = rr;
+        if (conv) {
+          st[ST_STOP_AT] = (double)a.pro_it;
+          st[ST_STOP] = 1.0;
+        } else {
+          st[ST_GAMMA] = c0;
+        }
+      }
+      return !conv;
+    }
+    case SC_MRR_ZETA: {  // zeta = <r,s>/<s,s>; eta = -zeta * gamma  (v3/gpu/mrr.py:47-49)
+      const double rs = slot(3), ss = slot(4);
+      const double zeta = rs / ss;
+      c0 = (-zeta) * st[ST_GAMMA];
+      c1 = zeta;
+      return true;
+    }
+  }
+  return true;
+}
+
 template <int OP, bool VEC, int U = 1, bool NTS = false>
 __global__ __launch_bounds__(kBlock) void ew_kernel(EwArgs a) {
   using T = EwTraits<OP>;
@@ -158,8 +221,9 @@ __global__ __launch_bounds__(kBlock) void ew_kernel(EwArgs a) {
   // Device-resident scalars (CG/MrR without a host sync): stop once the
   // convergence test fired; coefficients from the scalar kernel's output.
   if (a.stop && *a.stop != 0.0) return;
-  const double c0 = a.cdev ? a.cdev[0] : a.c0;
-  const double c1 = a.cdev ? a.cdev[1] : a.c1;
+  double c0 = a.cdev ? a.cdev[0] : a.c0;
+  double c1 = a.cdev ? a.cdev[1] : a.c1;
+  if (a.pro && !ew_prologue(a, s_red, c0, c1)) return;
   double acc[NP > 0 ? NP : 1];
 #pragma unroll
   for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;

@@ -247,16 +247,19 @@ def test_device_scalars_bitwise_equal_host(monkeypatch, shards, method, matrix, 
     operations in the same order as the host-scalar path (one sync per
     reduction): x and the whole history are bitwise identical, for batches of
     1, 3 and 32 iterations, convergence inside a batch, maxiter truncation,
-    tol = 0 and a test that fires at the first check -- on one shard and on
-    three in-process shards (slot totals gathered on the first shard, summed
-    in shard order; coefficients and stop flag copied to the others)."""
+    tol = 0 and a test that fires at the first check -- on one shard (scalar
+    steps fused into the vector kernels, or separate) and on three in-process
+    shards (slot totals gathered on the first shard, summed in shard order;
+    coefficients and stop flag copied to the others)."""
     A = golden_matrix(matrix)
     b = np.random.default_rng(11).standard_normal(A.shape[0])
     kw = dict(tol=tol, maxiter=maxiter)
     base = {"KRYLOV_AMD_SHARDS": shards}
     x0, i0 = _run_env(monkeypatch, {**base, "KR_DEVICE_SCALARS": "0"}, method, A, b, **kw)
-    for batch in ("1", "3", "32"):
-        x1, i1 = _run_env(monkeypatch, {**base, "KR_DEVICE_SCALARS": "1",
+    for batch, fuse in (("1", "1"), ("3", "1"), ("32", "1"), ("32", "0")):
+        # one shard: the scalar step inside the vector kernels (fused) or
+        # its own one-workgroup launch; several shards: always its own launch
+        x1, i1 = _run_env(monkeypatch, {**base, "KR_DEVICE_SCALARS": "1", "KR_FUSE_SCALAR": fuse,
                                         "KR_SCALAR_BATCH": batch}, method, A, b, **kw)
         np.testing.assert_array_equal(i1["nosl"], i0["nosl"])
         np.testing.assert_array_equal(i1["residual"], i0["residual"])
