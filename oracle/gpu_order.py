@@ -177,8 +177,13 @@ def _block_total(acc):
 
 def _visits_stencil(rows: int, grid: int, P: int, gap_at: int = 0, gap: int = 0):
     """512-row blocks each workgroup of the stencil SpMV visits, in order
-    (kr_stencil.h: XCD q = b & 7, position p and plane segment s of b >> 3)."""
+    (kr_stencil.h: XCD q = b & 7, position p and plane segment s of b >> 3;
+    a launch with a row-block gap -- the boundary launch, RELOAD -- visits
+    blocks b, b + grid, b + 2 grid, ...)."""
     nrb = -(-rows // 512) - gap
+    if gap > 0:
+        return [[v if v < gap_at else v + gap for v in range(b, nrb, grid)]
+                for b in range(grid)]
     planes = -(-nrb // P)
     Z = grid // (8 * P)
     out = []
@@ -242,7 +247,7 @@ def spmv_shard_total(p, s: ShardSched, split: bool):
     nb_gap = (s.int_hi - s.int_lo) // rbs
     nb_all = -(-s.n // rbs)
     if nb_all - nb_gap > 0:
-        g = 8 * P if P else min(s.spmv_grid, nb_all - nb_gap)
+        g = min(s.spmv_grid, nb_all - nb_gap)
         bnd = _launch_partials(p, s.n, g, nb_lo, nb_gap, P=P)
         part[:g] = part[:g] + bnd
     return finalize(part)

@@ -1097,9 +1097,8 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
       SpmvArgs ab = args_for(s, 0, s.n, s.pstride, 1);
       ab.rb_gap_at = nb_lo;
       ab.rb_gap = nb_gap;
-      // stencil: one plane segment per XCD and position (8 * P workgroups)
-      const int g = s.scode ? 8 * s.st_P
-                            : (int)std::min<int64_t>(s.spmv_grid, nb_all - nb_gap);
+      // (the stencil kernel's boundary launch spreads its blocks over the grid)
+      const int g = (int)std::min<int64_t>(s.spmv_grid, nb_all - nb_gap);
       launch_spmv_grid(epi, ab, g, s.stream);
     }
     prof_end(s, nm, t0s[li], bytes_of(s));

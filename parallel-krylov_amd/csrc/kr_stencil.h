@@ -204,7 +204,15 @@ __global__ __launch_bounds__(kBlock) void spmv_stencil_kernel(SpmvArgs a) {
   const int64_t pl0 = planes * q / 8, npl = planes * (q + 1) / 8 - pl0;
   const int64_t z0 = pl0 + npl * zs / Z, z1 = pl0 + npl * (zs + 1) / Z;
   auto phys = [&](int64_t v) { return v < a.rb_gap_at ? v : v + a.rb_gap; };
-  auto visit_ok = [&](int64_t z) { return z < z1 && z * P + p < nrb; };
+  // RELOAD (the boundary launch of a split SpMV: a plane or two at each end
+  // of the shard) carries nothing along a walk, so it spreads its blocks over
+  // the whole grid instead: visit z of workgroup b is block b + z * gridDim.
+  // The plane-per-XCD split would leave all but two XCDs idle there.
+  const int64_t G = gridDim.x;
+  auto blk = [&](int64_t z) { return RELOAD ? (int64_t)blockIdx.x + z * G : z * P + p; };
+  auto visit_ok = [&](int64_t z) {
+    return RELOAD ? blk(z) < nrb : (z < z1 && z * P + p < nrb);
+  };
   constexpr int NM_C = PAT ? (int)(PAT >> 28) : 8;
   const int nm = PAT ? NM_C : a.st_nm;
 
@@ -213,11 +221,11 @@ __global__ __launch_bounds__(kBlock) void spmv_stencil_kernel(SpmvArgs a) {
   SStage<NX, NFAR> sA, sB;
   int buf = 0;
   auto issue = [&](SStage<NX, NFAR>& st, int64_t z) {
-    const int64_t rl = phys(z * P + p) * kSBlock + 2 * tid;
+    const int64_t rl = phys(blk(z)) * kSBlock + 2 * tid;
     st_issue<EPI, RELOAD, NTM>(st, a, xs, rl, rl < a.n ? rl : a.n - 2);
   };
   auto issue_edges = [&](SStage<NX, NFAR>& st, int64_t z) {
-    st_issue_edges(st, a, xs, phys(z * P + p) * kSBlock);
+    st_issue_edges(st, a, xs, phys(blk(z)) * kSBlock);
   };
 
   // One visit: `cur` holds its loads (issued one visit earlier); the next
@@ -225,7 +233,7 @@ __global__ __launch_bounds__(kBlock) void spmv_stencil_kernel(SpmvArgs a) {
   // alternates the two stage register sets, so nothing copies a register a
   // load is still writing (a copy would wait for it).
   auto visit = [&](SStage<NX, NFAR>& cur, SStage<NX, NFAR>& nxs, int64_t z) {
-    const int64_t rb = phys(z * P + p);
+    const int64_t rb = phys(blk(z));
     const int64_t row0 = rb * kSBlock;
     const int64_t rl = row0 + 2 * tid;
     // Lanes past the last row (n is even: both rows or neither) run the same
@@ -362,7 +370,7 @@ __global__ __launch_bounds__(kBlock) void spmv_stencil_kernel(SpmvArgs a) {
     buf ^= 1;
   };
 
-  int64_t z = z0;
+  int64_t z = RELOAD ? 0 : z0;
   if (visit_ok(z)) {
     issue(sA, z);
     issue_edges(sA, z);
