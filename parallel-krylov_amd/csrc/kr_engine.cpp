@@ -56,6 +56,11 @@ int ew_vectors(EwOp op) {
   return 0;
 }
 
+// The products-only variant of a dual SpMV (System::products_only).
+const char* epi_name_po(SpmvEpi e) {
+  return e == EPI_DUAL_KCG ? "spmv2_gram_kcg_last" : "spmv2_gram_mrr_last";
+}
+
 const char* epi_name(SpmvEpi e) {
   switch (e) {
     case EPI_NONE: return "spmv";
@@ -624,6 +629,8 @@ void System::finalize() {
   {
     const char* env = getenv("KR_OVERLAP");  // 0 disables the split SpMV (A/B)
     overlap = !(env && atoi(env) == 0);
+    const char* pe = getenv("KR_PRODUCTS_ONLY");  // 0: store every basis vector (A/B)
+    products_only_on = !(pe && atoi(pe) == 0);
     const char* fz = getenv("KR_FUSE");  // 0: separate vector-step kernels (A/B)
     // Fusion pays for the short-row (row-walk) kernel: C4 +6 %. With the
     // product-then-sum kernel (long rows) the fused SpMV costs more than the
@@ -945,7 +952,12 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
   // boundary launches ADD their reduction partials to the interior launch's
   // (same stream, fixed order: deterministic).
   const bool split = exchange && overlap && all_interior;
-  const char* nm = epi_name(epi);
+  // products only: the stencil kernel skips the y1/y2 stores (its own stat
+  // name, and 16 N fewer bytes)
+  bool po = products_only && products_only_on && dual;
+  bool po_any = false;
+  for (auto& s : shards) po_any = po_any || (po && s.scode);
+  const char* nm = po_any ? epi_name_po(epi) : epi_name(epi);
 
   auto args_for = [&](Shard& s, int64_t r_begin, int64_t rows, int grid, int acc) {
     SpmvArgs a;
@@ -1009,6 +1021,7 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
       a.scratch = s.scratch;
     }
     a.epi_late = epi_late;
+    a.products_only = po && s.scode ? 1 : 0;
     a.stop = dev_stop ? s.st + ST_STOP : nullptr;
     a.nnz_total = s.nnz;
     if (s.dense) {
@@ -1044,7 +1057,8 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
                          : step ? (step_x ? 48.0 : 32.0) * s.n
                                 : (b >= 0 || e >= 0) ? 8.0 * s.n : 0.0;
     if (s.dense) return 8.0 * s.nnz + nv * 8.0 * (n_global + s.n) + extra;
-    return 12.0 * s.nnz + (s.rowptr64 ? 8.0 : 4.0) * (s.n + 1) + nv * 16.0 * s.n + extra;
+    const double stores = (po && s.scode) ? 0.0 : nv * 8.0 * s.n;  // y1 (, y2)
+    return 12.0 * s.nnz + (s.rowptr64 ? 8.0 : 4.0) * (s.n + 1) + nv * 8.0 * s.n + stores + extra;
   };
   // The partial stride is s.pstride for every launch; the full / interior
   // launch writes s.spmv_grid partials per product, the boundary launch (fewer
@@ -1658,9 +1672,13 @@ class KskipMrrSession : public Base {
 
   void head() { sys->spmv(EPI_HEAD_MRR, r0, -1, AR(1), -1, y0, -1, 0); }
   void chain(int kk) {
-    for (int m = 0; m < kk; ++m)
+    for (int m = 0; m < kk; ++m) {
+      // the last pair (Ar[kk+1], Ay[kk]) feeds only the Gram products
+      sys->products_only = m == kk - 1;
       sys->spmv(EPI_DUAL_MRR, AR(m + 1), m == 0 ? y0 : AY(m), AR(m + 2), AY(m + 1), -1, -1,
                 kHead + 7 * m);
+      sys->products_only = false;
+    }
   }
   // Initial / restart MrR step (v3/cpu/kskipmrr.py:26-31).
   void mrr_first(int x_from) {
@@ -1863,8 +1881,11 @@ class KskipCgSession : public Base {
       set_entry(index, rel(sys->reduce(kHead)[0]));
       return done = true;
     }
-    for (int j = 1; j <= k; ++j)
+    for (int j = 1; j <= k; ++j) {
+      sys->products_only = j == k;  // Ar[k], Ap[k+1] feed only the Gram products
       sys->spmv(EPI_DUAL_KCG, AR(j - 1), AP(j), AR(j), AP(j + 1), -1, -1, kHead + 7 * (j - 1));
+      sys->products_only = false;
+    }
     const std::vector<double> g = sys->reduce(gram_slots());
     set_entry(index, rel(g[0]));
     if (residual[index] < prm.tol) {

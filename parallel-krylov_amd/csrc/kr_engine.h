@@ -172,6 +172,10 @@ struct System {
   bool fuse_steps = true;           // k-skip steps fused into the SpMV epilogue
   bool fuse_first = true;           // k-skip MrR steps 0+1 in one SpMV (EPI_STEP_MRR_FIRST2)
   int epi_late = 0;                 // SpmvArgs::epi_late (A/B knob)
+  // Set around an SpMV whose outputs nobody reads (SpmvArgs::products_only);
+  // KR_PRODUCTS_ONLY=0 ignores it (A/B).
+  bool products_only = false;
+  bool products_only_on = true;
   std::unique_ptr<Session> session;
 
   ~System();

@@ -125,6 +125,9 @@ struct SpmvArgs {
   const double* stop = nullptr;  // skip the launch when *stop != 0 (EwArgs::stop)
   double c2 = 0, c3 = 0;       // EPI_STEP_MRR_FIRST2: step-1 scalars (eta1, zeta1)
   int epi_late = 0;  // 1: load own-row epilogue operands at the row end (A/B, KR_EPI_LATE)
+  // 1: the caller needs only the products (the last basis SpMV of a k-skip
+  // outer iteration): a kernel MAY skip storing y1/y2 (the stencil walk does)
+  int products_only = 0;
   int64_t nnz_total = -1;  // entries of val/col (-1: unknown; spmv_kernel2 needs >= 4)
   // Dense row block (gemv_kernel): val is n x ncols row-major with leading
   // dimension dld; x1 + xcol0 (x2 + xcol0) is the full input vector.

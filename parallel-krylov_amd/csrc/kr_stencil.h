@@ -357,7 +357,7 @@ __global__ __launch_bounds__(kBlock) void spmv_stencil_kernel(SpmvArgs a) {
       const EpiVals ohi = epi_values<EPI>(a, shi[0], NV == 2 ? shi[NV - 1] : 0.0, ihi, tmp);
 #pragma unroll
       for (int q = 0; q < (NP > 0 ? NP : 1); ++q) acc[q] = active ? tmp[q] : acc[q];
-      epi_store_pair<EPI, (NTM & 2) != 0>(a, rl, olo, ohi, active);
+      if constexpr (!(NTM & 4)) epi_store_pair<EPI, (NTM & 2) != 0>(a, rl, olo, ohi, active);
     }
     // (6) carry along the walk: this visit's centers are the next one's PREV
     if constexpr (!RELOAD) {
@@ -411,6 +411,24 @@ void spmv_stencil_launch_r(const SpmvArgs& a, int nblocks, hipStream_t s) {
   const int ntm = env ? atoi(env) : 3;
   const char* lenv = getenv("KR_STENCIL_LDS");
   const size_t lds = lenv ? (size_t)atoi(lenv) : 0;
+  if constexpr (E == EPI_DUAL_MRR || E == EPI_DUAL_KCG) {
+    // products only (SpmvArgs::products_only): NTM bit 2 drops the y1/y2
+    // stores (the last basis pair of a k-skip outer iteration feeds only the
+    // Gram products)
+    if (a.products_only) {
+      if (pat7) {
+        spmv_stencil_kernel<E, 2, kPat7, RELOAD, 7><<<nblocks, kBlock, lds, s>>>(a);
+        return;
+      }
+      switch (a.st_nfar) {
+        case 0: spmv_stencil_kernel<E, 0, 0, RELOAD, 7><<<nblocks, kBlock, 0, s>>>(a); return;
+        case 1: spmv_stencil_kernel<E, 1, 0, RELOAD, 7><<<nblocks, kBlock, 0, s>>>(a); return;
+        case 2: spmv_stencil_kernel<E, 2, 0, RELOAD, 7><<<nblocks, kBlock, 0, s>>>(a); return;
+        case 3: spmv_stencil_kernel<E, 3, 0, RELOAD, 7><<<nblocks, kBlock, 0, s>>>(a); return;
+        default: spmv_stencil_kernel<E, 4, 0, RELOAD, 7><<<nblocks, kBlock, 0, s>>>(a); return;
+      }
+    }
+  }
   if (pat7) {
     if constexpr (!RELOAD) {
       switch (ntm) {
