@@ -82,14 +82,28 @@ def _stencil_walk(blk, r0, nnz_row_mean):
     return W // 512
 
 
+def stencil_pm(P):
+    """kr_engine.cpp stencil_pm: the position-major walk (P % 8 == 0)."""
+    return P % 8 == 0
+
+
 def stencil_grid(rows, P):
-    """kr_engine.cpp stencil_grid: 8 XCDs x P positions x Z plane segments."""
+    """kr_engine.cpp stencil_grid: position-major P x Zt segments, or
+    plane-major 8 XCDs x P positions x Z segments."""
     nrb = -(-rows // 512)
     planes = -(-nrb // P)
+    pm = stencil_pm(P)
+    cols = P if pm else 8 * P
     Z = 1
-    while 8 * P * Z < 2048 and planes // (8 * Z * 2) >= 8:
-        Z *= 2
-    return 8 * P * Z
+    if pm:
+        while cols * Z < 4096 and planes // (Z * 2) >= 16:
+            Z *= 2
+        while cols * Z < 1024 and planes // (Z * 2) >= 8:
+            Z *= 2
+    else:
+        while cols * Z < 2048 and planes // (8 * Z * 2) >= 8:
+            Z *= 2
+    return cols * Z
 
 
 def shard_scheds(A, part, cus: int = 256):
@@ -177,7 +191,8 @@ def _block_total(acc):
 
 def _visits_stencil(rows: int, grid: int, P: int, gap_at: int = 0, gap: int = 0):
     """512-row blocks each workgroup of the stencil SpMV visits, in order
-    (kr_stencil.h: XCD q = b & 7, position p and plane segment s of b >> 3;
+    (kr_stencil.h: XCD q = b & 7, position p and plane segment s of b >> 3,
+    position-major for P % 8 == 0, else plane-major;
     a launch with a row-block gap -- the boundary launch, RELOAD -- visits
     blocks b, b + grid, b + 2 grid, ...)."""
     nrb = -(-rows // 512) - gap
@@ -185,14 +200,20 @@ def _visits_stencil(rows: int, grid: int, P: int, gap_at: int = 0, gap: int = 0)
         return [[v if v < gap_at else v + gap for v in range(b, nrb, grid)]
                 for b in range(grid)]
     planes = -(-nrb // P)
-    Z = grid // (8 * P)
+    pm = stencil_pm(P)
     out = []
     for b in range(grid):
         q, w = b & 7, b >> 3
-        p, zs = w % P, w // P
-        pl0 = planes * q // 8
-        npl = planes * (q + 1) // 8 - pl0
-        z0, z1 = pl0 + npl * zs // Z, pl0 + npl * (zs + 1) // Z
+        if pm:  # XCD q: positions [q P/8, (q+1) P/8), segment w // (P/8) of grid/P
+            PP, Zt = P // 8, grid // P
+            p, zs = q * PP + w % PP, w // PP
+            z0, z1 = planes * zs // Zt, planes * (zs + 1) // Zt
+        else:
+            Z = grid // (8 * P)
+            p, zs = w % P, w // P
+            pl0 = planes * q // 8
+            npl = planes * (q + 1) // 8 - pl0
+            z0, z1 = pl0 + npl * zs // Z, pl0 + npl * (zs + 1) // Z
         vis = []
         for z in range(z0, z1):
             v = z * P + p

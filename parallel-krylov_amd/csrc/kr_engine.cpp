@@ -354,21 +354,36 @@ void System::build_stencil(Shard& s) {
   s.int_hi = std::max<int64_t>(s.int_hi / kStencilBlock * kStencilBlock, s.int_lo);
 }
 
-// Stencil SpMV grid: 8 XCDs x P positions x Z plane segments (every
-// workgroup walks its position through a run of consecutive planes). More
-// segments give more workgroups but cost a reload of CENTER and PREV at each
-// segment start: at least 8 planes per segment, about 2048 workgroups.
+// Stencil SpMV grid. Position-major (P % 8 == 0, the 3-D stencils): P
+// positions x Zt plane segments (every segment start reloads CENTER and
+// PREV: 2 planes per walk, so walks stay long). Plane-major (small P: 2-D and narrow
+// bands): 8 XCDs x P positions x Z segments, at least 8 planes per segment.
+// KR_STENCIL_Z fixes the segment count, KR_STENCIL_PM=0 forces plane-major.
+bool stencil_pm(int P) {
+  const char* env = getenv("KR_STENCIL_PM");
+  if (env && atoi(env) == 0) return false;
+  return P % 8 == 0;
+}
+
 int stencil_grid(int64_t rows, int P) {
   const int64_t nrb = (rows + kStencilBlock - 1) / kStencilBlock;
   const int64_t planes = (nrb + P - 1) / P;
+  const bool pm = stencil_pm(P);
+  const int64_t cols = pm ? P : 8 * (int64_t)P;  // workgroups per segment
   int64_t Z = 1;
   const char* env = getenv("KR_STENCIL_Z");
   if (env && atoi(env) > 0) {
     Z = atoi(env);
+  } else if (pm) {
+    // walks of >= 16 planes up to 4096 workgroups (512^3: 4096 x 64 planes;
+    // an 8-GPU slab of 64 planes: 2048 x 16, +3 % over plane-major), then
+    // >= 8 planes up to 1024 workgroups (mid-size cubes keep their parallelism)
+    while (cols * Z < 4096 && planes / (Z * 2) >= 16) Z *= 2;
+    while (cols * Z < 1024 && planes / (Z * 2) >= 8) Z *= 2;
   } else {
-    while (8 * P * Z < 2048 && planes / (8 * Z * 2) >= 8) Z *= 2;
+    while (cols * Z < 2048 && planes / (8 * Z * 2) >= 8) Z *= 2;
   }
-  return (int)(8 * P * Z);
+  return (int)(cols * Z);
 }
 
 void System::build_vdict(Shard& s) {
@@ -1010,6 +1025,7 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
       KR_REQUIRE(r_begin % kStencilBlock == 0, "stencil launch must start on a row block");
       a.scode = s.scode + r_begin;
       a.st_P = s.st_P;
+      a.st_pm = stencil_pm(s.st_P) ? 1 : 0;
       a.st_nm = s.nm;
       a.st_nfar = s.st_nfar;
       for (int k = 0; k < 8; ++k) {

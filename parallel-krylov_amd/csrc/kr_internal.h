@@ -150,6 +150,11 @@ struct SpmvArgs {
   // 8 * st_P; rowptr, col, val, mask, vcode are not read.
   const uint64_t* scode = nullptr;
   int st_P = 0, st_nm = 0, st_nfar = 0;
+  // 1: position-major walk (st_P % 8 == 0): XCD q takes positions
+  // [q P/8, (q+1) P/8) of every plane segment; grid = P x segments.
+  // 0: plane-major: XCD q takes an eighth of the planes at every position;
+  // grid = 8 P x segments. See kr_stencil.h.
+  int st_pm = 0;
   int32_t st_off[8] = {};
   int32_t st_kind[8] = {};
   int32_t st_far[4] = {};

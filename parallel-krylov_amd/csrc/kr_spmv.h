@@ -1832,8 +1832,9 @@ void spmv_launch_epi(const SpmvArgs& a, int nblocks, hipStream_t s) {
   if (a.scode) {  // stencil codes (kr_stencil.h): 3-D stencils with a value dictionary
     // the walk needs whole (XCD, position) columns; the boundary launch
     // (row-block gap, block-strided) takes any grid
-    KR_REQUIRE(a.rb_gap > 0 || nblocks % (8 * a.st_P) == 0,
-               "stencil SpMV: grid must be a multiple of 8 * P");
+    KR_REQUIRE(a.rb_gap > 0 || (a.st_pm ? a.st_P % 8 == 0 && nblocks % a.st_P == 0
+                                        : nblocks % (8 * a.st_P) == 0),
+               "stencil SpMV: grid must be a multiple of P (position-major) or 8 * P");
     spmv_stencil_launch<E>(a, nblocks, s);
     return;
   }

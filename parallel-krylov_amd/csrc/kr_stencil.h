@@ -197,12 +197,27 @@ __global__ __launch_bounds__(kBlock) void spmv_stencil_kernel(SpmvArgs a) {
   const int64_t W = P * kSBlock;
   const int64_t nrb = (a.n + kSBlock - 1) / kSBlock - a.rb_gap;
   const int64_t planes = (nrb + P - 1) / P;
-  const int64_t Z = gridDim.x / (8 * P);
   const int64_t q = blockIdx.x & 7;
   const int64_t w = blockIdx.x >> 3;
-  const int64_t p = w % P, zs = w / P;
-  const int64_t pl0 = planes * q / 8, npl = planes * (q + 1) / 8 - pl0;
-  const int64_t z0 = pl0 + npl * zs / Z, z1 = pl0 + npl * (zs + 1) / Z;
+  int64_t p, z0, z1;
+  if (a.st_pm) {
+    // position-major: XCD q walks positions [q P/8, (q+1) P/8) (neighbouring
+    // positions, whose x rows are each other's +-512 offsets, share an L2)
+    // over plane segment zs of Zt = grid / P; fewer, longer walks than
+    // plane-major when the shard has few planes (an 8-GPU slab: 64)
+    const int64_t PP = P >> 3, Zt = gridDim.x / P;
+    p = q * PP + w % PP;
+    const int64_t zs = w / PP;
+    z0 = planes * zs / Zt;
+    z1 = planes * (zs + 1) / Zt;
+  } else {
+    const int64_t Z = gridDim.x / (8 * P);
+    p = w % P;
+    const int64_t zs = w / P;
+    const int64_t pl0 = planes * q / 8, npl = planes * (q + 1) / 8 - pl0;
+    z0 = pl0 + npl * zs / Z;
+    z1 = pl0 + npl * (zs + 1) / Z;
+  }
   auto phys = [&](int64_t v) { return v < a.rb_gap_at ? v : v + a.rb_gap; };
   // RELOAD (the boundary launch of a split SpMV: a plane or two at each end
   // of the shard) carries nothing along a walk, so it spreads its blocks over

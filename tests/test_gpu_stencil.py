@@ -73,10 +73,13 @@ MATRICES = {
     "p2d512x6": lambda: box(512, 6),             # 2-D: W = 512 = the line
     "band_far": lambda: stencil_band(6144, [1, 6, 512]),
     "band_far2": lambda: stencil_band(5120, [2, 14, 1024]),
+    "box64x64x20": lambda: box(64, 64, 20),      # W = 4096: P = 8, position-major walk
+    "box128x32x9": lambda: box(128, 32, 9),      # W = 4096, 9 planes: short walks
 }
 # expected stencil walk P (0: the row walk serves the matrix)
 EXPECT_P = {"p3d32": 2, "p3d64": 8, "box32x32x7": 2, "box64x16x9": 2, "box48x32x5": 3,
-            "box32x32x3": 2, "p2d512x6": 1, "band_far": 1, "band_far2": 2}
+            "box32x32x3": 2, "p2d512x6": 1, "band_far": 1, "band_far2": 2,
+            "box64x64x20": 8, "box128x32x9": 8}
 NOT_STENCIL = {
     "p3d24": lambda: golden_matrix(["poisson", 24, 3]),      # 576 % 512 != 0
     "p3d16": lambda: golden_matrix(["poisson", 16, 3]),
@@ -93,7 +96,9 @@ def test_stencil_kernel_is_chosen(name):
     A = MATRICES[name]()
     sc = gpu_order.shard_scheds(A, [0, A.shape[0]])[0]
     assert sc.stencil_walk == EXPECT_P[name]
-    assert sc.spmv_grid % (8 * sc.stencil_walk) == 0
+    P = sc.stencil_walk
+    # position-major walks (P % 8 == 0) take P x segments, plane-major 8 P x segments
+    assert sc.spmv_grid % (P if P % 8 == 0 else 8 * P) == 0 and sc.spmv_grid % 8 == 0
 
 
 @pytest.mark.parametrize("name", sorted(NOT_STENCIL))
@@ -158,6 +163,8 @@ CASES = [
     ("adaptivekskipmrr", "box32x32x7", 8, 2), ("kskipmrr", "p3d32", 4, 1),
     ("kskipmrr", "box64x16x9", 3, 2), ("kskipcg", "p3d32", 3, 1), ("kskipcg", "band_far", 2, 3),
     ("kskipmrr", "band_far2", 5, 1), ("adaptivekskipmrr", "p2d512x6", 6, 1),
+    ("kskipmrr", "box64x64x20", 4, 1), ("adaptivekskipmrr", "box64x64x20", 6, 2),
+    ("kskipcg", "box128x32x9", 3, 3),
 ]
 
 
