@@ -175,7 +175,7 @@ constexpr uint32_t kPat7 =
 // NTM: bit 0 = non-temporal code loads, bit 1 = non-temporal result stores
 // (A/B, KR_STENCIL_NT).
 template <int EPI, int NFAR, uint32_t PAT, bool RELOAD, int NTM = 3>
-__global__ __launch_bounds__(kBlock) void spmv_stencil_kernel(SpmvArgs a) {
+__device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
   if (a.stop && *a.stop != 0.0) return;  // converged (device-resident scalars)
   using T = EpiTraits<EPI>;
   constexpr int NP = T::NP;
@@ -414,6 +414,19 @@ __global__ __launch_bounds__(kBlock) void spmv_stencil_kernel(SpmvArgs a) {
   block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
 }
 
+template <int EPI, int NFAR, uint32_t PAT, bool RELOAD, int NTM = 3>
+__global__ __launch_bounds__(kBlock) void spmv_stencil_kernel(SpmvArgs a) {
+  spmv_stencil_body<EPI, NFAR, PAT, RELOAD, NTM>(a);
+}
+// The dual (basis) SpMVs fit 128 VGPRs without spilling: 4 waves per SIMD
+// instead of 3 (512^3 dual -1-4 %, products-only -4 %, 64-plane slab -6/-12 %).
+// The three-vector first-steps kernel and the RELOAD walk would spill there.
+template <int EPI, int NFAR, uint32_t PAT, bool RELOAD, int NTM = 3>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
+void spmv_stencil_kernel_w4(SpmvArgs a) {
+  spmv_stencil_body<EPI, NFAR, PAT, RELOAD, NTM>(a);
+}
+
 template <int E, bool RELOAD>
 void spmv_stencil_launch_r(const SpmvArgs& a, int nblocks, hipStream_t s) {
   bool pat7 = a.st_nm == 7 && a.st_nfar == 2;
@@ -432,7 +445,10 @@ void spmv_stencil_launch_r(const SpmvArgs& a, int nblocks, hipStream_t s) {
     // Gram products)
     if (a.products_only) {
       if (pat7) {
-        spmv_stencil_kernel<E, 2, kPat7, RELOAD, 7><<<nblocks, kBlock, lds, s>>>(a);
+        if constexpr (!RELOAD)
+          spmv_stencil_kernel_w4<E, 2, kPat7, RELOAD, 7><<<nblocks, kBlock, lds, s>>>(a);
+        else
+          spmv_stencil_kernel<E, 2, kPat7, RELOAD, 7><<<nblocks, kBlock, lds, s>>>(a);
         return;
       }
       switch (a.st_nfar) {
@@ -453,7 +469,10 @@ void spmv_stencil_launch_r(const SpmvArgs& a, int nblocks, hipStream_t s) {
         default: break;
       }
     }
-    spmv_stencil_kernel<E, 2, kPat7, RELOAD, 3><<<nblocks, kBlock, lds, s>>>(a);
+    if constexpr (!RELOAD && (E == EPI_DUAL_MRR || E == EPI_DUAL_KCG || E == EPI_DUAL_NONE))
+      spmv_stencil_kernel_w4<E, 2, kPat7, RELOAD, 3><<<nblocks, kBlock, lds, s>>>(a);
+    else
+      spmv_stencil_kernel<E, 2, kPat7, RELOAD, 3><<<nblocks, kBlock, lds, s>>>(a);
     return;
   }
   switch (a.st_nfar) {
