@@ -163,6 +163,9 @@ System::~System() {
   for (auto& s : shards) {
     (void)hipSetDevice(s.dev);
     if (s.stream) (void)hipStreamSynchronize(s.stream);
+    for (auto* list : {&s.send, &s.recv})
+      for (auto& p : *list)
+        if (p.stage) (void)hipFree(p.stage);
     for (double* v : s.vec) (void)hipFree(v);
     for (void* p : s.owned) (void)hipFree(p);
     if (s.partials) (void)hipFree(s.partials);
@@ -614,6 +617,20 @@ void System::finalize() {
   }
   if (hybrid()) {  // reduce(): the local slot totals, gathered over the ranks
     Shard& s0 = shards[0];
+    // staging on the communicator's device for the RCCL pieces of shards
+    // on other devices (halo_hybrid)
+    // KR_HYBRID_STAGE=1 stages every RCCL piece (test hook: exercises the
+    // path on a one-GPU box)
+    const char* fe = getenv("KR_HYBRID_STAGE");
+    const bool force = fe && atoi(fe) != 0;
+    for (auto& t : shards) {
+      if (t.dev == s0.dev && !force) continue;
+      KR_HIP_CHECK(hipSetDevice(s0.dev));
+      for (auto* list : {&t.send, &t.recv})
+        for (auto& p : *list)
+          if (owner[p.peer] != comm->rank && p.count > 0)
+            KR_HIP_CHECK(hipMalloc(&p.stage, sizeof(double) * 3 * (size_t)p.count));
+    }
     KR_HIP_CHECK(hipSetDevice(s0.dev));
     KR_HIP_CHECK(hipMalloc(&hy_send, sizeof(double) * kMaxLocal * kMaxSlots));
     KR_HIP_CHECK(hipMemset(hy_send, 0, sizeof(double) * kMaxLocal * kMaxSlots));
@@ -804,25 +821,55 @@ void System::halo_hybrid(int id1, int id2, int id3, bool async) {
   hipStream_t st0 = stream_of(s0);
   if (!sends.empty() || !recvs.empty()) {
     for (auto& s : shards) KR_HIP_CHECK(hipStreamWaitEvent(st0, ready(s), 0));
+    auto piece = [&](std::vector<HaloPiece>& list, int peer) -> HaloPiece& {
+      return *std::find_if(list.begin(), list.end(),
+                           [&](const HaloPiece& p) { return p.peer == peer; });
+    };
+    int slot = 0;  // vector slot of the staging buffers (<= 3 vectors)
+    for (int id : {id1, id2, id3}) {  // pieces of shards on other devices: stage out
+      if (id < 0) continue;
+      for (auto& x : sends) {
+        Shard& s = shards[x.send_shard - first_global];
+        HaloPiece& p = piece(s.send, x.recv_shard);
+        if (p.stage)
+          KR_HIP_CHECK(hipMemcpyPeerAsync(p.stage + slot * p.count, s0.dev,
+                                          s.vec[id] + s.local_index(p.g0), s.dev,
+                                          8 * (size_t)p.count, st0));
+      }
+      ++slot;
+    }
     KR_NCCL_CHECK(ncclGroupStart());
+    slot = 0;
     for (int id : {id1, id2, id3}) {
       if (id < 0) continue;
       for (auto& x : sends) {
         Shard& s = shards[x.send_shard - first_global];
-        auto it = std::find_if(s.send.begin(), s.send.end(),
-                               [&](const HaloPiece& p) { return p.peer == x.recv_shard; });
-        KR_NCCL_CHECK(ncclSend(s.vec[id] + s.local_index(it->g0), (size_t)it->count, ncclFloat64,
-                               x.peer_rank, comm->nccl, st0));
+        HaloPiece& p = piece(s.send, x.recv_shard);
+        const double* src = p.stage ? p.stage + slot * p.count : s.vec[id] + s.local_index(p.g0);
+        KR_NCCL_CHECK(ncclSend(src, (size_t)p.count, ncclFloat64, x.peer_rank, comm->nccl, st0));
       }
       for (auto& x : recvs) {
         Shard& s = shards[x.recv_shard - first_global];
-        for (auto& p : s.recv)
-          if (p.peer == x.send_shard)
-            KR_NCCL_CHECK(ncclRecv(s.vec[id] + s.local_index(p.g0), (size_t)p.count, ncclFloat64,
-                                   x.peer_rank, comm->nccl, st0));
+        HaloPiece& p = piece(s.recv, x.send_shard);
+        double* dst = p.stage ? p.stage + slot * p.count : s.vec[id] + s.local_index(p.g0);
+        KR_NCCL_CHECK(ncclRecv(dst, (size_t)p.count, ncclFloat64, x.peer_rank, comm->nccl, st0));
       }
+      ++slot;
     }
     KR_NCCL_CHECK(ncclGroupEnd());
+    slot = 0;
+    for (int id : {id1, id2, id3}) {  // staged pieces in
+      if (id < 0) continue;
+      for (auto& x : recvs) {
+        Shard& s = shards[x.recv_shard - first_global];
+        HaloPiece& p = piece(s.recv, x.send_shard);
+        if (p.stage)
+          KR_HIP_CHECK(hipMemcpyPeerAsync(s.vec[id] + s.local_index(p.g0), s.dev,
+                                          p.stage + slot * p.count, s0.dev,
+                                          8 * (size_t)p.count, st0));
+      }
+      ++slot;
+    }
   }
   KR_HIP_CHECK(hipEventRecord(hy_ev, st0));
   if (async) return;  // spmv() makes every shard wait for every ev_out and hy_ev

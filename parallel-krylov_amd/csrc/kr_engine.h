@@ -43,9 +43,13 @@ static_assert(kMaxSlots <= kFinalizeSlots, "finalize slot table too small");
 
 // A contiguous range of global rows exchanged with one peer shard/rank.
 struct HaloPiece {
-  int peer;        // local shard index (in-process) or rank (RCCL)
+  int peer;        // local shard index (in-process) or global shard (communicator)
   int64_t g0;      // first global row
   int64_t count;   // rows
+  // Several shards per rank: an RCCL piece of a shard on another device than
+  // the communicator's goes through this buffer on the communicator's device
+  // (3 vectors x count doubles), so RCCL only touches its own device's memory.
+  double* stage = nullptr;
 };
 
 struct KernelStat {

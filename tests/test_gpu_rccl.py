@@ -27,16 +27,18 @@ def test_mpi_family_over_rccl(ranks):
     assert out.count("-> ok") == 7, out[-3000:]
 
 
-@pytest.mark.parametrize("shards", ["2,2", "2,1", "1,3"])
-def test_mpi_family_several_shards_per_rank(shards):
+@pytest.mark.parametrize("shards,stage", [("2,2", "0"), ("2,1", "0"), ("1,3", "0"), ("2,2", "1")])
+def test_mpi_family_several_shards_per_rank(shards, stage):
     """Several GPUs per rank (GPU_IDS range, v3/gpu/mpi/common.py:100-118):
     one RCCL rank per process, its shards exchanging halos by device copies
     and with the other rank over RCCL; equal to the same partition run in
-    one process bit for bit, and to the oracle."""
-    env = dict(os.environ, NCCL_DEBUG="ERROR")
+    one process bit for bit, and to the oracle. stage=1 routes every RCCL
+    piece through the communicator-device staging buffers (the path of
+    shards on other GPUs than the communicator's)."""
+    env = dict(os.environ, NCCL_DEBUG="ERROR", KR_HYBRID_STAGE=stage)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            "--nproc-per-node=2", "--master-addr=127.0.0.1",
-           f"--master-port={29640 + int(shards.replace(',', ''))%97}",
+           f"--master-port={29640 + int(shards.replace(',', '')) % 97 + 50 * int(stage)}",
            os.path.join(REPO, "tests", "rccl_2rank_worker.py"), "--shards", shards]
     p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=110)
     out = "\n".join(l for l in (p.stdout + p.stderr).splitlines() if "WARN" not in l)
