@@ -142,9 +142,10 @@ def stored_format_delta(nnz, n, lay, long_row=12.0):
     masks replace the 4-byte columns by mw/8 bytes per row, a value
     dictionary the 8-byte values by 1-byte codes; long masked rows use the
     diagonal-offset values (8 bytes per offset and row, no rowptr); the
-    stencil SpMV streams one uint64 of codes per row and nothing else of A."""
+    stencil SpMV streams code_bits bytes of codes per row (8 slots of
+    code_bits bits) and nothing else of A."""
     if lay.get("stencil_walk"):
-        return 12.0 * nnz + 4.0 * (n + 1) - 8.0 * n
+        return 12.0 * nnz + 4.0 * (n + 1) - float(lay.get("code_bits") or 8) * n
     mw = lay["mask_bits"]
     if mw and lay["dict_values"] == 0 and nnz >= long_row * n:  # DIA (KR_DIA=1)
         n_pad = -(-n // 256) * 256
@@ -159,7 +160,8 @@ def stored_format_delta(nnz, n, lay, long_row=12.0):
 
 def format_name(lay):
     if lay.get("stencil_walk"):
-        return (f"stencil codes (8 x 1-byte dictionary codes per row, "
+        cb = lay.get("code_bits") or 8
+        return (f"stencil codes (8 x {cb}-bit dictionary codes per row, "
                 f"{lay['dict_values']}-entry table; walk {lay['stencil_walk']} blocks)")
     parts = [f"offset masks ({lay['mask_bits']}-bit)" if lay["mask_bits"] else "CSR columns"]
     parts.append(f"{lay['dict_values']}-entry value dictionary (1-byte codes)"

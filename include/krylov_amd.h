@@ -231,6 +231,12 @@ int kr_system_shard_layout(kr_system* sys, int shard, int* mask_bits, int* n_off
  * disables). Replaces nothing in the reference: the cuSPARSE csrmv behind
  * v3/gpu/common.py:119 always streams 8-byte values. */
 int kr_system_shard_values(kr_system* sys, int shard, int* dict_values);
+/* Stencil code width of shard s (after finalize): 0 when the stencil SpMV
+ * does not serve the shard, else the bits per slot code (8: one uint64 per
+ * row; 4 / 2: one uint32 / uint16 per row, for dictionaries of <= 15 / <= 3
+ * values on the 7-point pattern), i.e. the bytes of A one row streams.
+ * Replaces nothing in the reference (cuSPARSE csrmv streams CSR). */
+int kr_system_shard_codes(kr_system* sys, int shard, int* code_bits);
 /* Launch geometry of shard s (after finalize): grid = workgroups of the
  * elementwise kernels, spmv_grid = workgroups of the SpMV kernels,
  * stencil_walk = 0 for the row-walk SpMV (256-row blocks, one row per lane)

@@ -652,6 +652,15 @@ int kr_system_shard_values(kr_system* sys, int shard, int* dict_values) {
   });
 }
 
+int kr_system_shard_codes(kr_system* sys, int shard, int* code_bits) {
+  return guarded([&] {
+    KR_REQUIRE(sys && shard >= 0 && shard < (int)sys->shards.size(), "bad shard");
+    KR_REQUIRE(sys->finalized, "system not finalized");
+    const Shard& s = sys->shards[shard];
+    if (code_bits) *code_bits = s.scode ? s.st_cb : 0;
+  });
+}
+
 int kr_system_shard_sched(kr_system* sys, int shard, int* grid, int* spmv_grid,
                           int* stencil_walk, int* format) {
   return guarded([&] {

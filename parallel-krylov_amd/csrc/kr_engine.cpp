@@ -346,8 +346,35 @@ void System::build_stencil(Shard& s) {
   s.scratch = scratch;
   launch_stencil_codes(s.rowptr, s.rowptr64, s.n, s.col, s.vcode, s.pad, s.moff, s.nm, code,
                        s.stream);
-  KR_HIP_CHECK(hipStreamSynchronize(s.stream));
-  s.scode = code;
+  // Narrow codes for the 7-point pattern (the kernel's compile-time slot
+  // pattern kPat7): 2 bits per slot with <= 3 dictionary values (the Poisson
+  // systems: 2 B per row instead of 8), 4 bits with <= 15. KR_STENCIL_CB=4/8
+  // asks for at least that width (A/B).
+  int cb = 8;
+  const int32_t pat7[7] = {1, 4, 3, 0, 3, 5, 2};
+  if (s.nm == 7 && nfar == 2 && std::equal(pat7, pat7 + 7, kind)) {
+    const char* cenv = getenv("KR_STENCIL_CB");
+    const int want = cenv ? atoi(cenv) : 2;
+    cb = (want <= 2 && s.ntab <= 3) ? 2 : (want <= 4 && s.ntab <= 15) ? 4 : 8;
+  }
+  void* narrow = nullptr;
+  if (cb < 8 && hipMalloc(&narrow, (size_t)cb * (size_t)s.n) != hipSuccess) {
+    (void)hipGetLastError();
+    narrow = nullptr;
+    cb = 8;
+  }
+  if (narrow) {
+    launch_stencil_pack(code, s.n, cb, narrow, s.stream);
+    KR_HIP_CHECK(hipStreamSynchronize(s.stream));
+    s.owned.erase(std::find(s.owned.begin(), s.owned.end(), (void*)code));
+    KR_HIP_CHECK(hipFree(code));
+    s.owned.push_back(narrow);
+    s.scode = narrow;
+  } else {
+    KR_HIP_CHECK(hipStreamSynchronize(s.stream));
+    s.scode = code;
+  }
+  s.st_cb = cb;
   s.st_P = (int)(W / kStencilBlock);
   s.st_nfar = nfar;
   for (int k = 0; k < 8; ++k) s.st_kind[k] = kind[k];
@@ -1070,7 +1097,8 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
     }
     if (s.scode) {
       KR_REQUIRE(r_begin % kStencilBlock == 0, "stencil launch must start on a row block");
-      a.scode = s.scode + r_begin;
+      a.scode = static_cast<const char*>(s.scode) + r_begin * s.st_cb;
+      a.st_cb = s.st_cb;
       a.st_P = s.st_P;
       a.st_pm = stencil_pm(s.st_P) ? 1 : 0;
       a.st_nm = s.nm;

@@ -96,7 +96,8 @@ struct Shard {
   int64_t nz0 = 0;                  // rowptr[0]: index of the block's first stored entry
   std::vector<int32_t> moff_h;      // host copy of the offset table (moff)
   // stencil codes (SpmvArgs::scode, kr_stencil.h), owned; st_P = 0: not used
-  uint64_t* scode = nullptr;
+  void* scode = nullptr;
+  int st_cb = 8;                    // SpmvArgs::st_cb: bits per slot code = bytes per row
   double* scratch = nullptr;        // SpmvArgs::scratch (stencil SpMV), owned
   int st_P = 0, st_nfar = 0;
   int32_t st_kind[8] = {}, st_far[4] = {};

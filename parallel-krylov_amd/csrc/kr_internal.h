@@ -147,8 +147,12 @@ struct SpmvArgs {
   // entry. Rows are walked in 512-row blocks, st_P blocks per walk step
   // (W = 512 * st_P rows = the +-W offsets); st_kind[k] = StencilKind of
   // slot k; st_far[f] = the FAR offsets. Launch grids are multiples of
-  // 8 * st_P; rowptr, col, val, mask, vcode are not read.
-  const uint64_t* scode = nullptr;
+  // 8 * st_P; rowptr, col, val, mask, vcode are not read. st_cb: bits per
+  // slot code (8: uint64 per row, 0xFF = no entry; 4: uint32 per row, 0xF;
+  // 2: uint16 per row, 0x3 -- narrow codes for dictionaries of <= 15 / <= 3
+  // values), so a row streams st_cb bytes of A.
+  const void* scode = nullptr;
+  int st_cb = 8;
   int st_P = 0, st_nm = 0, st_nfar = 0;
   // 1: position-major walk (st_P % 8 == 0): XCD q takes positions
   // [q P/8, (q+1) P/8) of every plane segment; grid = P x segments.
@@ -168,6 +172,10 @@ constexpr int kStencilBlock = 2 * kBlock;
 void launch_stencil_codes(const void* rowptr, int rowptr64, int64_t n, const int32_t* col,
                           const uint8_t* vcode, int64_t base, const int32_t* M, int nm,
                           uint64_t* out, hipStream_t s);
+// Narrow stencil codes: out (uint16 per row for cb = 2, uint32 for cb = 4)
+// slot k = bits [cb k, cb k + cb) = byte k of in[i], all ones where byte k is
+// 0xFF (no entry). Every present code must be < 2^cb - 1.
+void launch_stencil_pack(const uint64_t* in, int64_t n, int cb, void* out, hipStream_t s);
 // Mean row length from which the product-then-sum SpMV is used.
 constexpr double kLongRow = 12.0;
 void launch_spmv(SpmvEpi epi, const SpmvArgs& a, hipStream_t s);

@@ -712,6 +712,26 @@ __global__ void stencil_codes_kernel(const RP* rowptr, int64_t n, const int32_t*
   }
 }
 
+// Narrow stencil codes (launch_stencil_pack).
+template <int CB>
+__global__ void stencil_pack_kernel(const uint64_t* __restrict__ in, int64_t n, void* out) {
+  constexpr uint32_t m = (1u << CB) - 1u;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t w = in[i];
+    uint32_t o = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t c = (uint32_t)(w >> (8 * k)) & 0xFFu;
+      o |= (c == 0xFFu ? m : c) << (CB * k);
+    }
+    if constexpr (CB == 2)
+      static_cast<uint16_t*>(out)[i] = (uint16_t)o;
+    else
+      static_cast<uint32_t*>(out)[i] = o;
+  }
+}
+
 template <typename RP>
 __global__ void col_shift_kernel(const RP* rowptr, int64_t n, int32_t* col, int64_t delta) {
   const int64_t base = (int64_t)rowptr[0];
@@ -1008,6 +1028,17 @@ void launch_stencil_codes(const void* rowptr, int rowptr64, int64_t n, const int
   else
     stencil_codes_kernel<int32_t><<<g, 256, 0, s>>>(static_cast<const int32_t*>(rowptr), n, col,
                                                     vcode, base, M, nm, out);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_stencil_pack(const uint64_t* in, int64_t n, int cb, void* out, hipStream_t s) {
+  KR_REQUIRE(cb == 2 || cb == 4, "stencil codes: 2 or 4 bits per slot");
+  if (n <= 0) return;
+  const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 65535);
+  if (cb == 2)
+    stencil_pack_kernel<2><<<g, 256, 0, s>>>(in, n, out);
+  else
+    stencil_pack_kernel<4><<<g, 256, 0, s>>>(in, n, out);
   KR_HIP_CHECK(hipGetLastError());
 }
 

@@ -63,9 +63,10 @@ struct SPair {
 };
 
 // One visit's prefetched loads.
-template <int NX, int NFAR>
+template <int NX, int NFAR, int CB = 8>
 struct SStage {
-  uint64_t clo, chi;          // codes of rows 2t, 2t+1
+  using Code = typename std::conditional<CB == 8, uint64_t, uint32_t>::type;
+  Code clo, chi;              // codes of rows 2t, 2t+1
   dbl2v nxt[NX];              // x[row + W]
   dbl2v far[NFAR > 0 ? NFAR : 1][NX];
   dbl2v u1, u2, us, e;        // own-row epilogue operands (as the EPI needs)
@@ -85,19 +86,40 @@ __device__ __forceinline__ dbl2v st_ld2_uniform(const double* x, int64_t i, int6
 // x loads use it as is -- rows past the own rows are halo rows, which the
 // +-1 neighbours of the last own rows need -- clamped only to the vector);
 // rr: rl clamped to the own rows (codes and own-row operands).
-template <int EPI, bool RELOAD, int NTM, int NX, int NFAR>
-__device__ __forceinline__ void st_issue(SStage<NX, NFAR>& st, const SpmvArgs& a,
+template <int EPI, bool RELOAD, int NTM, int NX, int NFAR, int CB>
+__device__ __forceinline__ void st_issue(SStage<NX, NFAR, CB>& st, const SpmvArgs& a,
                                          const double* const (&xs)[3], int64_t rl, int64_t rr) {
   using T = EpiTraits<EPI>;
-  const uint64_t* cp = a.scode + rr;
-  typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-  u64x2 c;
-  if constexpr (NTM & 1)  // codes: streamed once (non-temporal)
-    c = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(cp));
-  else
-    c = *reinterpret_cast<const u64x2*>(cp);
-  st.clo = c.x;
-  st.chi = c.y;
+  if constexpr (CB == 8) {
+    const uint64_t* cp = static_cast<const uint64_t*>(a.scode) + rr;
+    typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+    u64x2 c;
+    if constexpr (NTM & 1)  // codes: streamed once (non-temporal)
+      c = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(cp));
+    else
+      c = *reinterpret_cast<const u64x2*>(cp);
+    st.clo = c.x;
+    st.chi = c.y;
+  } else if constexpr (CB == 4) {
+    const uint32_t* cp = static_cast<const uint32_t*>(a.scode) + rr;
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    u32x2 c;
+    if constexpr (NTM & 1)
+      c = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(cp));
+    else
+      c = *reinterpret_cast<const u32x2*>(cp);
+    st.clo = c.x;
+    st.chi = c.y;
+  } else {  // CB == 2: both rows' uint16 codes in one dword (rr even)
+    const uint32_t* cp = reinterpret_cast<const uint32_t*>(static_cast<const uint16_t*>(a.scode) + rr);
+    uint32_t c;
+    if constexpr (NTM & 1)
+      c = __builtin_nontemporal_load(cp);
+    else
+      c = *cp;
+    st.clo = c & 0xFFFFu;
+    st.chi = c >> 16;
+  }
   const int64_t xi = a.xoff + rl;
   const int64_t W = (int64_t)a.st_P * kSBlock;
 #pragma unroll
@@ -127,8 +149,8 @@ __device__ __forceinline__ void st_issue(SStage<NX, NFAR>& st, const SpmvArgs& a
 
 // The line's edge pairs (uniform: scalar loads, counted by lgkmcnt). Issued
 // after the visit's barrier, whose lgkmcnt(0) would otherwise wait for them.
-template <int NX, int NFAR>
-__device__ __forceinline__ void st_issue_edges(SStage<NX, NFAR>& st, const SpmvArgs& a,
+template <int NX, int NFAR, int CB>
+__device__ __forceinline__ void st_issue_edges(SStage<NX, NFAR, CB>& st, const SpmvArgs& a,
                                                const double* const (&xs)[3], int64_t row0) {
 #pragma unroll
   for (int v = 0; v < NX; ++v) {
@@ -173,8 +195,8 @@ constexpr uint32_t kPat7 =
 // a row-block gap: the boundary launch of a split SpMV); otherwise they are
 // loaded once per plane segment, before the loop, and carried.
 // NTM: bit 0 = non-temporal code loads, bit 1 = non-temporal result stores
-// (A/B, KR_STENCIL_NT).
-template <int EPI, int NFAR, uint32_t PAT, bool RELOAD, int NTM = 3>
+// (A/B, KR_STENCIL_NT). CB: bits per slot code (SpmvArgs::st_cb).
+template <int EPI, int NFAR, uint32_t PAT, bool RELOAD, int NTM = 3, int CB = 8>
 __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
   if (a.stop && *a.stop != 0.0) return;  // converged (device-resident scalars)
   using T = EpiTraits<EPI>;
@@ -233,13 +255,13 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
 
   const double* const xs[3] = {a.x1, a.x2, a.x3};
   dbl2v cen[NX], prv[NX];  // carried: x at the rows, x at the rows - W
-  SStage<NX, NFAR> sA, sB;
+  SStage<NX, NFAR, CB> sA, sB;
   int buf = 0;
-  auto issue = [&](SStage<NX, NFAR>& st, int64_t z) {
+  auto issue = [&](SStage<NX, NFAR, CB>& st, int64_t z) {
     const int64_t rl = phys(blk(z)) * kSBlock + 2 * tid;
     st_issue<EPI, RELOAD, NTM>(st, a, xs, rl, rl < a.n ? rl : a.n - 2);
   };
-  auto issue_edges = [&](SStage<NX, NFAR>& st, int64_t z) {
+  auto issue_edges = [&](SStage<NX, NFAR, CB>& st, int64_t z) {
     st_issue_edges(st, a, xs, phys(blk(z)) * kSBlock);
   };
 
@@ -247,7 +269,7 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
   // visit's loads go to `nxs` before anything here waits. The loop below
   // alternates the two stage register sets, so nothing copies a register a
   // load is still writing (a copy would wait for it).
-  auto visit = [&](SStage<NX, NFAR>& cur, SStage<NX, NFAR>& nxs, int64_t z) {
+  auto visit = [&](SStage<NX, NFAR, CB>& cur, SStage<NX, NFAR, CB>& nxs, int64_t z) {
     const int64_t rb = phys(blk(z));
     const int64_t row0 = rb * kSBlock;
     const int64_t rl = row0 + 2 * tid;
@@ -311,10 +333,11 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
     for (int k = 0; k < NM_C; ++k) {
       if (k >= nm) break;
       const int kind = PAT ? (int)((PAT >> (4 * k)) & 0xFu) : a.st_kind[k];
-      const unsigned clo = (unsigned)(cur.clo >> (8 * k)) & 0xFFu;
-      const unsigned chi = (unsigned)(cur.chi >> (8 * k)) & 0xFFu;
-      const double vlo = s_tab[clo == 0xFFu ? 0u : clo];
-      const double vhi = s_tab[chi == 0xFFu ? 0u : chi];
+      constexpr unsigned kNone = (1u << CB) - 1u;  // no entry
+      const unsigned clo = (unsigned)(cur.clo >> (CB * k)) & kNone;
+      const unsigned chi = (unsigned)(cur.chi >> (CB * k)) & kNone;
+      const double vlo = s_tab[clo == kNone ? 0u : clo];
+      const double vhi = s_tab[chi == kNone ? 0u : chi];
       double xlo[NV], xhi[NV];
       if (kind == SK_CENTER) {
 #pragma unroll
@@ -348,11 +371,11 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
           for (int v = 0; v < NV; ++v) { xlo[v] = g[v].x; xhi[v] = g[v].y; }
         }
       }
-      if (clo != 0xFFu) {
+      if (clo != kNone) {
 #pragma unroll
         for (int v = 0; v < NV; ++v) slo[v] = slo[v] + vlo * xlo[v];
       }
-      if (chi != 0xFFu) {
+      if (chi != kNone) {
 #pragma unroll
         for (int v = 0; v < NV; ++v) shi[v] = shi[v] + vhi * xhi[v];
       }
@@ -414,27 +437,47 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
   block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
 }
 
-template <int EPI, int NFAR, uint32_t PAT, bool RELOAD, int NTM = 3>
+template <int EPI, int NFAR, uint32_t PAT, bool RELOAD, int NTM = 3, int CB = 8>
 __global__ __launch_bounds__(kBlock) void spmv_stencil_kernel(SpmvArgs a) {
-  spmv_stencil_body<EPI, NFAR, PAT, RELOAD, NTM>(a);
+  spmv_stencil_body<EPI, NFAR, PAT, RELOAD, NTM, CB>(a);
 }
 // The dual (basis) SpMVs fit 128 VGPRs without spilling: 4 waves per SIMD
 // instead of 3 (512^3 dual -1-4 %, products-only -4 %, 64-plane slab -6/-12 %).
 // The three-vector first-steps kernel and the RELOAD walk would spill there.
-template <int EPI, int NFAR, uint32_t PAT, bool RELOAD, int NTM = 3>
+template <int EPI, int NFAR, uint32_t PAT, bool RELOAD, int NTM = 3, int CB = 8>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
 void spmv_stencil_kernel_w4(SpmvArgs a) {
-  spmv_stencil_body<EPI, NFAR, PAT, RELOAD, NTM>(a);
+  spmv_stencil_body<EPI, NFAR, PAT, RELOAD, NTM, CB>(a);
+}
+
+// The 7-point pattern's launch at the shard's code width.
+template <int E, bool RELOAD, int NTM, bool W4>
+void st_launch_pat7(const SpmvArgs& a, int nblocks, size_t lds, hipStream_t s) {
+  auto go = [&](auto cbc) {
+    constexpr int CB = decltype(cbc)::value;
+    if constexpr (W4)
+      spmv_stencil_kernel_w4<E, 2, kPat7, RELOAD, NTM, CB><<<nblocks, kBlock, lds, s>>>(a);
+    else
+      spmv_stencil_kernel<E, 2, kPat7, RELOAD, NTM, CB><<<nblocks, kBlock, lds, s>>>(a);
+  };
+  switch (a.st_cb) {
+    case 2: go(std::integral_constant<int, 2>{}); return;
+    case 4: go(std::integral_constant<int, 4>{}); return;
+    default: go(std::integral_constant<int, 8>{}); return;
+  }
 }
 
 template <int E, bool RELOAD>
 void spmv_stencil_launch_r(const SpmvArgs& a, int nblocks, hipStream_t s) {
   bool pat7 = a.st_nm == 7 && a.st_nfar == 2;
   for (int k = 0; k < 7 && pat7; ++k) pat7 = a.st_kind[k] == (int)((kPat7 >> (4 * k)) & 0xFu);
+  // narrow codes exist only for the 7-point pattern (System::build_stencil)
+  KR_REQUIRE(pat7 || a.st_cb == 8, "stencil SpMV: narrow codes need the 7-point pattern");
   // Non-temporal code loads and result stores (NTM = 3): the streamed-once
   // bytes stop displacing the x lines neighbouring workgroups re-read from
-  // L2 (C4 +4-7 %). KR_STENCIL_NT=0..2 (A/B; 7-point pattern). KR_STENCIL_LDS
-  // (A/B): extra LDS per workgroup, i.e. fewer resident workgroups per CU.
+  // L2 (C4 +4-7 %). KR_STENCIL_NT=0..2 (A/B; 7-point pattern, 8-bit codes).
+  // KR_STENCIL_LDS (A/B): extra LDS per workgroup, i.e. fewer resident
+  // workgroups per CU.
   const char* env = getenv("KR_STENCIL_NT");
   const int ntm = env ? atoi(env) : 3;
   const char* lenv = getenv("KR_STENCIL_LDS");
@@ -445,10 +488,7 @@ void spmv_stencil_launch_r(const SpmvArgs& a, int nblocks, hipStream_t s) {
     // Gram products)
     if (a.products_only) {
       if (pat7) {
-        if constexpr (!RELOAD)
-          spmv_stencil_kernel_w4<E, 2, kPat7, RELOAD, 7><<<nblocks, kBlock, lds, s>>>(a);
-        else
-          spmv_stencil_kernel<E, 2, kPat7, RELOAD, 7><<<nblocks, kBlock, lds, s>>>(a);
+        st_launch_pat7<E, RELOAD, 7, !RELOAD>(a, nblocks, lds, s);
         return;
       }
       switch (a.st_nfar) {
@@ -462,6 +502,7 @@ void spmv_stencil_launch_r(const SpmvArgs& a, int nblocks, hipStream_t s) {
   }
   if (pat7) {
     if constexpr (!RELOAD) {
+      if (ntm != 3) KR_REQUIRE(a.st_cb == 8, "KR_STENCIL_NT A/B runs with KR_STENCIL_CB=8");
       switch (ntm) {
         case 0: spmv_stencil_kernel<E, 2, kPat7, RELOAD, 0><<<nblocks, kBlock, lds, s>>>(a); return;
         case 1: spmv_stencil_kernel<E, 2, kPat7, RELOAD, 1><<<nblocks, kBlock, lds, s>>>(a); return;
@@ -469,10 +510,8 @@ void spmv_stencil_launch_r(const SpmvArgs& a, int nblocks, hipStream_t s) {
         default: break;
       }
     }
-    if constexpr (!RELOAD && (E == EPI_DUAL_MRR || E == EPI_DUAL_KCG || E == EPI_DUAL_NONE))
-      spmv_stencil_kernel_w4<E, 2, kPat7, RELOAD, 3><<<nblocks, kBlock, lds, s>>>(a);
-    else
-      spmv_stencil_kernel<E, 2, kPat7, RELOAD, 3><<<nblocks, kBlock, lds, s>>>(a);
+    constexpr bool w4 = !RELOAD && (E == EPI_DUAL_MRR || E == EPI_DUAL_KCG || E == EPI_DUAL_NONE);
+    st_launch_pat7<E, RELOAD, 3, w4>(a, nblocks, lds, s);
     return;
   }
   switch (a.st_nfar) {

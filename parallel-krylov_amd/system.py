@@ -275,15 +275,17 @@ class KrylovSystem:
     def shard_layout(self, s: int) -> dict:
         """SpMV storage of shard s: mask_bits (0 = CSR columns), n_offsets,
         interior row range [interior_lo, interior_hi), dict_values (0 = 8-byte
-        values, else the size of the value dictionary)."""
+        values, else the size of the value dictionary), code_bits (stencil
+        SpMV: bits per slot code = bytes of A per row; 0 otherwise)."""
         mb, no = ctypes.c_int(), ctypes.c_int()
         lo, hi = ctypes.c_int64(), ctypes.c_int64()
         call("kr_system_shard_layout", self.handle, s, ctypes.byref(mb), ctypes.byref(no),
              ctypes.byref(lo), ctypes.byref(hi))
-        dv = ctypes.c_int()
+        dv, cb = ctypes.c_int(), ctypes.c_int()
         call("kr_system_shard_values", self.handle, s, ctypes.byref(dv))
+        call("kr_system_shard_codes", self.handle, s, ctypes.byref(cb))
         return dict(mask_bits=mb.value, n_offsets=no.value, interior_lo=lo.value,
-                    interior_hi=hi.value, dict_values=dv.value)
+                    interior_hi=hi.value, dict_values=dv.value, code_bits=cb.value)
 
     def shard_sched(self, s: int) -> dict:
         """Launch geometry of shard s: elementwise and SpMV grids plus the

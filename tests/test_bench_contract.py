@@ -76,3 +76,7 @@ def test_stored_format_bytes():
     st = dict(mask_bits=8, n_offsets=7, dict_values=2, stencil_walk=512)
     assert bench.stored_format_delta(nnz, n, st) == 12.0 * nnz + 4.0 * (n + 1) - 8.0 * n
     assert "stencil" in bench.format_name(st)
+    # narrow codes: 2 bits per slot (<= 3 dictionary values) stream 2 B per row
+    st2 = dict(st, code_bits=2)
+    assert bench.stored_format_delta(nnz, n, st2) == 12.0 * nnz + 4.0 * (n + 1) - 2.0 * n
+    assert "2-bit" in bench.format_name(st2)

@@ -1,6 +1,7 @@
 """The stencil SpMV (kr_stencil.h): 512-row blocks, two rows per lane, the
 walk carrying x[row - W] and x[row] in registers, +-1 neighbours from an LDS
-line, one uint64 of dictionary codes per row.
+line, one row's dictionary codes in 8 slots of 2, 4 or 8 bits (2 / 4 / 8
+bytes per row; the narrow widths for <= 3 / <= 15 values, 7-point pattern).
 
 It serves masked short-row shards with a value dictionary whose offsets hold
 a +-W pair (W a multiple of 512: 3-D stencils with n^2 % 512 == 0, 2-D ones
@@ -55,6 +56,24 @@ def stencil_band(n, offs, seed=0):
     return A
 
 
+def aniso(nx, ny, nz, cx, cy, cz):
+    """Anisotropic 7-point operator: 4 distinct values (4-bit stencil codes)."""
+    def T(m, c):
+        return sp.diags([-c, 2.0 * c, -c], [-1, 0, 1], shape=(m, m))
+    K = sp.csr_matrix(sp.kronsum(sp.kronsum(T(nx, cx), T(ny, cy)), T(nz, cz)))
+    K.sort_indices()
+    return K
+
+
+def revalued(A, nvals, seed=3):
+    """A's pattern with values drawn from nvals distinct numbers (SpMV only)."""
+    A = A.copy()
+    pool = np.random.default_rng(seed).standard_normal(nvals)
+    A.data = pool[np.random.default_rng(seed + 1).integers(0, nvals, A.nnz)]
+    A.data[:nvals] = pool  # every value present
+    return A
+
+
 def _bal(n, p):
     q, r = divmod(n, p)
     out = [0]
@@ -75,11 +94,19 @@ MATRICES = {
     "band_far2": lambda: stencil_band(5120, [2, 14, 1024]),
     "box64x64x20": lambda: box(64, 64, 20),      # W = 4096: P = 8, position-major walk
     "box128x32x9": lambda: box(128, 32, 9),      # W = 4096, 9 planes: short walks
+    "aniso32x32x7": lambda: aniso(32, 32, 7, 1.0, 0.5, 0.25),  # 4 values: 4-bit codes
+    "vals3_32x32x7": lambda: revalued(box(32, 32, 7), 3),      # 3 values: 2-bit, code 2 used
+    "vals15_64x64x9": lambda: revalued(box(64, 64, 9), 15),    # 15 values: 4-bit, P = 8
+    "vals40_32x32x7": lambda: revalued(box(32, 32, 7), 40),    # 40 values: 8-bit codes
 }
+# stencil code width (bits per slot) the engine picks for the 7-point pattern
+EXPECT_CB = {"aniso32x32x7": 4, "vals3_32x32x7": 2, "vals15_64x64x9": 4, "vals40_32x32x7": 8,
+             "p3d32": 2, "p3d64": 2, "box64x64x20": 2}
 # expected stencil walk P (0: the row walk serves the matrix)
 EXPECT_P = {"p3d32": 2, "p3d64": 8, "box32x32x7": 2, "box64x16x9": 2, "box48x32x5": 3,
             "box32x32x3": 2, "p2d512x6": 1, "band_far": 1, "band_far2": 2,
-            "box64x64x20": 8, "box128x32x9": 8}
+            "box64x64x20": 8, "box128x32x9": 8, "aniso32x32x7": 2, "vals3_32x32x7": 2,
+            "vals15_64x64x9": 8, "vals40_32x32x7": 2}
 NOT_STENCIL = {
     "p3d24": lambda: golden_matrix(["poisson", 24, 3]),      # 576 % 512 != 0
     "p3d16": lambda: golden_matrix(["poisson", 16, 3]),
@@ -153,6 +180,24 @@ def test_stencil_spmv_bitwise_scipy(monkeypatch, name, shards):
     np.testing.assert_array_equal(y0, y)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("want", [None, "4", "8"])
+@pytest.mark.parametrize("name", sorted(EXPECT_CB))
+def test_stencil_code_width_bitwise_scipy(monkeypatch, name, want):
+    """Narrow codes (2 / 4 bits per slot; KR_STENCIL_CB asks for at least a
+    width) give y = A x bitwise scipy's, on 1 and 2 shards."""
+    A = MATRICES[name]()
+    n = A.shape[0]
+    x = np.random.default_rng(7).standard_normal(n)
+    for shards in (1, 2):
+        sysm = _system(A, shards, {"KR_STENCIL_CB": want} if want else None, monkeypatch)
+        cb = EXPECT_CB[name] if want is None else max(EXPECT_CB[name], int(want))
+        assert [sysm.shard_layout(s)["code_bits"] for s in range(shards)] == [cb] * shards
+        y = sysm.gather(sysm.spmv(sysm.split(x))).cpu().numpy()
+        sysm.close()
+        np.testing.assert_array_equal(y, A @ x)
+
+
 def _solver(method):
     mod = importlib.import_module(f"parallel_krylov_amd.v3.gpu.{method}")
     return getattr(mod, method)
@@ -164,7 +209,8 @@ CASES = [
     ("kskipmrr", "box64x16x9", 3, 2), ("kskipcg", "p3d32", 3, 1), ("kskipcg", "band_far", 2, 3),
     ("kskipmrr", "band_far2", 5, 1), ("adaptivekskipmrr", "p2d512x6", 6, 1),
     ("kskipmrr", "box64x64x20", 4, 1), ("adaptivekskipmrr", "box64x64x20", 6, 2),
-    ("kskipcg", "box128x32x9", 3, 3),
+    ("kskipcg", "box128x32x9", 3, 3), ("kskipmrr", "aniso32x32x7", 4, 1),
+    ("adaptivekskipmrr", "aniso32x32x7", 8, 2),
 ]
 
 

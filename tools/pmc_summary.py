@@ -27,7 +27,7 @@ def short(name):
     m = re.search(r"spmv_kernel\w*<(\w+), (\d+), (\w+)", name)
     if m:
         return EPI[int(m.group(2))] + ("" if m.group(1) == "int" else "_rp64")
-    m = re.search(r"spmv_stencil_kernel(?:_w4)?<(\d+), \d+, \w+, \w+, (\d+)>", name)
+    m = re.search(r"spmv_stencil_kernel(?:_w4)?<(\d+), \d+, \w+, \w+, (\d+)(?:, \d+)?>", name)
     if m:  # NTM bit 2: the products-only dual (engine name ..._last)
         return EPI[int(m.group(1))] + ("_last" if int(m.group(2)) & 4 else "") + "_stencil"
     m = re.search(r"spmv_stencil_kernel(?:_w4)?<(\d+)\b", name)
