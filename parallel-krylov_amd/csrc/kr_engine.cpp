@@ -315,6 +315,9 @@ void System::build_stencil(Shard& s) {
     if (o > 0 && o % kStencilBlock == 0 && std::find(M.begin(), M.end(), -o) != M.end())
       W = std::max<int64_t>(W, o);
   if (W == 0) return;
+  // buffer loads take 32-bit byte offsets: every x offset the walk forms,
+  // (ld + W + a block) doubles, stays below 2^31 bytes (kr_stencil.h SRes)
+  if ((s.ld + W + 2 * kStencilBlock) * 8 >= (int64_t(1) << 31)) return;
   int nfar = 0;
   int32_t kind[8] = {}, far[4] = {};
   for (int k = 0; k < s.nm; ++k) {

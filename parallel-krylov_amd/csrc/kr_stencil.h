@@ -82,52 +82,77 @@ __device__ __forceinline__ dbl2v st_ld2_uniform(const double* x, int64_t i, int6
   return load_uniform(reinterpret_cast<const dbl2v*>(x), i >> 1);
 }
 
-// rl: the lane's first row (launch-relative, may lie past the last own row:
-// x loads use it as is -- rows past the own rows are halo rows, which the
-// +-1 neighbours of the last own rows need -- clamped only to the vector);
-// rr: rl clamped to the own rows (codes and own-row operands).
+// Buffer resources of one launch (wave-uniform descriptors): the x vectors
+// (xlen doubles each) and the codes (n rows). A buffer load takes a 32-bit
+// byte offset = a uniform part (SGPR arithmetic) + the lane's constant part,
+// and the hardware range check returns 0 for offsets past the buffer (a
+// negative uniform part wraps past it too): no per-lane clamp or 64-bit
+// address per load. Lanes whose offsets fall outside read 0; their values are
+// never used (absent codes, lanes past the last row). The host keeps the
+// stencil SpMV to shards with xlen * 8 < 2^31 (System::build_stencil).
+struct SRes {
+  __amdgpu_buffer_rsrc_t x[3];
+  __amdgpu_buffer_rsrc_t code;
+};
+
+template <int NX, int CB>
+__device__ __forceinline__ SRes st_res(const SpmvArgs& a, const double* const (&xs)[3]) {
+  SRes r;
+#pragma unroll
+  for (int v = 0; v < NX; ++v)
+    r.x[v] = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(xs[v]), 0,
+                                               (int)(a.xlen * 8), 0x00020000);
+  r.code = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.scode), 0, (int)(a.n * CB),
+                                             0x00020000);
+  return r;
+}
+
+// 16 bytes at byte offset `off` of a buffer (aux 2: non-temporal).
+template <int AUX = 0>
+__device__ __forceinline__ dbl2v st_bld2(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(dbl2v, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX));
+}
+
+// row0: the visit's first row (launch-relative, uniform); the lane's rows are
+// row0 + 2 tid, row0 + 2 tid + 1 (may lie past the last own row: x loads use
+// them as is -- rows past the own rows are halo rows, which the +-1
+// neighbours of the last own rows need); rr: the lane's first row clamped to
+// the own rows (own-row operands).
 template <int EPI, bool RELOAD, int NTM, int NX, int NFAR, int CB>
 __device__ __forceinline__ void st_issue(SStage<NX, NFAR, CB>& st, const SpmvArgs& a,
-                                         const double* const (&xs)[3], int64_t rl, int64_t rr) {
+                                         const SRes& res, int64_t row0, int tid, int64_t rr) {
   using T = EpiTraits<EPI>;
+  constexpr int kCodeAux = (NTM & 1) ? 2 : 0;  // codes: streamed once (non-temporal)
+  // codes of rows 2t, 2t+1 (lanes past the last row read 0: inactive)
+  const uint32_t coff = (uint32_t)(row0 * CB) + (uint32_t)tid * (2 * CB);
   if constexpr (CB == 8) {
-    const uint64_t* cp = static_cast<const uint64_t*>(a.scode) + rr;
     typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-    u64x2 c;
-    if constexpr (NTM & 1)  // codes: streamed once (non-temporal)
-      c = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(cp));
-    else
-      c = *reinterpret_cast<const u64x2*>(cp);
+    const u64x2 c = __builtin_bit_cast(
+        u64x2, __builtin_amdgcn_raw_buffer_load_b128(res.code, coff, 0, kCodeAux));
     st.clo = c.x;
     st.chi = c.y;
   } else if constexpr (CB == 4) {
-    const uint32_t* cp = static_cast<const uint32_t*>(a.scode) + rr;
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-    u32x2 c;
-    if constexpr (NTM & 1)
-      c = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(cp));
-    else
-      c = *reinterpret_cast<const u32x2*>(cp);
+    const u32x2 c = __builtin_bit_cast(
+        u32x2, __builtin_amdgcn_raw_buffer_load_b64(res.code, coff, 0, kCodeAux));
     st.clo = c.x;
     st.chi = c.y;
-  } else {  // CB == 2: both rows' uint16 codes in one dword (rr even)
-    const uint32_t* cp = reinterpret_cast<const uint32_t*>(static_cast<const uint16_t*>(a.scode) + rr);
-    uint32_t c;
-    if constexpr (NTM & 1)
-      c = __builtin_nontemporal_load(cp);
-    else
-      c = *cp;
+  } else {  // CB == 2: both rows' uint16 codes in one dword
+    const uint32_t c = __builtin_amdgcn_raw_buffer_load_b32(res.code, coff, 0, kCodeAux);
     st.clo = c & 0xFFFFu;
     st.chi = c >> 16;
   }
-  const int64_t xi = a.xoff + rl;
+  // x offsets: uniform (xoff + row0 + o) * 8, plus 16 bytes per lane
+  const int64_t ub = (a.xoff + row0) * 8;
+  const uint32_t lb = (uint32_t)tid * 16u;
   const int64_t W = (int64_t)a.st_P * kSBlock;
 #pragma unroll
-  for (int v = 0; v < NX; ++v) st.nxt[v] = st_ld2(xs[v], xi + W, a.xlen);
+  for (int v = 0; v < NX; ++v) st.nxt[v] = st_bld2(res.x[v], (uint32_t)(ub + W * 8) + lb);
 #pragma unroll
   for (int f = 0; f < NFAR; ++f)
 #pragma unroll
-    for (int v = 0; v < NX; ++v) st.far[f][v] = st_ld2(xs[v], xi + a.st_far[f], a.xlen);
+    for (int v = 0; v < NX; ++v)
+      st.far[f][v] = st_bld2(res.x[v], (uint32_t)(ub + (int64_t)a.st_far[f] * 8) + lb);
   if constexpr (is_step<EPI>()) {
     st.u1 = *reinterpret_cast<const dbl2v*>(a.u1 + rr);
     st.u2 = *reinterpret_cast<const dbl2v*>(a.u2 + rr);
@@ -141,8 +166,8 @@ __device__ __forceinline__ void st_issue(SStage<NX, NFAR, CB>& st, const SpmvArg
   if constexpr (RELOAD) {
 #pragma unroll
     for (int v = 0; v < NX; ++v) {
-      st.cen[v] = st_ld2(xs[v], xi, a.xlen);
-      st.prv[v] = st_ld2(xs[v], xi - W, a.xlen);
+      st.cen[v] = st_bld2(res.x[v], (uint32_t)ub + lb);
+      st.prv[v] = st_bld2(res.x[v], (uint32_t)(ub - W * 8) + lb);
     }
   }
 }
@@ -256,10 +281,12 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
   const double* const xs[3] = {a.x1, a.x2, a.x3};
   dbl2v cen[NX], prv[NX];  // carried: x at the rows, x at the rows - W
   SStage<NX, NFAR, CB> sA, sB;
+  const SRes res = st_res<NX, CB>(a, xs);
   int buf = 0;
   auto issue = [&](SStage<NX, NFAR, CB>& st, int64_t z) {
-    const int64_t rl = phys(blk(z)) * kSBlock + 2 * tid;
-    st_issue<EPI, RELOAD, NTM>(st, a, xs, rl, rl < a.n ? rl : a.n - 2);
+    const int64_t row0 = phys(blk(z)) * kSBlock;
+    const int64_t rl = row0 + 2 * tid;
+    st_issue<EPI, RELOAD, NTM>(st, a, res, row0, tid, rl < a.n ? rl : a.n - 2);
   };
   auto issue_edges = [&](SStage<NX, NFAR, CB>& st, int64_t z) {
     st_issue_edges(st, a, xs, phys(blk(z)) * kSBlock);
@@ -336,8 +363,10 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
       constexpr unsigned kNone = (1u << CB) - 1u;  // no entry
       const unsigned clo = (unsigned)(cur.clo >> (CB * k)) & kNone;
       const unsigned chi = (unsigned)(cur.chi >> (CB * k)) & kNone;
-      const double vlo = s_tab[clo == kNone ? 0u : clo];
-      const double vhi = s_tab[chi == kNone ? 0u : chi];
+      // an absent code reads an unused table entry (s_tab has kVdMax
+      // slots); its product is dropped below
+      const double vlo = s_tab[clo];
+      const double vhi = s_tab[chi];
       double xlo[NV], xhi[NV];
       if (kind == SK_CENTER) {
 #pragma unroll
@@ -371,13 +400,23 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
           for (int v = 0; v < NV; ++v) { xlo[v] = g[v].x; xhi[v] = g[v].y; }
         }
       }
-      if (clo != kNone) {
+      // Slot k present in both rows of every lane of the wave (the common
+      // case: absent entries sit at the grid's faces): no selects.
+      if (__builtin_amdgcn_ballot_w64(clo == kNone || chi == kNone) == 0) {
 #pragma unroll
-        for (int v = 0; v < NV; ++v) slo[v] = slo[v] + vlo * xlo[v];
-      }
-      if (chi != kNone) {
+        for (int v = 0; v < NV; ++v) {
+          slo[v] = slo[v] + vlo * xlo[v];
+          shi[v] = shi[v] + vhi * xhi[v];
+        }
+      } else {
+        if (clo != kNone) {
 #pragma unroll
-        for (int v = 0; v < NV; ++v) shi[v] = shi[v] + vhi * xhi[v];
+          for (int v = 0; v < NV; ++v) slo[v] = slo[v] + vlo * xlo[v];
+        }
+        if (chi != kNone) {
+#pragma unroll
+          for (int v = 0; v < NV; ++v) shi[v] = shi[v] + vhi * xhi[v];
+        }
       }
     }
     // (5) epilogue: row 2t, then row 2t+1 (products in that order)
