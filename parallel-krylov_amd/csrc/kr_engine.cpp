@@ -77,6 +77,7 @@ const char* epi_name(SpmvEpi e) {
     case EPI_STEP_MRR_X: return "spmv_step_mrr_x";
     case EPI_STEP_KCG: return "spmv_step_kcg";
     case EPI_STEP_MRR_FIRST2: return "spmv_step_mrr_first2";
+    case EPI_XY_VP: return "spmv_xy_vp";
   }
   return "spmv?";
 }
@@ -1025,6 +1026,10 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
                   int slot0, const StepOps* st) {
   const bool dual = (epi == EPI_DUAL_NONE || epi == EPI_DUAL_MRR || epi == EPI_DUAL_KCG);
   const bool virt = epi == EPI_STEP_MRR_FIRST2;
+  const bool vp = epi == EPI_XY_VP;  // CG's virtual p (System::spmv_vp)
+  KR_REQUIRE(!vp || (in2 >= 0 && st && st->u1 >= 0 && st->u1 != in1 && st->u1 != in2 &&
+                     vp_pro.sop == SC_CG_BETA),
+             "virtual-p SpMV: r / p output missing or aliased, or no scalar step");
   const bool step = (epi == EPI_STEP_MRR_NOX || epi == EPI_STEP_MRR_X2 ||
                      epi == EPI_STEP_MRR_X || epi == EPI_STEP_KCG || virt);
   KR_REQUIRE(!step || (st && st->u1 >= 0 && st->u2 >= 0 && out1 != in1),
@@ -1033,7 +1038,7 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
   KR_REQUIRE(!step_x || (st->us >= 0 && st->ud >= 0), "fused step: x operands missing");
   KR_REQUIRE(!virt || (in2 >= 0 && st->x3 >= 0 && st->u1 != in2 && st->u1 != st->x3),
              "fused first step: y0/Ar1 missing or y written over a gathered input");
-  const int hx2 = (dual || virt) ? in2 : -1;  // vectors whose halo the SpMV reads
+  const int hx2 = (dual || virt || vp) ? in2 : -1;  // vectors whose halo the SpMV reads
   const int hx3 = virt ? st->x3 : -1;
   KR_REQUIRE(slot0 + spmv_products(epi) <= kMaxSlots, "reduction slots exhausted");
   // one decision for every shard of every rank (the same summation order as
@@ -1060,7 +1065,7 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
     a.val = s.val;
     a.n = rows;
     a.x1 = s.vec[in1];
-    a.x2 = (dual || virt) ? s.vec[in2] : nullptr;
+    a.x2 = (dual || virt || vp) ? s.vec[in2] : nullptr;
     a.xoff = s.pad + r_begin;
     a.y1 = s.own(out1) + r_begin;
     a.y2 = dual ? s.own(out2) + r_begin : nullptr;
@@ -1125,6 +1130,19 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
       a.ncols = n_global;
       a.xcol0 = s.pad - s.row0;  // local index of global column 0
     }
+    if (vp) {
+      a.x3 = s.vec[in2];  // not read by the formula; gathered beside x2 by the row walks
+      a.u1 = s.own(st->u1) + r_begin;
+      a.pro = (int)SC_CG_BETA + 1;
+      a.pro_part = s.partials;
+      a.pro_stride = s.pstride;
+      for (int q = 0; q < 5; ++q) a.pro_cnt[q] = s.slot_n[q];
+      a.st = s.st;
+      a.pro_it = vp_pro.it;
+      a.pro_h = vp_pro.h;
+      a.pro_par = vp_pro.par;
+      a.pro_thr = vp_pro.thr;
+    }
     if (step) {
       a.u1 = s.own(st->u1) + r_begin;
       a.u2 = s.own(st->u2) + r_begin;
@@ -1147,7 +1165,8 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
     // fused step: u1, u2 read and written (+ x read and written)
     // fused first step: inputs r0, y0, Ar1 (3 x 8N, one counted below as
     // x), z and x read, y z r x written
-    const double extra = virt ? 64.0 * s.n
+    const double extra = vp ? 16.0 * s.n  // r gathered, p stored
+                         : virt ? 64.0 * s.n
                          : step ? (step_x ? 48.0 : 32.0) * s.n
                                 : (b >= 0 || e >= 0) ? 8.0 * s.n : 0.0;
     if (s.dense) return 8.0 * s.nnz + nv * 8.0 * (n_global + s.n) + extra;
@@ -1356,8 +1375,34 @@ bool System::fused_scalars() const {
   return !comm && shards.size() == 1;
 }
 
+bool System::vp_ok() const {
+  const char* env = getenv("KR_CG_VP");
+  if (env && atoi(env) == 0) return false;
+  if (!fused_scalars()) return false;
+  const Shard& s = shards[0];
+  if (s.dense || s.n == 0) return false;
+  if (s.scode || s.dia) return true;
+  // the row walk v2 (16-byte aligned val/col, >= 4 entries, short rows)
+  const bool vec = ((reinterpret_cast<uintptr_t>(s.val) | reinterpret_cast<uintptr_t>(s.col)) &
+                    15) == 0;
+  return vec && s.nnz >= 4 && (double)s.nnz < kLongRow * (double)s.n;
+}
+
+void System::spmv_vp(int p_old, int r, int out, int p_new, int64_t it, int h, int par,
+                     double thr) {
+  vp_pro.sop = SC_CG_BETA;
+  vp_pro.it = it;
+  vp_pro.h = h;
+  vp_pro.par = par;
+  vp_pro.thr = thr;
+  StepOps st;
+  st.u1 = p_new;
+  spmv(EPI_XY_VP, p_old, r, out, -1, -1, -1, 3, &st);
+  vp_pro.sop = -1;
+}
+
 void System::ew_pro(EwOp op, ScalarOp sop, std::array<int, 6> ids, int slot0, int64_t it, int h,
-                    int par, double thr) {
+                    int par, double thr, int s1) {
   KR_REQUIRE(slot0 + ew_products(op) <= kMaxSlots, "reduction slots exhausted");
   Shard& s = shards[0];
   KR_HIP_CHECK(hipSetDevice(s.dev));
@@ -1377,6 +1422,7 @@ void System::ew_pro(EwOp op, ScalarOp sop, std::array<int, 6> ids, int slot0, in
   a.pro_h = h;
   a.pro_par = par;
   a.pro_thr = thr;
+  a.pro_s1 = s1;
   for (int p = 0; p < ew_products(op); ++p) s.slot_n[slot0 + p] = s.grid;
   hipEvent_t t0 = nullptr;
   const char* nm = ew_name(op);
@@ -1537,7 +1583,8 @@ int scalar_batch() {
 // --------------------------------------------------------------------- CG
 // v3/gpu/cg.py:8-51 (oracle v3/cpu/cg.py:7-48)
 class CgSession : public Base {
-  enum { X, B, R, P, V, NV };
+  enum { X, B, R, P, V, P2, NV };
+  int pc = P;  // p's buffer: EPI_XY_VP writes the new p to the other one
   double gamma = 0;
   bool dev = false;
   double thr = 0;
@@ -1550,19 +1597,34 @@ class CgSession : public Base {
                                          prm.maxiter - i});
     sys->dev_stop = true;
     const bool fused = sys->fused_scalars();
+    // fused scalars + virtual p: iteration j > 0 of the batch folds the
+    // previous iteration's beta step and p = r + beta p into its SpMV, so an
+    // iteration is 2 launches (the batch's last one keeps EW_CG_P, whose
+    // beta step the host reads back)
+    const bool vpf = fused && sys->vp_ok();
     for (int64_t j = 0; j < m; ++j) {
       if (j > 0) sys->prof_active = (sys->prof_tick++ % sys->profile_every) == 0;
-      sys->spmv(EPI_XY, P, -1, V, -1, -1, -1, 0);              // v = A p ; sigma
       if (fused) {  // the scalar steps inside the vector kernels: 3 launches
         const int par = (int)((i + j) & 1);
-        sys->ew_pro(EW_CG, SC_CG_ALPHA, {X, P, R, V, -1, -1}, 0, i + j, (int)j, par, thr);
-        sys->ew_pro(EW_CG_P, SC_CG_BETA, {P, R, -1, -1, -1, -1}, 0, i + j, (int)j, par, thr);
+        int s1 = 1;
+        if (vpf && j > 0) {
+          const int pn = pc == P ? P2 : P;
+          sys->spmv_vp(pc, R, V, pn, i + j - 1, (int)j - 1, par ^ 1, thr);  // beta; p; v = A p
+          pc = pn;
+          s1 = 4;  // sigma: slot 4 (the SpMV's products sit in slots 3..5)
+        } else {
+          sys->spmv(EPI_XY, pc, -1, V, -1, -1, -1, 0);  // v = A p ; sigma
+        }
+        sys->ew_pro(EW_CG, SC_CG_ALPHA, {X, pc, R, V, -1, -1}, 0, i + j, (int)j, par, thr, s1);
+        if (!vpf || j == m - 1)
+          sys->ew_pro(EW_CG_P, SC_CG_BETA, {pc, R, -1, -1, -1, -1}, 0, i + j, (int)j, par, thr);
         continue;
       }
+      sys->spmv(EPI_XY, pc, -1, V, -1, -1, -1, 0);              // v = A p ; sigma
       sys->scalar(SC_CG_ALPHA, 1 << 1, i + j, (int)j, thr);     // alpha = gamma / sigma
-      sys->ew_dev(EW_CG, ST_C0, {X, P, R, V, -1, -1}, 0);       // x += a p ; r -= a v
+      sys->ew_dev(EW_CG, ST_C0, {X, pc, R, V, -1, -1}, 0);      // x += a p ; r -= a v
       sys->scalar(SC_CG_BETA, 1 << 0, i + j, (int)j, thr);      // beta, gamma, test
-      sys->ew_dev(EW_CG_P, ST_C2, {P, R, -1, -1, -1, -1}, 0);  // p = r + b p
+      sys->ew_dev(EW_CG_P, ST_C2, {pc, R, -1, -1, -1, -1}, 0);  // p = r + b p
     }
     sys->dev_stop = false;
     sys->scalar_state_read();
@@ -1589,6 +1651,7 @@ class CgSession : public Base {
     sys->spmv(EPI_BMINUS, X, -1, R, -1, -1, B, 0);  // r = b - A x
     gamma = sys->reduce(1)[0];                      // gamma = <r,r>
     sys->copy_own(P, R);                            // p = r.copy()
+    pc = P;
     dev = sys->device_scalars() && !prm.nan_guard;  // the guard tests every entry on the host
     if (dev) {
       thr = conv_threshold(bnorm, prm.tol);
@@ -1616,14 +1679,14 @@ class CgSession : public Base {
       if (qpos >= q.size()) run_batch();
       gamma = q[qpos++];
     } else {
-      sys->spmv(EPI_XY, P, -1, V, -1, -1, -1, 0);  // v = A p ; sigma = <p,v>
+      sys->spmv(EPI_XY, pc, -1, V, -1, -1, -1, 0);  // v = A p ; sigma = <p,v>
       const double sigma = sys->reduce(3)[1];
       const double alpha = gamma / sigma;
-      sys->ew(EW_CG, alpha, 0, {X, P, R, V, -1, -1}, 0);  // x += a p ; r -= a v
+      sys->ew(EW_CG, alpha, 0, {X, pc, R, V, -1, -1}, 0);  // x += a p ; r -= a v
       const double gnew = sys->reduce(1)[0];
       const double beta = gnew / gamma;
       gamma = gnew;
-      sys->ew(EW_CG_P, beta, 0, {P, R, -1, -1, -1, -1}, 0);  // p = r + b p
+      sys->ew(EW_CG_P, beta, 0, {pc, R, -1, -1, -1, -1}, 0);  // p = r + b p
     }
     i += 1;
     set_nosl(i, i);

@@ -217,7 +217,21 @@ struct System {
   // KR_FUSE_SCALAR=0 keeps the separate scalar kernel (A/B).
   bool fused_scalars() const;
   void ew_pro(EwOp op, ScalarOp sop, std::array<int, 6> ids, int slot0, int64_t it, int h,
-              int par, double thr);
+              int par, double thr, int s1 = 1);
+  // CG's p update folded into the next SpMV (EPI_XY_VP): the SpMV runs the
+  // SC_CG_BETA step of iteration `it` (ST_HIST slot h, gamma parity par)
+  // over the EW_CG partials in slot 0, gathers p = r + beta p_old, stores
+  // p_new and v = A p, products <p,p> <p,v> <v,v> in slots 3..5. vp_ok():
+  // one shard without a communicator (the fused scalar steps), a stencil or
+  // short-row CSR shard, KR_CG_VP != 0.
+  struct VpPro {
+    int sop = -1;
+    int64_t it = 0;
+    int h = 0, par = 0;
+    double thr = 0;
+  } vp_pro;
+  bool vp_ok() const;
+  void spmv_vp(int p_old, int r, int out, int p_new, int64_t it, int h, int par, double thr);
   bool dev_stop = false;
   // Device->host of the summed slots [0, nslots): the one host sync point.
   std::vector<double> reduce(int nslots);

@@ -69,6 +69,14 @@ enum SpmvEpi : int {
   // (c2, c3) runs in the epilogue: u1 (y) and y1 (r) are written to buffers
   // other than x2 / x1, which other rows still gather. Row walk v2 only.
   EPI_STEP_MRR_FIRST2,
+  // CG with device-resident scalars on one shard: the SpMV runs the
+  // SC_CG_BETA scalar step itself (SpmvArgs::pro: beta = gnew / gamma, the
+  // convergence test) and multiplies the virtual p = r + beta * p_old,
+  // formed at every gathered column from x1 = p_old, x2 = r exactly as
+  // ew_kernel<EW_CG_P> rounds it; the own rows' p is stored to u1 (a
+  // different buffer than x1: other rows still gather p_old), y1 = A p,
+  // products <p,p> <p,y> <y,y> as EPI_XY. Replaces EW_CG_P + EPI_XY.
+  EPI_XY_VP,
 };
 int spmv_products(SpmvEpi epi);
 
@@ -163,6 +171,20 @@ struct SpmvArgs {
   int32_t st_kind[8] = {};
   int32_t st_far[4] = {};
   double* scratch = nullptr;  // >= 2 doubles, 16-byte aligned: stores of lanes past the last row
+  // Fused scalar step (EPI_XY_VP; the fields of EwArgs::pro): every
+  // workgroup first runs scalar statement pro - 1 from the reduction
+  // partials pro_part[q * pro_stride + 0 .. pro_cnt[q]) and takes c0 from it.
+  int pro = 0;
+  const double* pro_part = nullptr;
+  int pro_stride = 0;
+  int pro_cnt[5] = {};
+  double* st = nullptr;
+  int64_t pro_it = 0;
+  int pro_h = 0;
+  int pro_par = 0;
+  int pro_check = 1;
+  double pro_thr = 0;
+  int pro_s1 = 1;
 };
 // Rows per row block of the stencil SpMV (2 per lane; kr_stencil.h).
 constexpr int kStencilBlock = 2 * kBlock;
@@ -223,6 +245,7 @@ struct EwArgs {
   int pro_par = 0;                 // CG: gamma of this iteration in st[gamma_slot(par)]
   int pro_check = 1;
   double pro_thr = 0;
+  int pro_s1 = 1;                  // SC_CG_ALPHA: sigma's slot (EPI_XY: 1, EPI_XY_VP: 4)
 };
 void launch_ew(EwOp op, const EwArgs& a, hipStream_t s);
 

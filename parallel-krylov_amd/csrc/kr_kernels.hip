@@ -169,7 +169,7 @@ __device__ bool ew_prologue(const EwArgs& a, double* s_red, double& c0, double& 
   c1 = 0.0;
   switch (a.pro - 1) {
     case SC_CG_ALPHA: {  // alpha = gamma / sigma  (v3/gpu/cg.py:33)
-      const double sigma = slot(1);
+      const double sigma = slot(a.pro_s1);
       c0 = st[gamma_slot(a.pro_par)] / sigma;
       return true;
     }
@@ -764,6 +764,7 @@ int spmv_products(SpmvEpi epi) {
     case EPI_STEP_MRR_X:
     case EPI_STEP_KCG:
     case EPI_STEP_MRR_FIRST2: return 0;
+    case EPI_XY_VP: return EpiTraits<EPI_XY_VP>::NP;
   }
   return 0;
 }
@@ -792,6 +793,7 @@ void launch_spmv_grid(SpmvEpi epi, const SpmvArgs& a, int nblocks, hipStream_t s
     KR_CASE(EPI_STEP_MRR_X)
     KR_CASE(EPI_STEP_KCG)
     KR_CASE(EPI_STEP_MRR_FIRST2)
+    KR_CASE(EPI_XY_VP)
 #undef KR_CASE
     default:
       throw Failure(KR_ERR_INVALID, "unknown SpMV epilogue");

@@ -119,6 +119,11 @@ template <>
 struct EpiTraits<EPI_STEP_KCG> : EpiStepTraits {};
 template <>
 struct EpiTraits<EPI_STEP_MRR_FIRST2> : EpiStepTraits {};
+template <>
+struct EpiTraits<EPI_XY_VP> {  // x = p_old, x2 = r at the row (p formed from them)
+  static constexpr int NP = 3, NV = 1;
+  static constexpr bool kX = true, kX2 = true, kE = false;
+};
 template <int EPI>
 constexpr bool is_step() {
   return EPI == EPI_STEP_MRR_NOX || EPI == EPI_STEP_MRR_X2 || EPI == EPI_STEP_MRR_X ||
@@ -127,7 +132,7 @@ constexpr bool is_step() {
 // The SpMV input is virtual: r1 = r0 - (c0*y0 + c1*Ar1) at every column.
 template <int EPI>
 constexpr bool is_virtual() {
-  return EPI == EPI_STEP_MRR_FIRST2;
+  return EPI == EPI_STEP_MRR_FIRST2 || EPI == EPI_XY_VP;
 }
 // r1 at one column, rounded exactly like ew_kernel<EW_MRR_NOX>'s step 0:
 // y1 = fl(fl(c0*y0) + fl(c1*ar1)), r1 = fl(r0 - y1).
@@ -137,6 +142,61 @@ __device__ __forceinline__ double virtual_r1(double c0, double c1, double r0, do
   const double t2 = c1 * ar1;
   const double y = t1 + t2;
   return r0 - y;
+}
+// CG's p = r + beta * p_old at one column, rounded as ew_kernel<EW_CG_P>.
+__device__ __forceinline__ double virtual_p(double beta, double p_old, double r) {
+  const double bp = beta * p_old;
+  return r + bp;
+}
+// The virtual SpMV input of epilogue EPI at one column from the physical
+// inputs x1, x2, x3 there (x3 unused by EPI_XY_VP).
+template <int EPI>
+__device__ __forceinline__ double virt_in(const SpmvArgs& a, double v1, double v2, double v3) {
+  if constexpr (EPI == EPI_XY_VP)
+    return virtual_p(a.c0, v1, v2);
+  else
+    return virtual_r1(a.c0, a.c1, v1, v2, v3);
+}
+
+// EPI_XY_VP's scalar step, run by every workgroup at kernel entry (after the
+// stop test): beta = gnew / gamma from the EW_CG partials (slot 0, summed in
+// the finalize order like ew_prologue / scalar_kernel), the convergence test
+// on gnew; workgroup 0 writes the state. Sets a.c0 = beta; false when the
+// test fired (the launch then does nothing, as EW_CG_P skips itself).
+__device__ __forceinline__ bool spmv_prologue_beta(SpmvArgs& a) {
+  __shared__ double s_r[4];
+  double t = 0.0;
+  for (int i = threadIdx.x; i < a.pro_cnt[0]; i += kBlock) t += a.pro_part[i];
+  for (int off = 32; off > 0; off >>= 1) t += __shfl_down(t, off, 64);
+  if ((threadIdx.x & 63) == 0) s_r[threadIdx.x >> 6] = t;
+  __syncthreads();
+  double g = s_r[0];
+  g = g + s_r[1];
+  g = g + s_r[2];
+  g = g + s_r[3];
+  __syncthreads();
+  const double gnew = 0.0 + g;
+  double* st = a.st;
+  a.c0 = gnew / st[gamma_slot(a.pro_par)];
+  const bool conv = a.pro_check && gnew >= 0.0 && gnew < a.pro_thr;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st[ST_HIST + a.pro_h] = gnew;
+    st[gamma_slot(a.pro_par ^ 1)] = gnew;
+    if (conv) {  // the test at the top of the next iteration
+      st[ST_STOP_AT] = (double)(a.pro_it + 1);
+      st[ST_STOP] = 1.0;
+    }
+  }
+  return !conv;
+}
+// Kernel entry of every SpMV kernel that serves virtual inputs.
+template <int EPI>
+__device__ __forceinline__ bool spmv_entry(SpmvArgs& a) {
+  if (a.stop && *a.stop != 0.0) return false;  // converged (device-resident scalars)
+  if constexpr (EPI == EPI_XY_VP) {
+    if (a.pro && !spmv_prologue_beta(a)) return false;
+  }
+  return true;
 }
 
 // Products of one row. x/x2: inputs at the row, y/y2: results, e: extra.
@@ -263,6 +323,11 @@ __device__ __forceinline__ EpiVals epi_values(const SpmvArgs& a, double sum1, do
     o.u1 = y2;
     o.u2 = z2;
     o.y1 = r1 - y2;  // Ar0 of step 2
+  } else if constexpr (EPI == EPI_XY_VP) {
+    const double pv = virtual_p(a.c0, in.x, in.x2);  // p at the own row
+    o.u1 = pv;
+    o.y1 = sum1;
+    epi_products<EPI_XY>(pv, 0.0, sum1, 0.0, 0.0, acc);
   } else if constexpr (is_step<EPI>()) {
     const double xv = in.x;
     if constexpr (EPI == EPI_STEP_KCG) {  // x = Ap0, sum1 = Ap1; u1 = x, u2 = Ar0
@@ -310,6 +375,7 @@ __device__ __forceinline__ void epi_store_row(const SpmvArgs& a, int64_t row, co
   } else {
     a.y1[row] = o.y1;
     if constexpr (EpiTraits<EPI>::NV == 2) a.y2[row] = o.y2;
+    if constexpr (EPI == EPI_XY_VP) a.u1[row] = o.u1;
   }
 }
 
@@ -334,6 +400,7 @@ __device__ __forceinline__ void epi_store_pair(const SpmvArgs& a, int64_t row, c
   } else {
     st2(a.y1, lo.y1, hi.y1);
     if constexpr (EpiTraits<EPI>::NV == 2) st2(a.y2, lo.y2, hi.y2);
+    if constexpr (EPI == EPI_XY_VP) st2(a.u1, lo.u1, hi.u1);
   }
 }
 
@@ -526,7 +593,7 @@ __device__ __forceinline__ void row_window(VS s_val, const int32_t* s_col,
 // Further gather batches of a row whose input is virtual (is_virtual):
 // x(c) = r1 at column c from r0 = x1, y0 = x2, Ar1 = x3 (SpmvArgs), summed in
 // stored order. Columns from the LDS column window or the offset masks.
-template <int GATHER, typename W, typename VS>
+template <int EPI, int GATHER, typename W, typename VS>
 __device__ __forceinline__ void row_window_virtual(VS s_val, const int32_t* s_col,
                                                    const int32_t* s_M, int64_t xrow,
                                                    const SpmvArgs& a, int js, int je, W& mrem,
@@ -555,7 +622,7 @@ __device__ __forceinline__ void row_window_virtual(VS s_val, const int32_t* s_co
     }
 #pragma unroll
     for (int u = 0; u < GATHER; ++u)
-      if (j + u < je) sum1 = sum1 + v[u] * virtual_r1(a.c0, a.c1, p1[u], p2[u], p3[u]);
+      if (j + u < je) sum1 = sum1 + v[u] * virt_in<EPI>(a, p1[u], p2[u], p3[u]);
   }
 }
 
@@ -1029,7 +1096,7 @@ __device__ __forceinline__ void stage_load2(Stage& st, const double* __restrict_
 template <typename RP, int EPI, bool VEC, int MW, bool DB = true, bool NT = false,
           bool VI = false>
 __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
-  if (a.stop && *a.stop != 0.0) return;  // converged (device-resident scalars)
+  if (!spmv_entry<EPI>(a)) return;  // converged / the fused scalar step's test fired
   using T = EpiTraits<EPI>;
   constexpr int NP = T::NP;
   constexpr int NV = T::NV;
@@ -1218,7 +1285,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
     for (int u = 0; u < G; ++u) {
       if (js + u < je) {
         if constexpr (VIRT) {
-          sum1 = sum1 + v[u] * virtual_r1(a.c0, a.c1, p1[u], p2[u], p3[u]);
+          sum1 = sum1 + v[u] * virt_in<EPI>(a, p1[u], p2[u], p3[u]);
         } else {
           sum1 = sum1 + v[u] * p1[u];
           if constexpr (NV == 2) sum2 = sum2 + v[u] * p2[u];
@@ -1228,9 +1295,9 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
     if (je - js > G) {
       if constexpr (VIRT) {
         if constexpr (COLS)
-          row_window_virtual<G>(sv, sc, nullptr, 0, a, js + G, je, mrem, sum1);
+          row_window_virtual<EPI, G>(sv, sc, nullptr, 0, a, js + G, je, mrem, sum1);
         else
-          row_window_virtual<G>(sv, nullptr, s_M, xrow, a, js + G, je, mrem, sum1);
+          row_window_virtual<EPI, G>(sv, nullptr, s_M, xrow, a, js + G, je, mrem, sum1);
       } else if constexpr (COLS) {
         row_window<NV, G>(sv, sc, x1, x2, js + G, je, sum1, sum2);
       } else {
@@ -1551,7 +1618,7 @@ __device__ __forceinline__ double2 window_pair(const double* __restrict__ x, int
 
 template <int EPI, int MW, int CH, bool XL>  // CH: offsets per load batch; XL: x window in LDS
 __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(SpmvArgs a) {
-  if (a.stop && *a.stop != 0.0) return;  // converged (device-resident scalars)
+  if (!spmv_entry<EPI>(a)) return;  // converged / the fused scalar step's test fired
   using T = EpiTraits<EPI>;
   constexpr int NP = T::NP;
   constexpr int NV = T::NV;
@@ -1604,8 +1671,8 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(SpmvArgs a) {
           if constexpr (VIRT) {  // r1 formed once per column, rounded as at every gather
             const double2 w2 = window_pair(x2, xi, a.xlen);
             const double2 w3 = window_pair(a.x3, xi, a.xlen);
-            d1[t] = make_double2(virtual_r1(a.c0, a.c1, w1.x, w2.x, w3.x),
-                                 virtual_r1(a.c0, a.c1, w1.y, w2.y, w3.y));
+            d1[t] = make_double2(virt_in<EPI>(a, w1.x, w2.x, w3.x),
+                                 virt_in<EPI>(a, w1.y, w2.y, w3.y));
           } else {
             d1[t] = w1;
           }
@@ -1639,7 +1706,7 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(SpmvArgs a) {
       for (int u = 0; u < CH; ++u) {
         const bool ok = k0 + u < nm && ((m >> min(k0 + u, nm - 1)) & 1);
         if constexpr (VIRT && !XL) {
-          const double t = sum1 + v[u] * virtual_r1(a.c0, a.c1, p1[u], p2[u], p3[u]);
+          const double t = sum1 + v[u] * virt_in<EPI>(a, p1[u], p2[u], p3[u]);
           sum1 = ok ? t : sum1;
         } else {
           const double t1 = sum1 + v[u] * p1[u];
@@ -1684,7 +1751,8 @@ template <int E>
 bool use_dia(const SpmvArgs& a) {
   if (!a.dia) return false;
   if (a.dia_wlen > 0) return true;  // x window in LDS: every epilogue
-  constexpr bool multi = EpiTraits<E>::NV == 2 || is_virtual<E>();
+  // (EPI_XY_VP routes as EPI_XY: the same kernel, so the same summation order)
+  constexpr bool multi = EpiTraits<E>::NV == 2 || E == EPI_STEP_MRR_FIRST2;
   if (!multi || a.long_rows) return true;
   const bool vec = ((reinterpret_cast<uintptr_t>(a.val) | reinterpret_cast<uintptr_t>(a.col)) &
                     15) == 0;

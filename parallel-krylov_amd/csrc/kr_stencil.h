@@ -35,6 +35,9 @@
 // (oracle/gpu_order.py restates this order).
 #pragma once
 
+#ifndef KR_ST_W4
+#define KR_ST_W4 4
+#endif
 constexpr int kSBlock = kStencilBlock;  // rows per stencil row block (2 per lane)
 constexpr int kSNear = 2;            // LDS line halo (offsets 0 < |o| <= kSNear)
 constexpr int kSLine = kSBlock + 2 * kSNear;
@@ -228,7 +231,7 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
   constexpr int NP = T::NP;
   constexpr int NV = T::NV;                    // sums (input vectors of the SpMV)
   constexpr bool VIRT = is_virtual<EPI>();     // operand r1 formed from x1, x2, x3
-  constexpr int NX = VIRT ? 3 : NV;            // physical input vectors
+  constexpr int NX = VIRT ? (EPI == EPI_XY_VP ? 2 : 3) : NV;  // physical input vectors
   __shared__ double s_red[(NP > 0 ? NP : 1) * 4];
   __shared__ double s_tab[kVdMax];
   __shared__ __attribute__((aligned(16))) double s_line[2][NV][kSLine];
@@ -280,7 +283,9 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
 
   const double* const xs[3] = {a.x1, a.x2, a.x3};
   dbl2v cen[NX], prv[NX];  // carried: x at the rows, x at the rows - W
-  SStage<NX, NFAR, CB> sA, sB;
+  // NTM bit 3: loads two visits ahead (three stage register sets) instead of one
+  constexpr int DEPTH = (!RELOAD && (NTM & 8)) ? 2 : 1;
+  SStage<NX, NFAR, CB> sA, sB, sC;
   const SRes res = st_res<NX, CB>(a, xs);
   int buf = 0;
   auto issue = [&](SStage<NX, NFAR, CB>& st, int64_t z) {
@@ -318,15 +323,15 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
     // (1) the next visit's loads, in flight across this visit's work. Issued
     // unconditionally (the last visit re-reads its own rows): a load under a
     // branch makes the compiler's wait counts assume the shorter path.
-    const int64_t zn = visit_ok(z + 1) ? z + 1 : z;
+    const int64_t zn = visit_ok(z + DEPTH) ? z + DEPTH : z;
     issue(nxs, zn);
     // (2) operand values at the rows: centers, the previous plane's centers
     dbl2v opc[NV], opp[NV];
     if constexpr (VIRT) {
-      opc[0] = dbl2v{virtual_r1(a.c0, a.c1, cen[0].x, cen[1].x, cen[2].x),
-                     virtual_r1(a.c0, a.c1, cen[0].y, cen[1].y, cen[2].y)};
-      opp[0] = dbl2v{virtual_r1(a.c0, a.c1, prv[0].x, prv[1].x, prv[2].x),
-                     virtual_r1(a.c0, a.c1, prv[0].y, prv[1].y, prv[2].y)};
+      opc[0] = dbl2v{virt_in<EPI>(a, cen[0].x, cen[1].x, cen[NX - 1].x),
+                     virt_in<EPI>(a, cen[0].y, cen[1].y, cen[NX - 1].y)};
+      opp[0] = dbl2v{virt_in<EPI>(a, prv[0].x, prv[1].x, prv[NX - 1].x),
+                     virt_in<EPI>(a, prv[0].y, prv[1].y, prv[NX - 1].y)};
     } else {
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
@@ -343,8 +348,8 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
       const dbl2v* e = tid == 0 ? cur.el : cur.er;
       if constexpr (VIRT) {
         *reinterpret_cast<dbl2v*>(dst) =
-            dbl2v{virtual_r1(a.c0, a.c1, e[0].x, e[1].x, e[2].x),
-                  virtual_r1(a.c0, a.c1, e[0].y, e[1].y, e[2].y)};
+            dbl2v{virt_in<EPI>(a, e[0].x, e[1].x, e[NX - 1].x),
+                  virt_in<EPI>(a, e[0].y, e[1].y, e[NX - 1].y)};
       } else {
 #pragma unroll
         for (int v = 0; v < NV; ++v) *reinterpret_cast<dbl2v*>(dst + v * kSLine) = e[v];
@@ -393,8 +398,8 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
             for (int v = 0; v < NX; ++v) g[v] = cur.far[f][v];
           }
         if constexpr (VIRT) {
-          xlo[0] = virtual_r1(a.c0, a.c1, g[0].x, g[1].x, g[2].x);
-          xhi[0] = virtual_r1(a.c0, a.c1, g[0].y, g[1].y, g[2].y);
+          xlo[0] = virt_in<EPI>(a, g[0].x, g[1].x, g[NX - 1].x);
+          xhi[0] = virt_in<EPI>(a, g[0].y, g[1].y, g[NX - 1].y);
         } else {
 #pragma unroll
           for (int v = 0; v < NV; ++v) { xlo[v] = g[v].x; xhi[v] = g[v].y; }
@@ -451,6 +456,11 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
   if (visit_ok(z)) {
     issue(sA, z);
     issue_edges(sA, z);
+    if constexpr (DEPTH == 2) {
+      const int64_t z1n = visit_ok(z + 1) ? z + 1 : z;
+      issue(sB, z1n);
+      issue_edges(sB, z1n);
+    }
     if constexpr (!RELOAD) {  // CENTER and PREV of the segment's first visit
       const int64_t xi = a.xoff + phys(z * P + p) * kSBlock + 2 * tid;
 #pragma unroll
@@ -464,13 +474,29 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
   // then start from an empty queue on every path into it.
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   __syncthreads();  // s_tab
-  for (;;) {
-    if (!visit_ok(z)) break;
-    visit(sA, sB, z);
-    ++z;
-    if (!visit_ok(z)) break;
-    visit(sB, sA, z);
-    ++z;
+  if constexpr (DEPTH == 2) {
+    // stage of visit z: A, B, C, A, ...; visit z issues z + 2 into the stage
+    // visit z - 1 consumed
+    for (;;) {
+      if (!visit_ok(z)) break;
+      visit(sA, sC, z);
+      ++z;
+      if (!visit_ok(z)) break;
+      visit(sB, sA, z);
+      ++z;
+      if (!visit_ok(z)) break;
+      visit(sC, sB, z);
+      ++z;
+    }
+  } else {
+    for (;;) {
+      if (!visit_ok(z)) break;
+      visit(sA, sB, z);
+      ++z;
+      if (!visit_ok(z)) break;
+      visit(sB, sA, z);
+      ++z;
+    }
   }
   __syncthreads();
   block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
@@ -478,15 +504,23 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
 
 template <int EPI, int NFAR, uint32_t PAT, bool RELOAD, int NTM = 3, int CB = 8>
 __global__ __launch_bounds__(kBlock) void spmv_stencil_kernel(SpmvArgs a) {
+  if (!spmv_entry<EPI>(a)) return;  // converged / the fused scalar step's test fired
   spmv_stencil_body<EPI, NFAR, PAT, RELOAD, NTM, CB>(a);
 }
 // The dual (basis) SpMVs fit 128 VGPRs without spilling: 4 waves per SIMD
 // instead of 3 (512^3 dual -1-4 %, products-only -4 %, 64-plane slab -6/-12 %).
 // The three-vector first-steps kernel and the RELOAD walk would spill there.
 template <int EPI, int NFAR, uint32_t PAT, bool RELOAD, int NTM = 3, int CB = 8>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KR_ST_W4)))
 void spmv_stencil_kernel_w4(SpmvArgs a) {
+  if (!spmv_entry<EPI>(a)) return;
   spmv_stencil_body<EPI, NFAR, PAT, RELOAD, NTM, CB>(a);
+}
+
+// KR_STENCIL_DEPTH=2 (A/B): the dual SpMVs load two visits ahead.
+inline int st_depth() {
+  const char* e = getenv("KR_STENCIL_DEPTH");
+  return e ? atoi(e) : 1;
 }
 
 // The 7-point pattern's launch at the shard's code width.
@@ -527,7 +561,10 @@ void spmv_stencil_launch_r(const SpmvArgs& a, int nblocks, hipStream_t s) {
     // Gram products)
     if (a.products_only) {
       if (pat7) {
-        st_launch_pat7<E, RELOAD, 7, !RELOAD>(a, nblocks, lds, s);
+        if (!RELOAD && st_depth() == 2)
+          st_launch_pat7<E, RELOAD, 15, false>(a, nblocks, lds, s);
+        else
+          st_launch_pat7<E, RELOAD, 7, !RELOAD>(a, nblocks, lds, s);
         return;
       }
       switch (a.st_nfar) {
@@ -550,7 +587,10 @@ void spmv_stencil_launch_r(const SpmvArgs& a, int nblocks, hipStream_t s) {
       }
     }
     constexpr bool w4 = !RELOAD && (E == EPI_DUAL_MRR || E == EPI_DUAL_KCG || E == EPI_DUAL_NONE);
-    st_launch_pat7<E, RELOAD, 3, w4>(a, nblocks, lds, s);
+    if (w4 && st_depth() == 2)
+      st_launch_pat7<E, RELOAD, 11, false>(a, nblocks, lds, s);
+    else
+      st_launch_pat7<E, RELOAD, 3, w4>(a, nblocks, lds, s);
     return;
   }
   switch (a.st_nfar) {

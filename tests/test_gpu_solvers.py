@@ -239,7 +239,8 @@ def test_fused_steps_bitwise_equal_unfused(monkeypatch, shards, method, matrix, 
     ("cg", ["poisson", 16, 2], 1e-10, 400), ("cg", ["poisson", 12, 3], 1e-8, 17),
     ("cg", ["banded", 3000, 13, 64, 0], 1e-10, 400), ("mrr", ["poisson", 16, 2], 1e-10, 400),
     ("mrr", ["poisson", 12, 3], 1e-8, 9), ("mrr", ["banded", 3000, 13, 64, 0], 1e-9, 400),
-    ("cg", ["poisson", 8, 2], 0.0, 40), ("mrr", ["poisson", 8, 2], 0.5, 40)])
+    ("cg", ["poisson", 8, 2], 0.0, 40), ("mrr", ["poisson", 8, 2], 0.5, 40),
+    ("cg", ["poisson", 64, 3], 1e-9, 90), ("cg", ["poisson", 64, 3], 0.0, 70)])
 @pytest.mark.parametrize("shards", ["0", "0,0,0"])
 def test_device_scalars_bitwise_equal_host(monkeypatch, shards, method, matrix, tol, maxiter):
     """CG / MrR with device-resident scalars (batches of iterations, the
@@ -250,17 +251,22 @@ def test_device_scalars_bitwise_equal_host(monkeypatch, shards, method, matrix, 
     tol = 0 and a test that fires at the first check -- on one shard (scalar
     steps fused into the vector kernels, or separate) and on three in-process
     shards (slot totals gathered on the first shard, summed in shard order;
-    coefficients and stop flag copied to the others)."""
+    coefficients and stop flag copied to the others). One-shard CG folds
+    the p update into the next SpMV (EPI_XY_VP) unless KR_CG_VP=0: the same
+    bits either way (64^3: the stencil kernel; 2-D: the row walk; banded:
+    the diagonal-offset kernel)."""
     A = golden_matrix(matrix)
     b = np.random.default_rng(11).standard_normal(A.shape[0])
     kw = dict(tol=tol, maxiter=maxiter)
     base = {"KRYLOV_AMD_SHARDS": shards}
     x0, i0 = _run_env(monkeypatch, {**base, "KR_DEVICE_SCALARS": "0"}, method, A, b, **kw)
-    for batch, fuse in (("1", "1"), ("3", "1"), ("32", "1"), ("32", "0")):
+    for batch, fuse, vp in (("1", "1", "1"), ("3", "1", "1"), ("32", "1", "1"),
+                            ("32", "1", "0"), ("32", "0", "1")):
         # one shard: the scalar step inside the vector kernels (fused) or
         # its own one-workgroup launch; several shards: always its own launch
         x1, i1 = _run_env(monkeypatch, {**base, "KR_DEVICE_SCALARS": "1", "KR_FUSE_SCALAR": fuse,
-                                        "KR_SCALAR_BATCH": batch}, method, A, b, **kw)
+                                        "KR_SCALAR_BATCH": batch, "KR_CG_VP": vp},
+                          method, A, b, **kw)
         np.testing.assert_array_equal(i1["nosl"], i0["nosl"])
         np.testing.assert_array_equal(i1["residual"], i0["residual"])
         np.testing.assert_array_equal(x1, x0)
