@@ -339,17 +339,7 @@ __global__ __launch_bounds__(kBlock) void finalize_kernel(const double* __restri
 // kernels (lane-strided, shuffle tree, then waves 0..3). Called by the whole
 // workgroup; every thread gets the result.
 __device__ double block_slot_sum(const double* __restrict__ part, int cnt, double* s_red) {
-  double t = 0.0;
-  for (int i = threadIdx.x; i < cnt; i += kBlock) t += part[i];
-  for (int off = 32; off > 0; off >>= 1) t += __shfl_down(t, off, 64);
-  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = t;
-  __syncthreads();
-  double r = s_red[0];
-  r = r + s_red[1];
-  r = r + s_red[2];
-  r = r + s_red[3];
-  __syncthreads();  // s_red may be reused by the caller
-  return r;
+  return slot_sum(part, cnt, s_red);  // kr_spmv.h
 }
 
 // As finalize_kernel, with a per-slot partial count (same fixed order).

@@ -143,6 +143,38 @@ __device__ __forceinline__ double virtual_r1(double c0, double c1, double r0, do
   const double y = t1 + t2;
   return r0 - y;
 }
+// Sum of the `cnt` partials of one slot in the fixed order of the finalize
+// kernels: lane t adds partials t, t + 256, ... in that order, then the
+// shuffle tree, then waves 0..3. The lane's partials are loaded 8 at a time
+// before they are added (in order), so a prologue pays about one load
+// latency instead of cnt / 256. Called by the whole workgroup; every thread
+// gets the result. s_red: 4 doubles.
+__device__ __forceinline__ double slot_sum(const double* __restrict__ part, int cnt,
+                                           double* s_red) {
+  constexpr int U = 8;
+  double t = 0.0;
+  for (int i0 = threadIdx.x; i0 < cnt; i0 += U * kBlock) {
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * kBlock;
+      v[u] = part[i < cnt ? i : i0];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i0 + u * kBlock < cnt) t += v[u];
+  }
+  for (int off = 32; off > 0; off >>= 1) t += __shfl_down(t, off, 64);
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = t;
+  __syncthreads();
+  double r = s_red[0];
+  r = r + s_red[1];
+  r = r + s_red[2];
+  r = r + s_red[3];
+  __syncthreads();  // s_red may be reused by the caller
+  return r;
+}
+
 // CG's p = r + beta * p_old at one column, rounded as ew_kernel<EW_CG_P>.
 __device__ __forceinline__ double virtual_p(double beta, double p_old, double r) {
   const double bp = beta * p_old;
@@ -165,17 +197,7 @@ __device__ __forceinline__ double virt_in(const SpmvArgs& a, double v1, double v
 // test fired (the launch then does nothing, as EW_CG_P skips itself).
 __device__ __forceinline__ bool spmv_prologue_beta(SpmvArgs& a) {
   __shared__ double s_r[4];
-  double t = 0.0;
-  for (int i = threadIdx.x; i < a.pro_cnt[0]; i += kBlock) t += a.pro_part[i];
-  for (int off = 32; off > 0; off >>= 1) t += __shfl_down(t, off, 64);
-  if ((threadIdx.x & 63) == 0) s_r[threadIdx.x >> 6] = t;
-  __syncthreads();
-  double g = s_r[0];
-  g = g + s_r[1];
-  g = g + s_r[2];
-  g = g + s_r[3];
-  __syncthreads();
-  const double gnew = 0.0 + g;
+  const double gnew = 0.0 + slot_sum(a.pro_part, a.pro_cnt[0], s_r);
   double* st = a.st;
   a.c0 = gnew / st[gamma_slot(a.pro_par)];
   const bool conv = a.pro_check && gnew >= 0.0 && gnew < a.pro_thr;
