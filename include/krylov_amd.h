@@ -39,6 +39,15 @@ extern "C" {
 #define KR_METHOD_KSKIPCG 2
 #define KR_METHOD_KSKIPMRR 3
 #define KR_METHOD_ADAPTIVE_KSKIPMRR 4
+/* Preconditioned and pipelined CG (reference v1/threads/pipeline/{pcg,
+ * chronopoulos_gear,gropp,pipeline}.py: `method(A, b, ilu, epsilon, T, pt)`),
+ * restated as the textbook algorithms those files name with a Jacobi
+ * preconditioner (kr_solve_set_precond). maxiter < 0 means
+ * 2N (v1/threads/common.py:47); iterations i = 1 .. maxiter-1. */
+#define KR_METHOD_PCG 5
+#define KR_METHOD_CG_GEAR 6
+#define KR_METHOD_GROPP 7
+#define KR_METHOD_PIPECG 8
 
 /* Library identification. */
 int kr_version(void);
@@ -308,6 +317,12 @@ typedef struct {
  * own rows (x0 may be NULL for zeros). Starts the timer. */
 int kr_solve_begin(kr_system* sys, const kr_solve_params* params,
                    const double* const* b_dev, const double* const* x0_dev);
+/* Jacobi preconditioner of the KR_METHOD_PCG .. KR_METHOD_PIPECG sessions
+ * begun after this call: d_dev[s] holds shard s's own rows of the diagonal d
+ * (M^-1 v = v / d: the `ilu.solve` of v1/threads/pipeline/pcg.py:27,45 and
+ * its siblings). The pointers are read at kr_solve_begin (copied into the
+ * session); d_dev == NULL restores the identity (d = 1). */
+int kr_solve_set_precond(kr_system* sys, const double* const* d_dev);
 /* Run up to `max_outer` further outer iterations (CG/MrR: iterations).
  * *done = 1 once converged or maxiter reached. */
 int kr_solve_step(kr_system* sys, int64_t max_outer, int* done);

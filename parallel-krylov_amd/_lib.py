@@ -15,7 +15,9 @@ _LIB_NAME = "libkrylov_amd.so"
 _lock = threading.Lock()
 _lib = None
 
-KR_METHOD = {"cg": 0, "mrr": 1, "kskipcg": 2, "kskipmrr": 3, "adaptivekskipmrr": 4}
+KR_METHOD = {"cg": 0, "mrr": 1, "kskipcg": 2, "kskipmrr": 3, "adaptivekskipmrr": 4,
+             # v1/threads/pipeline/*.py (include/krylov_amd.h KR_METHOD_PCG ..)
+             "pcg": 5, "chronopoulos_gear": 6, "gropp": 7, "pipeline": 8}
 KR_FORMAT = {0: "csr", 1: "stencil", 2: "dia", 3: "dense"}  # kr_system_shard_sched
 
 
@@ -97,6 +99,7 @@ _SIGNATURES = {
     "kr_system_csr": [_P, _I, _PP, _PI, _PP, _PP, _PI64],
     "kr_system_spmv": [_PP, _PP, _PP],
     "kr_solve_begin": [_P, ctypes.POINTER(SolveParams), _PP, _PP],
+    "kr_solve_set_precond": [_P, _PP],
     "kr_solve_step": [_P, _I64, _PI],
     "kr_solve_end": [_P, _PP, ctypes.POINTER(SolveResult)],
     "kr_solve_history": [_P, _PD, _PI64, _PI64, _I64],

@@ -742,6 +742,14 @@ int kr_solve_begin(kr_system* sys, const kr_solve_params* params, const double* 
   });
 }
 
+int kr_solve_set_precond(kr_system* sys, const double* const* d) {
+  return guarded([&] {
+    KR_REQUIRE(sys && sys->finalized, "system not finalized");
+    sys->precond.clear();
+    if (d) sys->precond.assign(d, d + sys->shards.size());
+  });
+}
+
 int kr_solve_step(kr_system* sys, int64_t max_outer, int* done) {
   return guarded([&] {
     KR_REQUIRE(sys, "NULL system");

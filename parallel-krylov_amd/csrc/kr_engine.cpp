@@ -52,6 +52,14 @@ int ew_vectors(EwOp op) {
     case EW_COPY: return 2;
     case EW_MRR_NOX: return 7;
     case EW_MRR_X2: return 9;
+    case EW_ONE: return 1;
+    case EW_PRE: return 3;
+    case EW_PCG: return 9;
+    case EW_CGG: return 12;
+    case EW_GROPP1: return 9;
+    case EW_GROPP2: return 6;
+    case EW_DIV: return 3;
+    case EW_PIPE: return 18;
   }
   return 0;
 }
@@ -94,6 +102,14 @@ const char* ew_name(EwOp op) {
     case EW_COPY: return "copy";
     case EW_MRR_NOX: return "update_mrr_nox";
     case EW_MRR_X2: return "update_mrr_x2";
+    case EW_ONE: return "fill_one";
+    case EW_PRE: return "precond";
+    case EW_PCG: return "update_pcg";
+    case EW_CGG: return "update_cg_gear";
+    case EW_GROPP1: return "update_gropp_xru";
+    case EW_GROPP2: return "update_gropp_ps";
+    case EW_DIV: return "precond_div";
+    case EW_PIPE: return "update_pipecg";
   }
   return "ew?";
 }
@@ -1233,13 +1249,21 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
 }
 
 void System::ew(EwOp op, double c0, double c1, std::array<int, 6> ids, int slot0) {
+  std::array<int, kEwOps> all;
+  all.fill(-1);
+  for (int q = 0; q < 6; ++q) all[q] = ids[q];
+  ew_n(op, c0, c1, all, slot0);
+}
+
+void System::ew_n(EwOp op, double c0, double c1, const std::array<int, kEwOps>& ids,
+                  int slot0) {
   KR_REQUIRE(slot0 + ew_products(op) <= kMaxSlots, "reduction slots exhausted");
   for (auto& s : shards) {
     KR_HIP_CHECK(hipSetDevice(s.dev));
     EwArgs a;
     a.c0 = c0;
     a.c1 = c1;
-    for (int q = 0; q < 6; ++q) a.p[q] = ids[q] >= 0 ? s.own(ids[q]) : nullptr;
+    for (int q = 0; q < kEwOps; ++q) a.p[q] = ids[q] >= 0 ? s.own(ids[q]) : nullptr;
     a.n = s.n;
     a.partials = s.partials + (size_t)slot0 * s.pstride;
     a.grid = s.grid;
@@ -2097,6 +2121,159 @@ class KskipCgSession : public Base {
   int result_x() const override { return X; }
 };
 
+// -------------------------------------------- preconditioned / pipelined CG
+// v1/threads/pipeline/{pcg,chronopoulos_gear,gropp,pipeline}.py, restated as
+// the textbook algorithms those files name (DESIGN.md §5b lists the defects
+// of the reference copies that the restatement fixes; oracle/pipecg.py is the
+// statement-for-statement CPU form). M^-1 v = v / d with the Jacobi diagonal
+// d (kr_solve_set_precond; none: d = 1, and v / 1.0 == v exactly). Loop
+// bookkeeping of v1/threads/common.py:41-52: iterations i = 1 .. maxiter-1,
+// residual[i] after the i-th update, nosl[i] = i. Scalars go through the
+// host (one sync per reduction point, as the CG host path); the reductions
+// that the algorithms make independent are fused into one sync.
+class PipeCgSession : public Base {
+  enum { X, B, R, U, D, P, S, W, Q, M, NN, Z, NV };
+  const int variant;  // KR_METHOD_PCG / _CG_GEAR / _GROPP / _PIPECG
+  double gamma = 0, delta = 0, alpha = 0, beta = 0;
+
+  std::array<int, kEwOps> ids(std::initializer_list<int> l) const {
+    std::array<int, kEwOps> a;
+    a.fill(-1);
+    int q = 0;
+    for (int v : l) a[q++] = v;
+    return a;
+  }
+
+ public:
+  explicit PipeCgSession(int v) : variant(v) {}
+
+  void begin(const double* const* b, const double* const* x0) override {
+    sys->alloc_vectors(NV);
+    load_bx(B, X, b, x0);
+    // d: the caller's diagonal, else ones
+    const bool have = !sys->precond.empty();
+    for (size_t li = 0; li < sys->shards.size(); ++li) {
+      Shard& s = sys->shards[li];
+      if (have && sys->precond[li]) {
+        KR_HIP_CHECK(hipSetDevice(s.dev));
+        KR_HIP_CHECK(hipMemcpyAsync(s.own(D), sys->precond[li], 8 * (size_t)s.n,
+                                    hipMemcpyDeviceToDevice, s.stream));
+      }
+    }
+    if (!have) sys->ew_n(EW_ONE, 0, 0, ids({D}), 0);
+    sys->spmv(EPI_BMINUS, X, -1, R, -1, -1, B, 0);      // r = b - A x
+    sys->ew_n(EW_PRE, 0, 0, ids({R, U, D}), 1);           // u = M^-1 r ; <r,r> <r,u>
+    const auto g = sys->reduce(3);                        // slot 0: <r,r> of the SpMV
+    set_entry(0, rel(g[0]));
+    set_nosl(0, 0);
+    gamma = g[2];                                         // <r,u>
+    switch (variant) {
+      case KR_METHOD_PCG:    // p = u.copy()  (pcg.py:28)
+      case KR_METHOD_GROPP:  // p = u.copy(); s = A p  (gropp.py:26-27)
+        sys->copy_own(P, U);
+        if (variant == KR_METHOD_GROPP) {
+          sys->spmv(EPI_XY, P, -1, S, -1, -1, -1, 0);     // s = A p ; <p,s>
+          delta = sys->reduce(3)[1];
+        }
+        break;
+      case KR_METHOD_CG_GEAR:  // w = A u; alpha = (r,u)/(w,u); beta = 0
+      case KR_METHOD_PIPECG: {  // w = A u; (r,u), (w,u) at the loop top
+        sys->spmv(EPI_XY, U, -1, W, -1, -1, -1, 0);       // w = A u ; <u,w>
+        delta = sys->reduce(3)[1];
+        alpha = gamma / delta;
+        beta = 0.0;
+        break;
+      }
+    }
+    i = 0;
+    index = 0;
+    start_timer();
+  }
+
+  bool step_once() override {
+    if (i + 1 >= prm.maxiter) return done = true;  // for i in range(1, max_iter) exhausted
+    const int64_t it = i + 1;
+    double rr = 0;
+    switch (variant) {
+      case KR_METHOD_PCG: {  // pcg.py:31-49
+        sys->spmv(EPI_XY, P, -1, S, -1, -1, -1, 0);             // s = A p ; <p,s>
+        const double sigma = sys->reduce(3)[1];
+        alpha = gamma / sigma;
+        sys->ew_n(EW_PCG, alpha, 0, ids({X, P, R, S, U, D}), 0);  // x, r, u ; <r,r> <r,u>
+        const auto g = sys->reduce(2);
+        rr = g[0];
+        if (!(rel(rr) < prm.tol)) {
+          const double gnew = g[1];
+          beta = gnew / gamma;
+          gamma = gnew;
+          sys->ew(EW_CG_P, beta, 0, {P, U, -1, -1, -1, -1}, 0);  // p = u + beta p
+        }
+        break;
+      }
+      case KR_METHOD_CG_GEAR: {  // chronopoulos_gear.py:36-51: one sync per iteration
+        sys->ew_n(EW_CGG, alpha, beta, ids({P, U, S, W, X, R, D}), 0);  // <r,r> <r,u>
+        sys->spmv(EPI_XY, U, -1, W, -1, -1, -1, 2);              // w = A u ; <u,w>: slot 3
+        const auto g = sys->reduce(5);
+        rr = g[0];
+        const double gnew = g[1];
+        delta = g[3];
+        beta = gnew / gamma;
+        alpha = gnew / (delta - beta * gnew / alpha);
+        gamma = gnew;
+        break;
+      }
+      case KR_METHOD_GROPP: {  // gropp.py:30-45
+        alpha = gamma / delta;
+        sys->ew_n(EW_GROPP1, alpha, 0, ids({X, P, R, S, U, D}), 0);  // <r,r> <r,u>
+        sys->spmv(EPI_NONE, U, -1, W, -1, -1, -1, 2);                 // w = A u (overlaps)
+        const auto g = sys->reduce(2);
+        rr = g[0];
+        if (!(rel(rr) < prm.tol)) {
+          const double gnew = g[1];
+          beta = gnew / gamma;
+          gamma = gnew;
+          sys->ew_n(EW_GROPP2, beta, 0, ids({P, U, S, W}), 0);  // p, s ; <p,s>
+          delta = sys->reduce(1)[0];
+        }
+        break;
+      }
+      case KR_METHOD_PIPECG: {  // pipeline.py:31-55: one sync per iteration
+        sys->ew_n(EW_DIV, 0, 0, ids({M, W, D}), 0);                   // m = M^-1 w
+        sys->spmv(EPI_NONE, M, -1, NN, -1, -1, -1, 0);                // n = A m
+        if (it > 1) {
+          beta = gamma / gold;
+          alpha = gamma / (delta - beta * gamma / alpha);
+        } else {
+          beta = 0.0;
+          alpha = gamma / delta;
+        }
+        gold = gamma;
+        sys->ew_n(EW_PIPE, alpha, beta, ids({Z, NN, Q, M, S, W, P, U, X, R}), 0);
+        const auto g = sys->reduce(3);                                // <r,r> <r,u> <w,u>
+        rr = g[0];
+        gamma = g[1];
+        delta = g[2];
+        break;
+      }
+      default: throw Failure(KR_ERR_INVALID, "unknown pipelined CG variant");
+    }
+    i = it;
+    index = i;
+    set_nosl(i, i);
+    set_entry(i, rel(rr));
+    if (residual[i] < prm.tol) {
+      converged = true;
+      return done = true;
+    }
+    if (guard_stop(i)) return true;
+    return false;
+  }
+  int result_x() const override { return X; }
+
+ private:
+  double gold = 0;  // pipelined CG: gamma of the previous iteration
+};
+
 }  // namespace
 
 std::unique_ptr<Session> make_session(System* sys, const kr_solve_params& p) {
@@ -2107,15 +2284,21 @@ std::unique_ptr<Session> make_session(System* sys, const kr_solve_params& p) {
     case KR_METHOD_KSKIPCG: s.reset(new KskipCgSession()); break;
     case KR_METHOD_KSKIPMRR: s.reset(new KskipMrrSession(false)); break;
     case KR_METHOD_ADAPTIVE_KSKIPMRR: s.reset(new KskipMrrSession(true)); break;
+    case KR_METHOD_PCG:
+    case KR_METHOD_CG_GEAR:
+    case KR_METHOD_GROPP:
+    case KR_METHOD_PIPECG: s.reset(new PipeCgSession(p.method)); break;
     default: throw Failure(KR_ERR_INVALID, "unknown method");
   }
   s->sys = sys;
   s->prm = p;
-  if (s->prm.maxiter < 0) s->prm.maxiter = sys->n_global;  // None -> N (v3/cpu/common.py:29-30)
+  const bool pipe = p.method >= KR_METHOD_PCG && p.method <= KR_METHOD_PIPECG;
+  if (s->prm.maxiter < 0)  // None -> N (v3/cpu/common.py:29-30); v1: 2N (v1/threads/common.py:47)
+    s->prm.maxiter = pipe ? 2 * sys->n_global : sys->n_global;
   // maxiter = 0: CG and k-skip CG return the initial residual; the MrR family
   // takes its first step unconditionally and writes nosl[1] of a length-1
   // array, an IndexError in the reference (v3/cpu/mrr.py:31, kskipmrr.py:32)
-  KR_REQUIRE(s->prm.maxiter > 0 || p.method == KR_METHOD_CG || p.method == KR_METHOD_KSKIPCG,
+  KR_REQUIRE(s->prm.maxiter > 0 || p.method == KR_METHOD_CG || p.method == KR_METHOD_KSKIPCG || pipe,
              "maxiter=0: the MrR family writes nosl[1] past its maxiter+1 entries (IndexError in the reference)");
   return s;
 }

@@ -200,6 +200,12 @@ struct System {
   void spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int b, int slot0,
             const StepOps* st = nullptr);
   void ew(EwOp op, double c0, double c1, std::array<int, 6> ids, int slot0);
+  // The same for ops with more than 6 operands (-1: unused slot).
+  void ew_n(EwOp op, double c0, double c1, const std::array<int, kEwOps>& ids, int slot0);
+  // Jacobi diagonal of the preconditioned / pipelined CG family, per local
+  // shard (own rows; kr_solve_set_precond), copied into the session's d
+  // vector at begin; empty / null: the identity (d = 1).
+  std::vector<const double*> precond;
   // Device-resident scalars (one shard per rank, or every shard in this
   // process): the vector kernel takes c0, c1 from st[coef], st[coef + 1];
   // scalar() runs one scalar_kernel step over the reductions in slots `need`

@@ -218,12 +218,27 @@ enum EwOp : int {
   EW_COPY,        // p0 <- p1
   EW_MRR_NOX,     // EW_MRR without the x update (x deferred to the next step)
   EW_MRR_X2,      // EW_MRR with xd = (xs - z_old) - z_new (two steps of x at once)
+  // Preconditioned / pipelined CG family (v1/threads/pipeline/*.py, DESIGN.md
+  // §5b); d = the Jacobi diagonal, M^-1 v = v / d.
+  EW_ONE,         // p0 = 1.0 (identity preconditioner: d = 1, v / 1.0 == v)
+  EW_PRE,         // u = r / d; <r,r> <r,u>                  (p: r u d)
+  EW_PCG,         // x += a p; r -= a s; u = r / d; <r,r> <r,u>        (x p r s u d)
+  EW_CGG,         // p = u + b p; s = w + b s; x += a p; r -= a s; u = r / d;
+                  // <r,r> <r,u>                             (p u s w x r d)
+  EW_GROPP1,      // x += a p; r -= a s; u -= a (s / d); <r,r> <r,u>  (x p r s u d)
+  EW_GROPP2,      // p = u + b p; s = w + b s; <p,s>         (p u s w)
+  EW_DIV,         // m = w / d                               (m w d)
+  EW_PIPE,        // z = n + b z; q = m + b q; s = w + b s; p = u + b p; x += a p;
+                  // r -= a s; u -= a q; w -= a z; <r,r> <r,u> <w,u>
+                  //                                         (z n q m s w p u x r)
 };
+// Operand slots of an elementwise op (EwArgs::p).
+constexpr int kEwOps = 10;
 int ew_products(EwOp op);
 
 struct EwArgs {
   double c0 = 0, c1 = 0;           // scalars (eta/alpha/gamma, zeta/beta)
-  double* p[6] = {};               // operand pointers, meaning per op
+  double* p[kEwOps] = {};          // operand pointers, meaning per op
   int64_t n = 0;
   double* partials = nullptr;
   int grid = 0;                    // workgroups launched

@@ -84,9 +84,43 @@ template <>
 struct EwTraits<EW_MRR_X2> {  // p: y ar1 z r xs xd
   static constexpr int NP = 0, R = 0b011111, W = 0b101101;
 };
+// Preconditioned / pipelined CG family (v1/threads/pipeline/*.py restated,
+// DESIGN.md §5b): Jacobi M^-1 v = v / d.
+template <>
+struct EwTraits<EW_ONE> {  // p: d
+  static constexpr int NP = 0, R = 0, W = 0b1;
+};
+template <>
+struct EwTraits<EW_PRE> {  // p: r u d
+  static constexpr int NP = 2, R = 0b101, W = 0b010;
+};
+template <>
+struct EwTraits<EW_PCG> {  // p: x p r s u d
+  static constexpr int NP = 2, R = 0b101111, W = 0b010101;
+};
+template <>
+struct EwTraits<EW_CGG> {  // p: p u s w x r d
+  static constexpr int NP = 2, R = 0b1111111, W = 0b0110111;
+};
+template <>
+struct EwTraits<EW_GROPP1> {  // p: x p r s u d
+  static constexpr int NP = 2, R = 0b111111, W = 0b010101;
+};
+template <>
+struct EwTraits<EW_GROPP2> {  // p: p u s w
+  static constexpr int NP = 1, R = 0b1111, W = 0b0101;
+};
+template <>
+struct EwTraits<EW_DIV> {  // p: m w d
+  static constexpr int NP = 0, R = 0b110, W = 0b001;
+};
+template <>
+struct EwTraits<EW_PIPE> {  // p: z n q m s w p u x r
+  static constexpr int NP = 3, R = 0b1111111111, W = 0b1111110101;
+};
 
 template <int OP>
-__device__ __forceinline__ void ew_elem(double c0, double c1, double (&v)[6],
+__device__ __forceinline__ void ew_elem(double c0, double c1, double (&v)[kEwOps],
                                         double (&acc)[EwTraits<OP>::NP > 0
                                                           ? EwTraits<OP>::NP
                                                           : 1]) {
@@ -147,6 +181,88 @@ __device__ __forceinline__ void ew_elem(double c0, double c1, double (&v)[6],
     v[0] = y;
     v[2] = z;
     v[3] = v[3] - y;
+  } else if constexpr (OP == EW_ONE) {
+    v[0] = 1.0;
+  } else if constexpr (OP == EW_PRE) {  // u = ilu.solve(r)  (pcg.py:27)
+    const double u = v[0] / v[2];
+    v[1] = u;
+    acc[0] += v[0] * v[0];
+    acc[1] += v[0] * u;
+  } else if constexpr (OP == EW_PCG) {  // c0 = alpha  (pcg.py:34-43)
+    const double ap = c0 * v[1];
+    v[0] = v[0] + ap;
+    const double as = c0 * v[3];
+    const double r = v[2] - as;
+    const double u = r / v[5];
+    v[2] = r;
+    v[4] = u;
+    acc[0] += r * r;
+    acc[1] += r * u;
+  } else if constexpr (OP == EW_CGG) {  // c0 = alpha, c1 = beta  (chronopoulos_gear.py:37-47)
+    const double bp = c1 * v[0];
+    const double p = v[1] + bp;
+    const double bs = c1 * v[2];
+    const double sv = v[3] + bs;
+    const double ap = c0 * p;
+    v[4] = v[4] + ap;
+    const double as = c0 * sv;
+    const double r = v[5] - as;
+    const double u = r / v[6];
+    v[0] = p;
+    v[2] = sv;
+    v[5] = r;
+    v[1] = u;
+    acc[0] += r * r;
+    acc[1] += r * u;
+  } else if constexpr (OP == EW_GROPP1) {  // c0 = alpha  (gropp.py:29-39)
+    const double q = v[3] / v[5];
+    const double ap = c0 * v[1];
+    v[0] = v[0] + ap;
+    const double as = c0 * v[3];
+    const double r = v[2] - as;
+    const double aq = c0 * q;
+    const double u = v[4] - aq;
+    v[2] = r;
+    v[4] = u;
+    acc[0] += r * r;
+    acc[1] += r * u;
+  } else if constexpr (OP == EW_GROPP2) {  // c0 = beta  (gropp.py:43-44, 28)
+    const double bp = c0 * v[0];
+    const double p = v[1] + bp;
+    const double bs = c0 * v[2];
+    const double sv = v[3] + bs;
+    v[0] = p;
+    v[2] = sv;
+    acc[0] += p * sv;
+  } else if constexpr (OP == EW_DIV) {  // m = ilu.solve(w)
+    v[0] = v[1] / v[2];
+  } else if constexpr (OP == EW_PIPE) {  // c0 = alpha, c1 = beta  (pipeline.py:43-55)
+    const double bz = c1 * v[0];
+    const double z = v[1] + bz;
+    const double bq = c1 * v[2];
+    const double q = v[3] + bq;
+    const double bs = c1 * v[4];
+    const double sv = v[5] + bs;
+    const double bp = c1 * v[6];
+    const double p = v[7] + bp;
+    const double ap = c0 * p;
+    v[8] = v[8] + ap;
+    const double as = c0 * sv;
+    const double r = v[9] - as;
+    const double aq = c0 * q;
+    const double u = v[7] - aq;
+    const double az = c0 * z;
+    const double w = v[5] - az;
+    v[0] = z;
+    v[2] = q;
+    v[4] = sv;
+    v[5] = w;
+    v[6] = p;
+    v[7] = u;
+    v[9] = r;
+    acc[0] += r * r;
+    acc[1] += r * u;
+    acc[2] += w * u;
   }
 }
 
@@ -235,12 +351,12 @@ __global__ __launch_bounds__(kBlock) void ew_kernel(EwArgs a) {
     // the next iteration's loads above this iteration's stores by itself).
     const int64_t npairs = a.n >> 1;
     for (int64_t q0 = t0; q0 < npairs; q0 += U * stride) {
-      double va[U][6], vb[U][6];
+      double va[U][kEwOps], vb[U][kEwOps];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t q = q0 + u * stride;
 #pragma unroll
-        for (int k = 0; k < 6; ++k) {
+        for (int k = 0; k < kEwOps; ++k) {
           if ((T::R & (1 << k)) && q < npairs) {
             const double2 d = reinterpret_cast<const double2*>(a.p[k])[q];
             va[u][k] = d.x;
@@ -257,7 +373,7 @@ __global__ __launch_bounds__(kBlock) void ew_kernel(EwArgs a) {
         ew_elem<OP>(c0, c1, va[u], acc);
         ew_elem<OP>(c0, c1, vb[u], acc);
 #pragma unroll
-        for (int k = 0; k < 6; ++k)
+        for (int k = 0; k < kEwOps; ++k)
           if (T::W & (1 << k)) {
             double2* dst = reinterpret_cast<double2*>(a.p[k]) + q;
             if constexpr (NTS) {
@@ -271,22 +387,22 @@ __global__ __launch_bounds__(kBlock) void ew_kernel(EwArgs a) {
     }
     if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
       const int64_t i = a.n - 1;
-      double v[6];
+      double v[kEwOps];
 #pragma unroll
-      for (int k = 0; k < 6; ++k) v[k] = (T::R & (1 << k)) ? a.p[k][i] : 0.0;
+      for (int k = 0; k < kEwOps; ++k) v[k] = (T::R & (1 << k)) ? a.p[k][i] : 0.0;
       ew_elem<OP>(c0, c1, v, acc);
 #pragma unroll
-      for (int k = 0; k < 6; ++k)
+      for (int k = 0; k < kEwOps; ++k)
         if (T::W & (1 << k)) a.p[k][i] = v[k];
     }
   } else {
     for (int64_t i = t0; i < a.n; i += stride) {
-      double v[6];
+      double v[kEwOps];
 #pragma unroll
-      for (int k = 0; k < 6; ++k) v[k] = (T::R & (1 << k)) ? a.p[k][i] : 0.0;
+      for (int k = 0; k < kEwOps; ++k) v[k] = (T::R & (1 << k)) ? a.p[k][i] : 0.0;
       ew_elem<OP>(c0, c1, v, acc);
 #pragma unroll
-      for (int k = 0; k < 6; ++k)
+      for (int k = 0; k < kEwOps; ++k)
         if (T::W & (1 << k)) a.p[k][i] = v[k];
     }
   }
@@ -296,7 +412,7 @@ __global__ __launch_bounds__(kBlock) void ew_kernel(EwArgs a) {
 template <int OP>
 void ew_dispatch_op(const EwArgs& a, hipStream_t s) {
   bool aligned = true;
-  for (int k = 0; k < 6; ++k)
+  for (int k = 0; k < kEwOps; ++k)
     if (((EwTraits<OP>::R | EwTraits<OP>::W) & (1 << k)) &&
         (reinterpret_cast<uintptr_t>(a.p[k]) & 15))
       aligned = false;
@@ -803,6 +919,14 @@ int ew_products(EwOp op) {
     case EW_COPY: return EwTraits<EW_COPY>::NP;
     case EW_MRR_NOX: return EwTraits<EW_MRR_NOX>::NP;
     case EW_MRR_X2: return EwTraits<EW_MRR_X2>::NP;
+    case EW_ONE: return EwTraits<EW_ONE>::NP;
+    case EW_PRE: return EwTraits<EW_PRE>::NP;
+    case EW_PCG: return EwTraits<EW_PCG>::NP;
+    case EW_CGG: return EwTraits<EW_CGG>::NP;
+    case EW_GROPP1: return EwTraits<EW_GROPP1>::NP;
+    case EW_GROPP2: return EwTraits<EW_GROPP2>::NP;
+    case EW_DIV: return EwTraits<EW_DIV>::NP;
+    case EW_PIPE: return EwTraits<EW_PIPE>::NP;
   }
   return 0;
 }
@@ -820,6 +944,14 @@ void launch_ew(EwOp op, const EwArgs& a, hipStream_t s) {
     case EW_COPY: ew_dispatch_op<EW_COPY>(a, s); break;
     case EW_MRR_NOX: ew_dispatch_op<EW_MRR_NOX>(a, s); break;
     case EW_MRR_X2: ew_dispatch_op<EW_MRR_X2>(a, s); break;
+    case EW_ONE: ew_dispatch_op<EW_ONE>(a, s); break;
+    case EW_PRE: ew_dispatch_op<EW_PRE>(a, s); break;
+    case EW_PCG: ew_dispatch_op<EW_PCG>(a, s); break;
+    case EW_CGG: ew_dispatch_op<EW_CGG>(a, s); break;
+    case EW_GROPP1: ew_dispatch_op<EW_GROPP1>(a, s); break;
+    case EW_GROPP2: ew_dispatch_op<EW_GROPP2>(a, s); break;
+    case EW_DIV: ew_dispatch_op<EW_DIV>(a, s); break;
+    case EW_PIPE: ew_dispatch_op<EW_PIPE>(a, s); break;
     default: throw Failure(KR_ERR_INVALID, "unknown elementwise op");
   }
   KR_HIP_CHECK(hipGetLastError());

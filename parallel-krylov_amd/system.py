@@ -357,6 +357,21 @@ class KrylovSystem:
              ptr_array([y.data_ptr() for y in ys]))
         return ys
 
+    def set_precond(self, d_parts=None) -> None:
+        """Jacobi diagonal (own rows per shard, float64 device tensors) of the
+        preconditioned / pipelined CG sessions begun afterwards
+        (kr_solve_set_precond); None restores the identity."""
+        if d_parts is None:
+            self._precond = None
+            call("kr_solve_set_precond", self.handle, None)
+            return
+        self._precond = list(d_parts)  # kept alive until the next call
+        for s, t in enumerate(self._precond):
+            n_own = self.row_begin[s + 1] - self.row_begin[s]
+            if t.numel() != n_own or t.dtype != _torch().float64 or not t.is_cuda:
+                raise ValueError(f"preconditioner part {s}: need {n_own} float64 device values")
+        call("kr_solve_set_precond", self.handle, ptr_array([t.data_ptr() for t in self._precond]))
+
     def solve(self, method: str, b_parts, x0_parts=None, tol=1e-5, maxiter=None, k=0,
               profile=False, max_outer=None, nan_guard=None) -> SolveOutput:
         """Run one solver to completion (or for ``max_outer`` outer steps).

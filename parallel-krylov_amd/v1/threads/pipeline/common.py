@@ -1,0 +1,96 @@
+"""Runtime of the preconditioned / pipelined CG variants (reference
+v1/threads/pipeline/*.py, with the loop bookkeeping of v1/threads/common.py).
+
+The reference signature is kept -- ``method(A, b, ilu, epsilon, T=np.float64,
+pt='cpu')`` returning ``(elapsed_time, num_of_solution_updates, residual)`` --
+and the whole loop runs in libkrylov_amd (PipeCgSession, kr_engine.cpp; HIP
+kernels EW_PCG / EW_CGG / EW_GROPP* / EW_PIPE). ``pt`` is accepted for
+compatibility; both values run on the GPUs (the package has no CPU path).
+
+``ilu`` is the preconditioner: the reference passes an object whose
+``solve(v)`` applies M^-1 (pcg.py:26). On the device the preconditioner is
+diagonal (Jacobi, M^-1 v = v / d):
+  * ``None``: the identity (d = 1);
+  * ``Jacobi(A)`` (or any object with a 1-D ``d`` attribute) or a 1-D array /
+    tensor of N values: the diagonal d.
+Anything else -- e.g. scipy's ``spilu`` SuperLU object, whose triangular
+solves run on the host -- raises TypeError instead of silently falling back.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ....system import KrylovSystem, balanced_partition, visible_devices
+from ....v3.gpu.common import _host_vector
+from ...common import _end, _start
+
+
+class Jacobi:
+    """Jacobi preconditioner: d = diag(A) (or the given diagonal); ``solve``
+    is M^-1 v = v / d, the interface of the reference's ``ilu`` argument."""
+
+    def __init__(self, A=None, d=None):
+        if d is None:
+            if A is None:
+                raise ValueError("Jacobi needs A or d")
+            d = A.diagonal() if hasattr(A, "diagonal") else np.diag(np.asarray(A))
+        self.d = np.ascontiguousarray(np.asarray(d, dtype=np.float64))
+        if not np.all(self.d != 0.0):
+            raise ValueError("Jacobi: zero on the diagonal")
+
+    def solve(self, v):
+        return v / self.d
+
+
+def _diagonal(ilu, N):
+    if ilu is None:
+        return None
+    d = getattr(ilu, "d", ilu)
+    try:
+        import torch
+        if isinstance(d, torch.Tensor):
+            d = d.detach().to("cpu", dtype=torch.float64).numpy()
+    except ImportError:  # pragma: no cover
+        pass
+    if isinstance(d, (np.ndarray, list, tuple)):
+        d = np.ascontiguousarray(np.asarray(d, dtype=np.float64))
+        if d.ndim == 1 and d.size == N:
+            return d
+        raise ValueError(f"ilu: a diagonal of {N} values is required, got shape {d.shape}")
+    raise TypeError(
+        f"ilu={type(ilu).__name__}: the device path takes a diagonal (Jacobi) preconditioner "
+        "-- None, Jacobi(A) or the diagonal as a 1-D array; triangular ILU solves "
+        "(scipy spilu) run on the host and are not offered (DESIGN.md §5b)")
+
+
+def run(method: str, banner: str, A, b, ilu, epsilon, T=np.float64, pt="cpu", maxiter=None,
+        x0=None, return_x=False):
+    """Shared body of the four solver functions: 2N iterations at most
+    (v1/threads/common.py:47) unless ``maxiter`` is given; the banner of
+    v1/common.py. Returns ``(elapsed, nosl, residual)``, plus ``(x, converged)``
+    with ``return_x=True`` (the reference returns no x)."""
+    if np.dtype(T) != np.float64:
+        raise ValueError("only T=np.float64 is supported")
+    if pt not in ("cpu", "gpu"):
+        raise ValueError(f"pt must be 'cpu' or 'gpu', got {pt!r}")
+    bh = _host_vector(b)
+    N = bh.size
+    d = _diagonal(ilu, N)
+    devices = visible_devices()
+    sysm = KrylovSystem(N, balanced_partition(N, len(devices)), devices)
+    try:
+        sysm.set_matrix(A)
+        sysm.finalize()
+        b_parts = sysm.split(bh)
+        x0_parts = sysm.split(_host_vector(x0)) if x0 is not None else None
+        sysm.set_precond(sysm.split(d) if d is not None else None)
+        _start(banner, None)
+        out = sysm.solve(method, b_parts, x0_parts, tol=epsilon,
+                         maxiter=2 * N if maxiter is None else maxiter)
+        _end(out.info["time"], out.converged, out.iterations, out.final_residual)
+        res = (out.info["time"], out.info["nosl"], out.info["residual"])
+        if return_x:
+            res = res + (sysm.gather(out.x), out.converged)
+        return res
+    finally:
+        sysm.close()

@@ -1,0 +1,211 @@
+"""Preconditioned / pipelined CG (reference
+v1/threads/pipeline/*.py, restated in oracle/pipecg.py).
+
+CPU: the oracle's PCG with M = I is the reference's v3/cpu CG statement for
+statement, so it reproduces the reference-generated CG fixtures bit for bit
+(the pin); the four variants agree with each other (same Krylov iteration);
+the Python API's argument handling and the v1 banner.
+GPU: every variant x {identity, Jacobi} x {1, 3 shards} against the oracle
+on the same system: identical iteration counts, residual entries >= 1e-8
+within the tolerance stated per variant, x within 1e-9 relative.
+"""
+import contextlib
+import io
+
+import numpy as np
+import pytest
+
+from conftest import golden_case, golden_manifest, golden_matrix
+
+METHODS = ["pcg", "chronopoulos_gear", "gropp", "pipeline"]
+# Residual-history tolerance (entries >= 1e-8) and x tolerance against the
+# oracle. The GPU's dot products sum in another order than OpenBLAS, so the
+# bar is 10x each variant's own reduction-order envelope (SURVEY.md §8c's
+# rule), measured by test_oracle_reduction_order_envelope below (oracle vs the
+# oracle with GPU-like 4096-lane strided dots, 2-D/3-D Poisson and band2000,
+# identity and Jacobi): pcg and chronopoulos_gear recompute u = M^-1 r and
+# stay at CG's envelope (<= 1.1e-14; the CG contract 1e-12); gropp's u and the
+# pipelined u, w, z, q are recurrences, which amplify rounding like a k-skip
+# method (gropp + Jacobi 2.6e-10, pipeline 3.6e-8).
+RTOL = {"pcg": 1e-12, "chronopoulos_gear": 1e-12, "gropp": 3e-9, "pipeline": 5e-7}
+XTOL = {"pcg": 1e-10, "chronopoulos_gear": 1e-10, "gropp": 1e-9, "pipeline": 1e-7}
+
+CG_FIXTURES = [c for c in golden_manifest() if c["method"] == "cg"]
+
+
+# ----------------------------------------------------------------- CPU
+@pytest.mark.parametrize("c", CG_FIXTURES, ids=lambda c: c["name"])
+def test_oracle_pcg_identity_is_reference_cg_bitwise(c):
+    """The pin: PCG with M = I is v3/cpu/cg.py statement for statement."""
+    from oracle import pipecg
+    g = golden_case(c["name"])
+    A = golden_matrix(c["matrix"])
+    x0 = None if c["x0"] is None else np.random.default_rng(c["x0"]).standard_normal(A.shape[0])
+    maxiter = None if c["maxiter"] is None else c["maxiter"] + 1  # v1: range(1, max_iter)
+    _, nosl, res, x, _ = pipecg.pcg(A, g["b"], None, c["tol"], maxiter=maxiter, x0=x0,
+                                    return_x=True)
+    assert np.array_equal(res, g["residual"])
+    assert np.array_equal(nosl, g["nosl"])
+    assert np.array_equal(x, g["x"])
+
+
+@pytest.mark.parametrize("method", METHODS)
+@pytest.mark.parametrize("spec", [("poisson", 16, 2), ("banded", 2000, 13, 64, 0)])
+def test_oracle_variants_agree(method, spec):
+    """Same Krylov iteration in exact arithmetic: every variant, preconditioned
+    or not, tracks PCG's history and reaches the same x."""
+    from oracle import pipecg
+    A = golden_matrix(spec)
+    b = np.random.default_rng(1).standard_normal(A.shape[0])
+    for pre in (None, pipecg.Jacobi(A)):
+        _, n0, r0, x0, c0 = pipecg.pcg(A, b, pre, 1e-10, return_x=True)
+        _, n1, r1, x1, c1 = pipecg.METHODS[method](A, b, pre, 1e-10, return_x=True)
+        assert c0 and c1 and len(r1) == len(r0)
+        keep = r0 >= 1e-8
+        assert np.max(np.abs(r1[keep] - r0[keep]) / r0[keep]) < 1e-6
+        assert np.linalg.norm(x1 - x0) / np.linalg.norm(x0) < 1e-8
+        assert np.array_equal(n1, np.arange(len(r1)))
+
+
+def _gpu_like_dot(a, b):
+    """Dot product in a GPU-like order: 4096 lane-strided partials, then a sum."""
+    p = a * b
+    pad = np.zeros(-(-p.size // 4096) * 4096)
+    pad[:p.size] = p
+    return float(np.sum(pad.reshape(-1, 4096).sum(axis=0)))
+
+
+@pytest.mark.parametrize("method", METHODS)
+def test_oracle_reduction_order_envelope(monkeypatch, method):
+    """The basis of RTOL / XTOL: the oracle against itself with another
+    reduction order stays 10x inside them (same iteration counts)."""
+    from oracle import pipecg
+    worst = wx = 0.0
+    for spec in (("poisson", 16, 2), ("poisson", 16, 3), ("banded", 2000, 13, 64, 0)):
+        A = golden_matrix(spec)
+        b = np.random.default_rng(1).standard_normal(A.shape[0])
+        for pre in (None, pipecg.Jacobi(A)):
+            monkeypatch.setattr(pipecg, "_dot", np.dot)
+            _, n0, r0, x0, _ = pipecg.METHODS[method](A, b, pre, 1e-10, return_x=True)
+            monkeypatch.setattr(pipecg, "_dot", _gpu_like_dot)
+            _, n1, r1, x1, _ = pipecg.METHODS[method](A, b, pre, 1e-10, return_x=True)
+            assert np.array_equal(n0, n1)
+            keep = r0 >= 1e-8
+            worst = max(worst, float(np.max(np.abs(r1[keep] - r0[keep]) / r0[keep])))
+            wx = max(wx, float(np.linalg.norm(x1 - x0) / np.linalg.norm(x0)))
+    assert worst * 10 <= RTOL[method], worst
+    assert wx * 10 <= XTOL[method], wx
+
+
+def test_jacobi_reduces_iterations_on_varying_diagonal():
+    """Jacobi pays on a badly scaled SPD system (row scaling 1..1e4)."""
+    import scipy.sparse as sp
+    from oracle import pipecg
+    A0 = golden_matrix(("banded", 2000, 13, 64, 0))
+    s = sp.diags(np.sqrt(np.logspace(0, 4, A0.shape[0])))
+    A = (s @ A0 @ s).tocsr()
+    b = np.random.default_rng(1).standard_normal(A.shape[0])
+    _, _, r_id = pipecg.pcg(A, b, None, 1e-10)
+    _, _, r_j = pipecg.pcg(A, b, pipecg.Jacobi(A), 1e-10)
+    assert len(r_j) < len(r_id) // 2
+
+
+def test_ilu_argument_forms():
+    import scipy.sparse.linalg as spla
+    from parallel_krylov_amd.v1.threads.pipeline.common import Jacobi, _diagonal
+    A = golden_matrix(("banded", 200, 3, 8, 0)).tocsc()
+    d = A.diagonal()
+    assert _diagonal(None, 200) is None
+    assert np.array_equal(_diagonal(Jacobi(A), 200), d)
+    assert np.array_equal(_diagonal(d, 200), d)
+    assert np.array_equal(_diagonal(list(d), 200), d)
+    with pytest.raises(ValueError):
+        _diagonal(d[:10], 200)
+    with pytest.raises(TypeError, match="spilu"):
+        _diagonal(spla.spilu(A), 200)
+    with pytest.raises(ValueError):
+        Jacobi(d=np.zeros(3))
+
+
+def test_v1_banner_text():
+    from parallel_krylov_amd.v1.common import _end, _start
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        _start("pipeline", None)
+        _end(1.5, False, 7, 0.25)
+    assert buf.getvalue() == (
+        "\033[32m# ================ INFO ================ #\033[0m\n"
+        "Method:\t\tpipeline\ninitial_k:\tNone\ntime:\t\t1.5 s\nstatus:\t\tdiverged\n"
+        "iteration:\t7 times\nfinal residual:\t0.25\n"
+        "\033[32m# ====================================== #\033[0m\n")
+
+
+def test_methods_registered():
+    from parallel_krylov_amd import _lib
+    for i, m in enumerate(METHODS):
+        assert _lib.KR_METHOD[m] == 5 + i
+
+
+# ----------------------------------------------------------------- GPU
+def _systems():
+    return [("p2d16", ("poisson", 16, 2)), ("p3d16", ("poisson", 16, 3)),
+            ("band2000", ("banded", 2000, 13, 64, 0))]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shards", [1, 3])
+@pytest.mark.parametrize("jacobi", [False, True])
+@pytest.mark.parametrize("sysname,spec", _systems(), ids=[s[0] for s in _systems()])
+@pytest.mark.parametrize("method", METHODS)
+def test_gpu_matches_oracle(monkeypatch, method, sysname, spec, jacobi, shards):
+    import importlib
+    from oracle import pipecg
+    monkeypatch.setenv("KRYLOV_AMD_SHARDS", ",".join(["0"] * shards))
+    mod = importlib.import_module(f"parallel_krylov_amd.v1.threads.pipeline.{method}")
+    A = golden_matrix(spec)
+    b = np.random.default_rng(1).standard_normal(A.shape[0])
+    pre_o = pipecg.Jacobi(A) if jacobi else None
+    _, n_o, r_o, x_o, c_o = pipecg.METHODS[method](A, b, pre_o, 1e-10, return_x=True)
+    out = io.StringIO()
+    with contextlib.redirect_stdout(out):
+        el, nosl, res, x, conv = getattr(mod, method)(A, b, A.diagonal() if jacobi else None,
+                                                      1e-10, return_x=True)
+    assert conv == c_o and "status:\t\tconverged" in out.getvalue()
+    assert np.array_equal(nosl, n_o), (len(nosl), len(n_o))
+    keep = r_o >= 1e-8
+    rel = np.abs(res - r_o) / r_o
+    assert rel[keep].max() < RTOL[method], rel[keep].max()
+    assert rel.max() < 1e-5, rel.max()
+    xh = x.cpu().numpy()
+    assert np.linalg.norm(xh - x_o) / np.linalg.norm(x_o) < XTOL[method]
+
+
+@pytest.mark.gpu
+def test_gpu_pcg_identity_matches_reference_cg_fixture():
+    """The GPU PCG with M = I against the reference-generated CG fixture
+    (the CG parity contract: entries within 1e-12, same nosl)."""
+    from parallel_krylov_amd.v1.threads.pipeline import pcg
+    c = next(c for c in CG_FIXTURES if c["name"] == "band2000_cg")
+    g = golden_case(c["name"])
+    A = golden_matrix(c["matrix"])
+    with contextlib.redirect_stdout(io.StringIO()):
+        _, nosl, res = pcg(A, g["b"], None, c["tol"])
+    assert np.array_equal(nosl, g["nosl"])
+    assert np.max(np.abs(res - g["residual"]) / g["residual"]) < 1e-12
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method", METHODS)
+def test_gpu_maxiter_truncation(method):
+    """maxiter=m: iterations 1..m-1 (v1's range(1, max_iter)); not converged."""
+    from oracle import pipecg
+    import importlib
+    mod = importlib.import_module(f"parallel_krylov_amd.v1.threads.pipeline.{method}")
+    A = golden_matrix(("poisson", 16, 2))
+    b = np.random.default_rng(1).standard_normal(A.shape[0])
+    _, n_o, r_o = pipecg.METHODS[method](A, b, None, 1e-10, maxiter=8)
+    with contextlib.redirect_stdout(io.StringIO()):
+        _, nosl, res, _, conv = getattr(mod, method)(A, b, None, 1e-10, maxiter=8,
+                                                     return_x=True)
+    assert not conv and len(res) == 8 and np.array_equal(nosl, n_o)
+    assert np.max(np.abs(res - r_o) / r_o) < RTOL[method]
