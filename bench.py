@@ -346,8 +346,9 @@ def main():
             parity = history_parity(run["history"], ref_info)
     if rank == 0:
         rec = {
-            "metric": (HEADLINE_METRIC if args.config == "C4"
-                       else f"solver iterations/sec, {cfg['label']}"),
+            "metric": (HEADLINE_METRIC if args.config == "C4" and method == cfg["method"]
+                       else f"solver iterations/sec, {cfg['label']}"
+                       + ("" if method == cfg["method"] else f" ({method})")),
             "value": round(value, 3),
             "unit": "iterations/s",
             "n_gpus": world,
