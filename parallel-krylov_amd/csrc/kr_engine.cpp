@@ -623,8 +623,19 @@ void System::finalize() {
       const char* sub = getenv("KR_SLAB_SUB");
       s.slab_sub = sub ? atoll(sub) : 0;
     }
-    if (!s.comm_stream)
-      KR_HIP_CHECK(hipStreamCreateWithFlags(&s.comm_stream, hipStreamNonBlocking));
+    if (!s.comm_stream) {
+      // The halo exchange is on the critical path of every split SpMV (the
+      // boundary rows wait for it) while the interior launch fills the GPU:
+      // its queue gets the highest priority, so the command processor
+      // dispatches the RCCL / copy work ahead of the interior workgroups
+      // still waiting for a slot. KR_COMM_PRIORITY=0: default priority (A/B).
+      int lo = 0, hi = 0;
+      KR_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      const char* env = getenv("KR_COMM_PRIORITY");
+      const bool prio = !(env && atoi(env) == 0);
+      KR_HIP_CHECK(hipStreamCreateWithPriority(&s.comm_stream, hipStreamNonBlocking,
+                                               prio ? hi : 0));
+    }
     if (!s.ev_in) KR_HIP_CHECK(hipEventCreateWithFlags(&s.ev_in, hipEventDisableTiming));
     if (!s.ev_out) KR_HIP_CHECK(hipEventCreateWithFlags(&s.ev_out, hipEventDisableTiming));
     if (!s.dense) {
