@@ -1625,11 +1625,55 @@ class CgSession : public Base {
   double thr = 0;
   std::vector<double> q;  // gamma of the iterations of the current batch
   size_t qpos = 0;
+  // Persistent batches (small single-shard systems, launch_cg_persist): one
+  // cooperative launch per batch instead of 2 launches per iteration; grid
+  // size, barrier counter + timeout flag. Opt-in (KR_PERSIST=1): measured
+  // slower than the two launches per iteration on C1 (37k vs 58-62k it/s,
+  // DESIGN.md §3); KR_PERSIST_MAXN (default 2^19 rows) bounds the size.
+  int persist = 0;
+  unsigned* pbar = nullptr;
+
+  void persist_batch(int64_t m) {
+    Shard& s = sys->shards[0];
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    const int other = pc == P ? P2 : P;
+    CgPersistArgs a;
+    a.rowptr = s.rowptr;
+    a.rowptr64 = s.rowptr64;
+    a.col = s.col;
+    a.val = s.val;
+    a.n = s.n;
+    a.pad = s.pad;
+    a.x = s.vec[X];
+    a.r = s.vec[R];
+    a.pa = s.vec[pc];
+    a.pb = s.vec[other];
+    a.v = s.vec[V];
+    a.part = s.partials;
+    a.bar = pbar;
+    a.err = reinterpret_cast<int*>(pbar + 1);
+    a.st = s.st;
+    a.gamma = gamma;
+    a.it0 = i;
+    a.m = (int)m;
+    a.thr = thr;
+    KR_HIP_CHECK(hipMemsetAsync(pbar, 0, 2 * sizeof(unsigned), s.stream));
+    hipEvent_t t0 = nullptr;
+    sys->prof_begin(s, "cg_persist", t0);
+    launch_cg_persist(a, persist, s.stream);
+    // per iteration: the CSR SpMV (p and r gathered, p and v stored) + EW_CG
+    const double it_bytes = 12.0 * s.nnz + 4.0 * (s.n + 1) + 32.0 * s.n + 48.0 * s.n;
+    sys->prof_end(s, "cg_persist", t0, it_bytes * (double)m);
+    if ((m - 1) % 2 != 0) pc = other;  // where the final p = r + beta p landed
+  }
 
   // Iterations i .. i+m-1 on the device; q[j] = gamma at the top of i+j+1.
   void run_batch() {
     const int64_t m = std::min<int64_t>({(int64_t)scalar_batch(), std::max<int64_t>(hint, 1),
                                          prm.maxiter - i});
+    if (persist) {
+      persist_batch(m);
+    } else {
     sys->dev_stop = true;
     const bool fused = sys->fused_scalars();
     // fused scalars + virtual p: iteration j > 0 of the batch folds the
@@ -1662,7 +1706,13 @@ class CgSession : public Base {
       sys->ew_dev(EW_CG_P, ST_C2, {pc, R, -1, -1, -1, -1}, 0);  // p = r + b p
     }
     sys->dev_stop = false;
+    }
     sys->scalar_state_read();
+    if (persist) {
+      int err = 0;
+      KR_HIP_CHECK(hipMemcpy(&err, pbar + 1, sizeof(int), hipMemcpyDeviceToHost));
+      if (err) throw Failure(KR_ERR_HIP, "persistent CG: a grid barrier timed out");
+    }
     const double* h = sys->shards[0].hst;
     q.assign(h + ST_HIST, h + ST_HIST + m);
     qpos = 0;
@@ -1691,11 +1741,25 @@ class CgSession : public Base {
     if (dev) {
       thr = conv_threshold(bnorm, prm.tol);
       sys->scalar_state_init(gamma);
+      const char* env = getenv("KR_PERSIST");
+      const char* envn = getenv("KR_PERSIST_MAXN");
+      const int64_t maxn = envn ? atoll(envn) : (int64_t)1 << 19;
+      if (env && atoi(env) == 1 && sys->shards.size() == 1 && !sys->comm) {
+        Shard& s = sys->shards[0];
+        if (!s.dense && s.col && s.n > 0 && s.n <= maxn) {
+          KR_HIP_CHECK(hipSetDevice(s.dev));
+          persist = cg_persist_grid(s.n);
+          if (persist && !pbar) KR_HIP_CHECK(hipMalloc(&pbar, 2 * sizeof(unsigned)));
+        }
+      }
     }
     i = 0;
     index = 0;
     set_nosl(0, 0);
     start_timer();
+  }
+  ~CgSession() override {
+    if (pbar) (void)hipFree(pbar);
   }
   bool step_once() override {
     if (i >= prm.maxiter) {  // while-else branch

@@ -395,6 +395,34 @@ void banded_offsets(int h, int64_t width, uint64_t seed, int64_t* out_sorted);
 // Scratch for the primitive entry points (grown on demand, per device).
 double* primitive_scratch(size_t doubles);
 
+// ---------------------------------------------------------------------------
+// Persistent CG (small single-shard systems): m iterations of
+// v3/gpu/cg.py:31-39 in ONE cooperative launch, grid-wide barriers instead of
+// kernel boundaries. Vectors are full bases (Shard::vec), own row i at
+// pad + i; the CSR block is in local column numbering. Writes the same scalar
+// state as the device-scalar batches (st[ST_HIST + j] = <r,r> after
+// iteration j, ST_STOP / ST_STOP_AT); the final p = r + beta p lands in
+// p_a if (iterations run - 1) is even, else p_b.
+struct CgPersistArgs {
+  const void* rowptr = nullptr;
+  int rowptr64 = 0;
+  const int32_t* col = nullptr;
+  const double* val = nullptr;
+  int64_t n = 0, pad = 0;
+  double *x = nullptr, *r = nullptr, *pa = nullptr, *pb = nullptr, *v = nullptr;
+  double* part = nullptr;    // [2][grid] partials
+  unsigned* bar = nullptr;   // barrier counter, zero at launch
+  int* err = nullptr;        // set to 1 when a barrier wait timed out
+  double* st = nullptr;
+  double gamma = 0;          // <r,r> at the top of iteration it0
+  int64_t it0 = 0;
+  int m = 0;
+  double thr = 0;            // convergence threshold on <r,r> (0 <= g < thr)
+};
+// Workgroups of the cooperative launch (all co-resident); 0 if unsupported.
+int cg_persist_grid(int64_t n);
+void launch_cg_persist(const CgPersistArgs& a, int grid, hipStream_t s);
+
 int default_grid(int64_t n);
 // Workgroups of the SpMV kernels for a block of n rows with column reach `reach` rows.
 int spmv_grid_for(int64_t n, int64_t reach);

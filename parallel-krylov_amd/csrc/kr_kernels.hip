@@ -957,6 +957,150 @@ void launch_ew(EwOp op, const EwArgs& a, hipStream_t s) {
   KR_HIP_CHECK(hipGetLastError());
 }
 
+// ---------------------------------------------------------------------------
+// Persistent CG (CgPersistArgs). One workgroup per CU at most, each owning a
+// contiguous range of rows (one lane per row, strided); every iteration is
+// two phases separated by grid barriers:
+//   A: v = A p (p formed at every gathered column as r + beta p_old from the
+//      previous iteration, rounded as EW_CG_P, own rows stored to the other
+//      p buffer), partial <p,v>;            barrier
+//      sigma = the partials summed in a fixed order by every workgroup alike;
+//   B: x += alpha p; r -= alpha v (rounded as EW_CG), partial <r,r>; barrier
+//      gnew summed alike -> beta, the convergence test (every workgroup takes
+//      the same branch), state written by workgroup 0.
+// Rows are summed in stored order from 0.0 (bitwise scipy's y, as every SpMV
+// here). The barrier is a device-scope counter: release fence + atomic add,
+// then acquire polling until every workgroup of this phase arrived; a wait
+// that exceeds ~1 s sets *err and gives up, so the grid always drains.
+namespace {
+
+__device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned target, int* err) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    // release once (write back this XCD's dirty L2 lines), arrive, poll with
+    // relaxed device-scope loads (they bypass the non-coherent L2 without
+    // invalidating it on every poll), then acquire once
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned spins = 0;
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 25)) {
+        *err = 1;
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
+template <typename RP>
+__global__ __launch_bounds__(kBlock) void cg_persist_kernel(CgPersistArgs a) {
+  __shared__ double s_red[4];
+  const int G = gridDim.x;
+  const int64_t per = (a.n + G - 1) / G;
+  const int64_t lo = min(a.n, (int64_t)blockIdx.x * per);
+  const int64_t hi = min(a.n, lo + per);
+  const RP* __restrict__ rowptr = static_cast<const RP*>(a.rowptr);
+  const int32_t* __restrict__ col = a.col;
+  const double* __restrict__ val = a.val;
+  double* x = a.x;
+  double* r = a.r;
+  double* v = a.v;
+  double* pc = a.pa;  // p of this iteration (complete at j = 0)
+  double* pn = a.pb;  // p of the next one (j > 0: formed in phase A)
+  double gamma = a.gamma, beta = 0.0;
+  unsigned target = 0;
+  for (int j = 0; j < a.m; ++j) {
+    // phase A: v = A p ; <p,v>
+    double acc[1] = {0.0};
+    for (int64_t i = lo + threadIdx.x; i < hi; i += kBlock) {
+      const int64_t e = (int64_t)rowptr[i + 1];
+      double sum = 0.0;
+      for (int64_t k = (int64_t)rowptr[i]; k < e; ++k) {
+        const int64_t c = col[k];
+        const double pv = j == 0 ? pc[c] : virtual_p(beta, pc[c], r[c]);
+        const double t = val[k] * pv;
+        sum = sum + t;
+      }
+      const int64_t o = a.pad + i;
+      const double po = j == 0 ? pc[o] : virtual_p(beta, pc[o], r[o]);
+      if (j > 0) pn[o] = po;
+      v[o] = sum;
+      acc[0] += po * sum;
+    }
+    block_reduce_store<1>(acc, a.part, G, s_red);
+    target += G;
+    grid_barrier(a.bar, target, a.err);
+    const double sigma = 0.0 + slot_sum(a.part, G, s_red);
+    const double alpha = gamma / sigma;
+    if (j > 0) {
+      double* t = pc;
+      pc = pn;
+      pn = t;
+    }
+    // phase B: x += alpha p ; r -= alpha v ; <r,r>
+    acc[0] = 0.0;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += kBlock) {
+      const int64_t o = a.pad + i;
+      const double ap = alpha * pc[o];
+      const double av = alpha * v[o];
+      x[o] = x[o] + ap;
+      const double rn = r[o] - av;
+      r[o] = rn;
+      acc[0] += rn * rn;
+    }
+    block_reduce_store<1>(acc, a.part + G, G, s_red);
+    target += G;
+    grid_barrier(a.bar, target, a.err);
+    const double gnew = 0.0 + slot_sum(a.part + G, G, s_red);
+    beta = gnew / gamma;
+    gamma = gnew;
+    const bool conv = gnew >= 0.0 && gnew < a.thr;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      a.st[ST_HIST + j] = gnew;
+      if (conv) {  // the test at the top of the next iteration
+        a.st[ST_STOP_AT] = (double)(a.it0 + j + 1);
+        a.st[ST_STOP] = 1.0;
+      }
+    }
+    if (conv) return;
+  }
+  // the last iteration's p = r + beta p, own rows, in place
+  for (int64_t i = lo + threadIdx.x; i < hi; i += kBlock) {
+    const int64_t o = a.pad + i;
+    pc[o] = virtual_p(beta, pc[o], r[o]);
+  }
+}
+
+}  // namespace
+
+int cg_persist_grid(int64_t n) {
+  int dev = 0, cus = 0, coop = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev) != hipSuccess)
+    return 0;
+  if (!coop || cus <= 0) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &per_cu, reinterpret_cast<const void*>(cg_persist_kernel<int32_t>), kBlock, 0) !=
+          hipSuccess ||
+      per_cu < 1)
+    return 0;
+  const int64_t need = std::max<int64_t>(1, (n + kBlock - 1) / kBlock);
+  return (int)std::min<int64_t>(need, cus);
+}
+
+void launch_cg_persist(const CgPersistArgs& a, int grid, hipStream_t s) {
+  KR_REQUIRE(grid > 0 && a.m > 0 && a.m <= kScalarBatch, "persistent CG: bad launch shape");
+  CgPersistArgs arg = a;
+  void* params[] = {&arg};
+  const void* fn = a.rowptr64 ? reinterpret_cast<const void*>(cg_persist_kernel<int64_t>)
+                              : reinterpret_cast<const void*>(cg_persist_kernel<int32_t>);
+  KR_HIP_CHECK(hipLaunchCooperativeKernel(fn, dim3(grid), dim3(kBlock), params, 0, s));
+}
+
 void launch_finalize(const double* partials, int grid, int nslots, double* out,
                      hipStream_t s) {
   if (nslots <= 0) return;

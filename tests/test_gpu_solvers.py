@@ -258,7 +258,9 @@ def test_device_scalars_bitwise_equal_host(monkeypatch, shards, method, matrix, 
     A = golden_matrix(matrix)
     b = np.random.default_rng(11).standard_normal(A.shape[0])
     kw = dict(tol=tol, maxiter=maxiter)
-    base = {"KRYLOV_AMD_SHARDS": shards}
+    # (KR_PERSIST=0: the persistent one-launch batches sum their dots in
+    # another order; test_persistent_cg_* below check them)
+    base = {"KRYLOV_AMD_SHARDS": shards, "KR_PERSIST": "0"}
     x0, i0 = _run_env(monkeypatch, {**base, "KR_DEVICE_SCALARS": "0"}, method, A, b, **kw)
     for batch, fuse, vp in (("1", "1", "1"), ("3", "1", "1"), ("32", "1", "1"),
                             ("32", "1", "0"), ("32", "0", "1")):
@@ -270,6 +272,60 @@ def test_device_scalars_bitwise_equal_host(monkeypatch, shards, method, matrix, 
         np.testing.assert_array_equal(i1["nosl"], i0["nosl"])
         np.testing.assert_array_equal(i1["residual"], i0["residual"])
         np.testing.assert_array_equal(x1, x0)
+
+
+PERSIST_CASES = [c for c in CASES if c["method"] == "cg"]
+
+
+@pytest.mark.parametrize("batch", ["1", "3", "32"])
+@pytest.mark.parametrize("c", PERSIST_CASES, ids=[c["name"] for c in PERSIST_CASES])
+def test_persistent_cg_matches_reference(monkeypatch, c, batch):
+    """CG batches as ONE cooperative launch (grid barriers instead of kernel
+    boundaries, launch_cg_persist): the reference fixtures' contract (same
+    nosl, residuals within 1e-12 / the envelope, x), for batches of 1, 3 and
+    32 iterations (convergence inside a batch, maxiter truncation, x0)."""
+    g = golden_case(c["name"])
+    A = golden_matrix(c["matrix"])
+    x0 = None if c["x0"] is None else np.random.default_rng(c["x0"]).standard_normal(A.shape[0])
+    x, info = _run_env(monkeypatch, {"KR_PERSIST": "1", "KR_SCALAR_BATCH": batch}, "cg", A,
+                       g["b"], x=x0, tol=c["tol"], maxiter=c["maxiter"])
+    check_parity(c, g, x, info)
+
+
+@pytest.mark.parametrize("matrix,tol,maxiter", [(["poisson", 64, 3], 1e-9, 400),
+                                                (["poisson", 256, 2], 1e-10, 2000),
+                                                (["banded", 3000, 13, 64, 0], 1e-10, 400),
+                                                (["poisson", 8, 2], 0.0, 40)])
+def test_persistent_cg_matches_launch_path(monkeypatch, matrix, tol, maxiter):
+    """The persistent batches against the two-launches-per-iteration path on
+    the same system: same iteration count, residuals within the CG contract
+    (only the dot summation order differs), and the persistent kernel is the
+    one that ran (kernel statistics)."""
+    from parallel_krylov_amd.system import KrylovSystem, balanced_partition, visible_devices
+    A = golden_matrix(matrix)
+    b = np.random.default_rng(13).standard_normal(A.shape[0])
+    outs = []
+    for env in ("1", "0"):
+        monkeypatch.setenv("KR_PERSIST", env)
+        n = A.shape[0]
+        sysm = KrylovSystem(n, balanced_partition(n, 1), visible_devices()[:1])
+        try:
+            sysm.set_matrix(A)
+            sysm.finalize()
+            out = sysm.solve("cg", sysm.split(b), tol=tol, maxiter=maxiter, profile=1)
+            names = {s_["name"] for s_ in out.kernel_stats if s_["launches"]}
+            outs.append((out.x[0].cpu().numpy(), out.info, names))
+        finally:
+            sysm.close()
+    (x1, i1, n1), (x0, i0, n0) = outs
+    assert "cg_persist" in n1 and "cg_persist" not in n0, (n1, n0)
+    np.testing.assert_array_equal(i1["nosl"], i0["nosl"])
+    # entries >= 1e-8 (tol = 0 runs on into rounding noise, as the reference)
+    keep = i0["residual"] >= 1e-8
+    rel = np.abs(i1["residual"] - i0["residual"])[keep] / i0["residual"][keep]
+    assert rel.max() < 1e-12, rel.max()
+    if tol > 0:
+        assert np.linalg.norm(x1 - x0) / np.linalg.norm(x0) < 1e-11
 
 
 @pytest.mark.parametrize("method,tol,maxiter", [("cg", 1e-10, 400), ("mrr", 1e-10, 400),
