@@ -52,6 +52,9 @@ int ew_vectors(EwOp op) {
     case EW_COPY: return 2;
     case EW_MRR_NOX: return 7;
     case EW_MRR_X2: return 9;
+    case EW_CG_NOX: return 3;
+    case EW_CG_X2: return 7;
+    case EW_AXPY: return 3;
     case EW_ONE: return 1;
     case EW_PRE: return 3;
     case EW_PCG: return 9;
@@ -102,6 +105,9 @@ const char* ew_name(EwOp op) {
     case EW_COPY: return "copy";
     case EW_MRR_NOX: return "update_mrr_nox";
     case EW_MRR_X2: return "update_mrr_x2";
+    case EW_CG_NOX: return "update_cg_nox";
+    case EW_CG_X2: return "update_cg_x2";
+    case EW_AXPY: return "update_x";
     case EW_ONE: return "fill_one";
     case EW_PRE: return "precond";
     case EW_PCG: return "update_pcg";
@@ -1437,7 +1443,7 @@ void System::spmv_vp(int p_old, int r, int out, int p_new, int64_t it, int h, in
 }
 
 void System::ew_pro(EwOp op, ScalarOp sop, std::array<int, 6> ids, int slot0, int64_t it, int h,
-                    int par, double thr, int s1) {
+                    int par, double thr, int s1, int alpha) {
   KR_REQUIRE(slot0 + ew_products(op) <= kMaxSlots, "reduction slots exhausted");
   Shard& s = shards[0];
   KR_HIP_CHECK(hipSetDevice(s.dev));
@@ -1458,6 +1464,7 @@ void System::ew_pro(EwOp op, ScalarOp sop, std::array<int, 6> ids, int slot0, in
   a.pro_par = par;
   a.pro_thr = thr;
   a.pro_s1 = s1;
+  a.pro_alpha = alpha;
   for (int p = 0; p < ew_products(op); ++p) s.slot_n[slot0 + p] = s.grid;
   hipEvent_t t0 = nullptr;
   const char* nm = ew_name(op);
@@ -1681,6 +1688,15 @@ class CgSession : public Base {
     // iteration is 2 launches (the batch's last one keeps EW_CG_P, whose
     // beta step the host reads back)
     const bool vpf = fused && sys->vp_ok();
+    // x += alpha p deferred in pairs of iterations (x is not read inside the
+    // loop): step j (even, j+1 < m) only updates r (EW_CG_NOX, alpha kept in
+    // ST_ALPHA), step j+1 does x = (x + alpha_j p_j) + alpha_j+1 p_j+1
+    // (EW_CG_X2): the same two roundings per element as two EW_CG steps,
+    // one x read and write fewer. p_j is still in the other p buffer then
+    // (EPI_XY_VP wrote p_j+1 beside it). KR_CG_XDEFER=0 disables (A/B).
+    const char* xenv = getenv("KR_CG_XDEFER");
+    const bool defer = vpf && !(xenv && atoi(xenv) == 0);
+    std::vector<int> pbuf(m, -1);  // p_j's buffer at the NOX steps
     for (int64_t j = 0; j < m; ++j) {
       if (j > 0) sys->prof_active = (sys->prof_tick++ % sys->profile_every) == 0;
       if (fused) {  // the scalar steps inside the vector kernels: 3 launches
@@ -1694,7 +1710,17 @@ class CgSession : public Base {
         } else {
           sys->spmv(EPI_XY, pc, -1, V, -1, -1, -1, 0);  // v = A p ; sigma
         }
-        sys->ew_pro(EW_CG, SC_CG_ALPHA, {X, pc, R, V, -1, -1}, 0, i + j, (int)j, par, thr, s1);
+        if (defer && j % 2 == 0 && j + 1 < m) {
+          pbuf[j] = pc;
+          sys->ew_pro(EW_CG_NOX, SC_CG_ALPHA, {X, pc, R, V, -1, -1}, 0, i + j, (int)j, par, thr,
+                      s1, 1);
+        } else if (defer && j % 2 == 1) {
+          const int pp = pc == P ? P2 : P;  // p_j-1
+          sys->ew_pro(EW_CG_X2, SC_CG_ALPHA, {X, pc, R, V, pp, -1}, 0, i + j, (int)j, par, thr,
+                      s1, 2);
+        } else {
+          sys->ew_pro(EW_CG, SC_CG_ALPHA, {X, pc, R, V, -1, -1}, 0, i + j, (int)j, par, thr, s1);
+        }
         if (!vpf || j == m - 1)
           sys->ew_pro(EW_CG_P, SC_CG_BETA, {pc, R, -1, -1, -1, -1}, 0, i + j, (int)j, par, thr);
         continue;
@@ -1706,9 +1732,18 @@ class CgSession : public Base {
       sys->ew_dev(EW_CG_P, ST_C2, {pc, R, -1, -1, -1, -1}, 0);  // p = r + b p
     }
     sys->dev_stop = false;
-    }
     sys->scalar_state_read();
+    // stopped right after a NOX step: apply its deferred x += alpha p (the
+    // stream runs it before anything reads x)
+    const double* hs = sys->shards[0].hst;
+    if (hs[ST_STOP] != 0.0) {
+      const int64_t jl = (int64_t)hs[ST_STOP_AT] - 1 - i;  // the last step that ran
+      if (jl >= 0 && jl < m && pbuf[jl] >= 0)
+        sys->ew_dev(EW_AXPY, ST_ALPHA, {X, pbuf[jl], -1, -1, -1, -1}, 0);
+    }
+    }
     if (persist) {
+      sys->scalar_state_read();
       int err = 0;
       KR_HIP_CHECK(hipMemcpy(&err, pbar + 1, sizeof(int), hipMemcpyDeviceToHost));
       if (err) throw Failure(KR_ERR_HIP, "persistent CG: a grid barrier timed out");

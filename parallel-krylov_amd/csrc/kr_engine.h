@@ -223,7 +223,7 @@ struct System {
   // KR_FUSE_SCALAR=0 keeps the separate scalar kernel (A/B).
   bool fused_scalars() const;
   void ew_pro(EwOp op, ScalarOp sop, std::array<int, 6> ids, int slot0, int64_t it, int h,
-              int par, double thr, int s1 = 1);
+              int par, double thr, int s1 = 1, int alpha = 0);
   // CG's p update folded into the next SpMV (EPI_XY_VP): the SpMV runs the
   // SC_CG_BETA step of iteration `it` (ST_HIST slot h, gamma parity par)
   // over the EW_CG partials in slot 0, gathers p = r + beta p_old, stores

@@ -228,6 +228,11 @@ enum EwOp : int {
   EW_GROPP1,      // x += a p; r -= a s; u -= a (s / d); <r,r> <r,u>  (x p r s u d)
   EW_GROPP2,      // p = u + b p; s = w + b s; <p,s>         (p u s w)
   EW_DIV,         // m = w / d                               (m w d)
+  // Fused CG with the x update deferred to every second iteration (x is
+  // never read inside the loop): (x p r v pp)
+  EW_CG_NOX,      // r -= alpha*v; <r,r>                   (alpha saved to ST_ALPHA)
+  EW_CG_X2,       // x = (x + alpha_prev*pp) + alpha*p; r -= alpha*v; <r,r>
+  EW_AXPY,        // x += c0*p                              (the flush after a NOX step)
   EW_PIPE,        // z = n + b z; q = m + b q; s = w + b s; p = u + b p; x += a p;
                   // r -= a s; u -= a q; w -= a z; <r,r> <r,u> <w,u>
                   //                                         (z n q m s w p u x r)
@@ -261,6 +266,7 @@ struct EwArgs {
   int pro_check = 1;
   double pro_thr = 0;
   int pro_s1 = 1;                  // SC_CG_ALPHA: sigma's slot (EPI_XY: 1, EPI_XY_VP: 4)
+  int pro_alpha = 0;               // SC_CG_ALPHA: 1 save alpha to ST_ALPHA, 2 c1 = ST_ALPHA
 };
 void launch_ew(EwOp op, const EwArgs& a, hipStream_t s);
 
@@ -274,7 +280,8 @@ enum ScalarState : int {
   ST_STOP = 5,     // 1.0 once the convergence test fired
   ST_STOP_AT = 6,  // iteration at whose top it fired
   ST_GAMMA_ALT = 7,  // fused CG steps: gamma of odd iterations (even: ST_GAMMA)
-  ST_HIST = 8,     // ring of reduced norms, one per iteration of a batch
+  ST_ALPHA = 8,    // fused CG, deferred x: alpha of the last EW_CG_NOX step
+  ST_HIST = 9,     // ring of reduced norms, one per iteration of a batch
 };
 // Fused CG steps read this iteration's gamma while workgroup 0 writes the
 // next one: two slots, alternating with the iteration's parity.

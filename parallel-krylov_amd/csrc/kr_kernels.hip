@@ -84,6 +84,18 @@ template <>
 struct EwTraits<EW_MRR_X2> {  // p: y ar1 z r xs xd
   static constexpr int NP = 0, R = 0b011111, W = 0b101101;
 };
+template <>
+struct EwTraits<EW_CG_NOX> {  // p: x p r v
+  static constexpr int NP = 1, R = 0b01100, W = 0b00100;
+};
+template <>
+struct EwTraits<EW_CG_X2> {  // p: x p r v pp
+  static constexpr int NP = 1, R = 0b11111, W = 0b00101;
+};
+template <>
+struct EwTraits<EW_AXPY> {  // p: x p
+  static constexpr int NP = 0, R = 0b11, W = 0b01;
+};
 // Preconditioned / pipelined CG family (v1/threads/pipeline/*.py restated,
 // DESIGN.md §5b): Jacobi M^-1 v = v / d.
 template <>
@@ -150,6 +162,21 @@ __device__ __forceinline__ void ew_elem(double c0, double c1, double (&v)[kEwOps
     v[0] = v[0] + ap;
     v[2] = v[2] - av;
     acc[0] += v[2] * v[2];
+  } else if constexpr (OP == EW_CG_NOX) {  // c0 = alpha; x += alpha p deferred
+    const double av = c0 * v[3];
+    v[2] = v[2] - av;
+    acc[0] += v[2] * v[2];
+  } else if constexpr (OP == EW_CG_X2) {  // c0 = alpha, c1 = the previous step's alpha
+    const double app = c1 * v[4];
+    const double xm = v[0] + app;  // the deferred x += alpha_prev p_prev
+    const double ap = c0 * v[1];
+    v[0] = xm + ap;
+    const double av = c0 * v[3];
+    v[2] = v[2] - av;
+    acc[0] += v[2] * v[2];
+  } else if constexpr (OP == EW_AXPY) {  // c0 = alpha
+    const double ap = c0 * v[1];
+    v[0] = v[0] + ap;
   } else if constexpr (OP == EW_CG_P) {  // c0 = beta
     const double bp = c0 * v[0];
     v[0] = v[1] + bp;
@@ -287,6 +314,8 @@ __device__ bool ew_prologue(const EwArgs& a, double* s_red, double& c0, double& 
     case SC_CG_ALPHA: {  // alpha = gamma / sigma  (v3/gpu/cg.py:33)
       const double sigma = slot(a.pro_s1);
       c0 = st[gamma_slot(a.pro_par)] / sigma;
+      if (a.pro_alpha == 1 && w0) st[ST_ALPHA] = c0;  // the deferred x step's alpha
+      if (a.pro_alpha == 2) c1 = st[ST_ALPHA];
       return true;
     }
     case SC_CG_BETA: {  // beta = gnew / gamma; gamma = gnew  (v3/gpu/cg.py:36-38)
@@ -919,6 +948,9 @@ int ew_products(EwOp op) {
     case EW_COPY: return EwTraits<EW_COPY>::NP;
     case EW_MRR_NOX: return EwTraits<EW_MRR_NOX>::NP;
     case EW_MRR_X2: return EwTraits<EW_MRR_X2>::NP;
+    case EW_CG_NOX: return EwTraits<EW_CG_NOX>::NP;
+    case EW_CG_X2: return EwTraits<EW_CG_X2>::NP;
+    case EW_AXPY: return EwTraits<EW_AXPY>::NP;
     case EW_ONE: return EwTraits<EW_ONE>::NP;
     case EW_PRE: return EwTraits<EW_PRE>::NP;
     case EW_PCG: return EwTraits<EW_PCG>::NP;
@@ -944,6 +976,9 @@ void launch_ew(EwOp op, const EwArgs& a, hipStream_t s) {
     case EW_COPY: ew_dispatch_op<EW_COPY>(a, s); break;
     case EW_MRR_NOX: ew_dispatch_op<EW_MRR_NOX>(a, s); break;
     case EW_MRR_X2: ew_dispatch_op<EW_MRR_X2>(a, s); break;
+    case EW_CG_NOX: ew_dispatch_op<EW_CG_NOX>(a, s); break;
+    case EW_CG_X2: ew_dispatch_op<EW_CG_X2>(a, s); break;
+    case EW_AXPY: ew_dispatch_op<EW_AXPY>(a, s); break;
     case EW_ONE: ew_dispatch_op<EW_ONE>(a, s); break;
     case EW_PRE: ew_dispatch_op<EW_PRE>(a, s); break;
     case EW_PCG: ew_dispatch_op<EW_PCG>(a, s); break;
