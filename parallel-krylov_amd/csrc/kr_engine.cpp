@@ -1846,22 +1846,38 @@ class MrrSession : public Base {
                                          prm.maxiter - i});
     sys->dev_stop = true;
     const bool fused = sys->fused_scalars();
+    // x -= z deferred in pairs of iterations (x is not read inside the loop):
+    // step j (even, j+1 < m) EW_MRR_NOX, step j+1 EW_MRR_X2 with
+    // x = (x - z_j+1) - z_j+2 -- its z input is z_j+1 -- the same roundings,
+    // one x read and write fewer per pair. KR_MRR_XDEFER=0 disables (A/B).
+    const char* xenv = getenv("KR_MRR_XDEFER");
+    const bool defer = !(xenv && atoi(xenv) == 0);
+    auto step_op = [&](int64_t j) {
+      if (defer && j % 2 == 0 && j + 1 < m) return EW_MRR_NOX;
+      if (defer && j % 2 == 1) return EW_MRR_X2;
+      return EW_MRR;
+    };
     for (int64_t j = 0; j < m; ++j) {
       if (j > 0) sys->prof_active = (sys->prof_tick++ % sys->profile_every) == 0;
       sys->spmv(EPI_MRR_LOOP, R, -1, AR, -1, Y, -1, 0);            // Ar = A r ; <r,r> mu nu
       if (fused) {  // the scalar steps inside the vector kernels: 3 launches
         sys->ew_pro(EW_MRR_S, SC_MRR_GAMMA, {AR, Y, R, -1, -1, -1}, 3, i + j, (int)j, 0, thr);
-        sys->ew_pro(EW_MRR, SC_MRR_ZETA, {Y, AR, Z, R, X, X}, 0, i + j, (int)j, 0, thr);
+        sys->ew_pro(step_op(j), SC_MRR_ZETA, {Y, AR, Z, R, X, X}, 0, i + j, (int)j, 0, thr);
         continue;
       }
       sys->scalar(SC_MRR_GAMMA, 0x7, i + j, (int)j, thr);          // test ; gamma = nu / mu
       sys->ew_dev(EW_MRR_S, ST_C0, {AR, Y, R, -1, -1, -1}, 3);     // s ; <r,s> <s,s>
       sys->scalar(SC_MRR_ZETA, 0x18, i + j, (int)j, thr);          // zeta, eta
-      sys->ew_dev(EW_MRR, ST_C2, {Y, AR, Z, R, X, X}, 0);
+      sys->ew_dev(step_op(j), ST_C2, {Y, AR, Z, R, X, X}, 0);
     }
     sys->dev_stop = false;
     sys->scalar_state_read();
     const double* h = sys->shards[0].hst;
+    if (h[ST_STOP] != 0.0) {  // stopped right after a NOX step: its x -= z
+      const int64_t jl = (int64_t)h[ST_STOP_AT] - 1 - i;  // the last update that ran
+      if (jl >= 0 && jl < m && step_op(jl) == EW_MRR_NOX)
+        sys->ew(EW_AXPY, -1.0, 0, {X, Z, -1, -1, -1, -1}, 0);  // x + (-1) z == x - z
+    }
     q.assign(h + ST_HIST, h + ST_HIST + m);
     qpos = 0;
     int64_t stop_at = -1;
