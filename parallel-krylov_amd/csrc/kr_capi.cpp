@@ -770,6 +770,7 @@ int kr_solve_end(kr_system* sys, double* const* x, kr_solve_result* res) {
     KR_REQUIRE(sys, "NULL system");
     if (!sys->session) throw Failure(KR_ERR_STATE, "kr_solve_begin was not called");
     Session& ss = *sys->session;
+    ss.settle();
     for (auto& s : sys->shards) {
       KR_HIP_CHECK(hipSetDevice(s.dev));
       KR_HIP_CHECK(hipStreamSynchronize(s.stream));

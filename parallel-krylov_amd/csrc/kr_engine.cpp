@@ -1189,6 +1189,7 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
         a.x3 = s.vec[st->x3];
         a.c2 = st->c2;
         a.c3 = st->c3;
+        a.xpend = st->xpend;
       }
     }
     return a;
@@ -1998,8 +1999,22 @@ class KskipMrrSession : public Base {
   // x -= z is deferred pairwise: step j stores z and leaves x (kind 0), step
   // j+1 applies x = (x - z_j) - z_{j+1} in registers (kind 1) -- the same two
   // roundings as the reference's two statements, one x read+write fewer. The
-  // last step of an outer iteration applies its own x -= z (kind 2).
-  int step_kind(int j) const { return (j % 2 == 0 && j < k) ? 0 : (j % 2 == 1 ? 1 : 2); }
+  // last step of an outer iteration applies its own x -= z (kind 2) -- unless
+  // xdefer: then it is left pending too (xpend) and the next outer
+  // iteration's fused steps 0+1 apply x = ((x - z_k) - z_1) - z_2, z_k being
+  // their z input (even k, non-adaptive: the adaptive rollback snapshots x).
+  // Every exit (convergence, maxiter, kr_solve_end) settles it first.
+  bool xdefer = false, xpend = false;
+  int step_kind(int j) const {
+    if (j % 2 == 0 && j < k) return 0;
+    if (j % 2 == 1) return 1;
+    return xdefer ? 0 : 2;
+  }
+  void settle() override {
+    if (!xpend) return;
+    sys->ew(EW_AXPY, -1.0, 0, {xsrc, Z, -1, -1, -1, -1}, 0);  // x + (-1) z == x - z
+    xpend = false;
+  }
 
  public:
   explicit KskipMrrSession(bool adapt) : adaptive(adapt) {}
@@ -2028,12 +2043,17 @@ class KskipMrrSession : public Base {
     i = 1;
     index = 1;
     set_entry(1, 0.0);
+    const char* xenv = getenv("KR_KSKIP_XDEFER");
+    xdefer = !adaptive && sys->fuse_steps && sys->fuse_first && k >= 2 && k % 2 == 0 &&
+             !(xenv && atoi(xenv) == 0);
+    xpend = false;
     head();
   }
 
   bool step_once() override {
     if (i >= prm.maxiter) {
       set_entry(index, rel(sys->reduce(kHead)[0]));
+      settle();
       return done = true;
     }
     chain(k);  // speculative: launched before the convergence test
@@ -2062,9 +2082,13 @@ class KskipMrrSession : public Base {
     }
     if (residual[index] < prm.tol) {
       converged = true;
+      settle();
       return done = true;
     }
-    if (guard_stop(index)) return true;
+    if (guard_stop(index)) {
+      settle();
+      return true;
+    }
     // Gram -> (alpha, beta, delta) as the reference lays them out.
     std::vector<double> alpha(2 * k + 3, 0.0), beta(2 * k + 2, 0.0), delta(2 * k + 1, 0.0);
     alpha[0] = g[0];
@@ -2112,7 +2136,9 @@ class KskipMrrSession : public Base {
       st.x3 = AR(1);
       st.c2 = eta[1];
       st.c3 = zeta[1];
+      st.xpend = xpend ? 1 : 0;
       sys->spmv(EPI_STEP_MRR_FIRST2, r0, y0, r_alt, -1, -1, -1, 0, &st);
+      xpend = false;
       xsrc = cur;
       std::swap(r0, r_alt);
       std::swap(y0, y_alt);
@@ -2136,6 +2162,7 @@ class KskipMrrSession : public Base {
                                     : kind == 1 ? EPI_STEP_MRR_X2 : EPI_STEP_MRR_X;
         sys->spmv(e, r0, -1, r_alt, -1, -1, -1, 0, &st);
         if (kind != 0) xsrc = cur;
+        if (kind == 0 && j == k) xpend = true;  // xdefer: left to the next outer iteration
         std::swap(r0, r_alt);
       } else {
         sys->spmv(EPI_NONE, r0, -1, AR(1), -1, -1, -1, 0);

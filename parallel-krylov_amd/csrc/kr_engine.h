@@ -139,6 +139,7 @@ struct StepOps {
   double c0 = 0, c1 = 0;
   int x3 = -1;          // EPI_STEP_MRR_FIRST2: Ar1 (gathered with r0 = in1, y0 = in2)
   double c2 = 0, c3 = 0;
+  int xpend = 0;        // EPI_STEP_MRR_FIRST2: SpmvArgs::xpend
 };
 
 // Exchange plan of global shard `me`: the rows it receives from / sends to
@@ -257,6 +258,8 @@ class Session {
   // Returns true when done.
   virtual bool step_once() = 0;
   virtual int result_x() const = 0;  // vector id holding the solution
+  // Apply any update of x still deferred (kr_solve_end, before x is read).
+  virtual void settle() {}
 
   System* sys = nullptr;
   kr_solve_params prm{};

@@ -132,6 +132,9 @@ struct SpmvArgs {
   const double* x3 = nullptr;  // EPI_STEP_MRR_FIRST2: Ar1 (halo-extended)
   const double* stop = nullptr;  // skip the launch when *stop != 0 (EwArgs::stop)
   double c2 = 0, c3 = 0;       // EPI_STEP_MRR_FIRST2: step-1 scalars (eta1, zeta1)
+  // EPI_STEP_MRR_FIRST2: the previous outer iteration's last x -= z is still
+  // pending (its z is this launch's z input u2): x = ((x - z0) - z1) - z2
+  int xpend = 0;
   int epi_late = 0;  // 1: load own-row epilogue operands at the row end (A/B, KR_EPI_LATE)
   // 1: the caller needs only the products (the last basis SpMV of a k-skip
   // outer iteration): a kernel MAY skip storing y1/y2 (the stencil walk does)

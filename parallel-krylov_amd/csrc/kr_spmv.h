@@ -340,7 +340,8 @@ __device__ __forceinline__ EpiVals epi_values(const SpmvArgs& a, double sum1, do
     const double s3 = a.c2 * z1;
     const double s4 = a.c3 * r1;
     const double z2 = s3 - s4;
-    const double xm = in.us - z1;  // x -= z of step 0, deferred
+    const double xs = a.xpend ? in.us - in.u2 : in.us;  // the previous outer's last x -= z
+    const double xm = xs - z1;  // x -= z of step 0, deferred
     o.ud = xm - z2;
     o.u1 = y2;
     o.u2 = z2;
