@@ -20,7 +20,9 @@ EPI = ["spmv", "spmv_bminus", "spmv_xy", "spmv_head_mrr", "spmv_head_kcg", "spmv
        "spmv2", "spmv2_gram_mrr", "spmv2_gram_kcg", "spmv_step_mrr_nox", "spmv_step_mrr_x2",
        "spmv_step_mrr_x", "spmv_step_kcg", "spmv_step_mrr_first2", "spmv_xy_vp"]
 EW = ["dot", "update_mrr_first", "update_mrr", "update_cg", "update_cg_p", "update_kcg",
-      "mrr_s", "copy", "update_mrr_nox", "update_mrr_x2"]
+      "mrr_s", "copy", "update_mrr_nox", "update_mrr_x2", "fill_one", "precond", "update_pcg",
+      "update_cg_gear", "update_gropp_xru", "update_gropp_ps", "precond_div", "update_cg_nox",
+      "update_cg_x2", "update_x", "update_pipecg"]
 
 
 def short(name):
@@ -38,7 +40,8 @@ def short(name):
         return EPI[int(m.group(2))] + ("_dia" if m.group(1) == "spmv_dia" else "_dense")
     m = re.search(r"ew_kernel<(\d+), (\w+)", name)
     if m:
-        return EW[int(m.group(1))] + ("" if m.group(2) == "true" else "_scalar")
+        i = int(m.group(1))
+        return (EW[i] if i < len(EW) else f"ew{i}") + ("" if m.group(2) == "true" else "_scalar")
     m = re.search(r"(\w+_kernel)\b", name)
     if m and name.startswith(("kr::", "void kr::")):
         return m.group(1)
