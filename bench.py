@@ -149,7 +149,10 @@ def stored_format_delta(nnz, n, lay, long_row=12.0):
     mw = lay["mask_bits"]
     if mw and lay["dict_values"] == 0 and nnz >= long_row * n:  # DIA (KR_DIA=1)
         n_pad = -(-n // 256) * 256
-        return 12.0 * nnz + 4.0 * (n + 1) - (8.0 * lay["n_offsets"] * n_pad + mw / 8 * n)
+        # symmetric values: the lower entries are read as the mirrored upper
+        # ones (L2 hits), so only the upper half + diagonal must stream
+        slots = (lay["n_offsets"] + 1) // 2 if lay.get("dia_sym") else lay["n_offsets"]
+        return 12.0 * nnz + 4.0 * (n + 1) - (8.0 * slots * n_pad + mw / 8 * n)
     d = 0.0
     if mw:
         d += 4.0 * nnz - mw / 8 * n
@@ -163,6 +166,9 @@ def format_name(lay):
         cb = lay.get("code_bits") or 8
         return (f"stencil codes (8 x {cb}-bit dictionary codes per row, "
                 f"{lay['dict_values']}-entry table; walk {lay['stencil_walk']} blocks)")
+    if lay.get("dia_sym"):
+        return (f"diagonal-offset values, {lay['n_offsets']} offsets, symmetric (upper half + "
+                f"diagonal streamed, lower entries read as the mirrored upper ones)")
     parts = [f"offset masks ({lay['mask_bits']}-bit)" if lay["mask_bits"] else "CSR columns"]
     parts.append(f"{lay['dict_values']}-entry value dictionary (1-byte codes)"
                  if lay["dict_values"] else "8-byte values")

@@ -246,6 +246,14 @@ int kr_system_shard_values(kr_system* sys, int shard, int* dict_values);
  * values on the 7-point pattern), i.e. the bytes of A one row streams.
  * Replaces nothing in the reference (cuSPARSE csrmv streams CSR). */
 int kr_system_shard_codes(kr_system* sys, int shard, int* code_bits);
+/* Symmetric diagonal-offset values of shard s (after finalize): 1 when the
+ * shard's offsets and stored values are symmetric (checked bitwise at
+ * finalize) and the DIA SpMV reads each lower entry as the mirrored upper
+ * entry of an earlier row, which the workgroup of that row block streams at
+ * the same time: only the upper half and the diagonal come from HBM (KR_DIA_SYM=0
+ * disables). Same values, same summation order: the results do not change.
+ * Replaces nothing in the reference (cuSPARSE csrmv streams every value). */
+int kr_system_shard_dia_sym(kr_system* sys, int shard, int* sym);
 /* Launch geometry of shard s (after finalize): grid = workgroups of the
  * elementwise kernels, spmv_grid = workgroups of the SpMV kernels,
  * stencil_walk = 0 for the row-walk SpMV (256-row blocks, one row per lane)

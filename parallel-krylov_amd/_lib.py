@@ -94,6 +94,7 @@ _SIGNATURES = {
     "kr_system_shard_layout": [_P, _I, _PI, _PI, _PI64, _PI64],
     "kr_system_shard_values": [_P, _I, _PI],
     "kr_system_shard_codes": [_P, _I, _PI],
+    "kr_system_shard_dia_sym": [_P, _I, _PI],
     "kr_system_shard_sched": [_P, _I, _PI, _PI, _PI, _PI],
     "kr_fill_rhs": [_P, _I, _U64, _P],
     "kr_system_csr": [_P, _I, _PP, _PI, _PP, _PP, _PI64],

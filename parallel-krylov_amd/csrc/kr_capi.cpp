@@ -661,6 +661,15 @@ int kr_system_shard_codes(kr_system* sys, int shard, int* code_bits) {
   });
 }
 
+int kr_system_shard_dia_sym(kr_system* sys, int shard, int* sym) {
+  return guarded([&] {
+    KR_REQUIRE(sys && shard >= 0 && shard < (int)sys->shards.size(), "bad shard");
+    KR_REQUIRE(sys->finalized, "system not finalized");
+    const Shard& s = sys->shards[shard];
+    if (sym) *sym = s.dia && s.dia_sym ? 1 : 0;
+  });
+}
+
 int kr_system_shard_sched(kr_system* sys, int shard, int* grid, int* spmv_grid,
                           int* stencil_walk, int* format) {
   return guarded([&] {

@@ -311,6 +311,22 @@ void System::build_masks(Shard& s) {
                     s.dia_ks, s.stream);
     s.dia = dia;
     plan_window(s, M);
+    // symmetric offsets and values: lower entries read as the mirrored upper
+    // ones (SpmvArgs::dia_sym; KR_DIA_SYM=0 disables, A/B)
+    const char* se = getenv("KR_DIA_SYM");
+    bool symM = blocked && nm % 2 == 1 && M[nm / 2] == 0;
+    for (int k = 0; symM && k < nm; ++k) symM = M[k] == -M[nm - 1 - k];
+    if (symM && !(se && atoi(se) == 0)) {
+      int* flag = nullptr;
+      KR_HIP_CHECK(hipMalloc(&flag, sizeof(int)));
+      KR_HIP_CHECK(hipMemsetAsync(flag, 0, sizeof(int), s.stream));
+      launch_dia_symcheck(mask, mw, s.n, dM, nm, dia, s.dia_bs, s.dia_ks, flag, s.stream);
+      int h = 1;
+      KR_HIP_CHECK(hipMemcpyAsync(&h, flag, sizeof(int), hipMemcpyDeviceToHost, s.stream));
+      KR_HIP_CHECK(hipStreamSynchronize(s.stream));
+      KR_HIP_CHECK(hipFree(flag));
+      s.dia_sym = h == 0 ? 1 : 0;
+    }
   }
   KR_HIP_CHECK(hipStreamSynchronize(s.stream));
   s.mask = mask;
@@ -1120,6 +1136,7 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
         a.dia = s.dia + (r_begin / kDiaRows) * s.dia_bs;
         a.dia_bs = s.dia_bs;
         a.dia_ks = s.dia_ks;
+        a.dia_sym = s.dia_sym;
         a.dia_wlen = s.dia_wlen;
         a.nseg = s.nseg;
         for (int g = 0; g < s.nseg; ++g) {

@@ -85,6 +85,7 @@ struct Shard {
   void* mask = nullptr;             // offset masks (SpmvArgs::mask), owned
   double* dia = nullptr;            // diagonal-offset values (SpmvArgs::dia), owned
   int64_t dia_bs = 0, dia_ks = 0;  // SpmvArgs::dia_bs / dia_ks
+  int dia_sym = 0;                  // SpmvArgs::dia_sym
   int dia_wlen = 0, nseg = 0;       // SpmvArgs x window (dia_wlen, nseg, seg_*, woff)
   int seg_lo[4] = {}, seg_len[4] = {}, seg_base[4] = {};
   int32_t* woff = nullptr;

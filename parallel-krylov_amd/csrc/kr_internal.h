@@ -113,6 +113,11 @@ struct SpmvArgs {
   // dia_ks = 256. The SpMV then needs neither LDS staging nor rowptr.
   const double* dia = nullptr;
   int64_t dia_bs = 0, dia_ks = 0;
+  // Symmetric values (System::build_masks checked A[i][i-o] == A[i-o][i]
+  // bitwise for every stored lower entry): a lower entry is read as its
+  // mirrored upper entry of row i - o, which the workgroup of that row block
+  // streams at the same time (an L2 hit), instead of its own copy (HBM).
+  int dia_sym = 0;
   // x window in LDS (spmv_dia_kernel): nseg segments, segment g = rows
   // row0 + seg_lo[g] .. + seg_len[g] - 1 of the row block at s_xw[seg_base[g]]
   // (starts and lengths even), dia_wlen doubles in all (0: gathers from global
@@ -374,6 +379,10 @@ constexpr int kMaxMaskBits = 64;
 // Diagonal-offset values from a masked CSR block (values of row i at offset
 // M[b] land in dia[b * ld + i]; absent entries stay 0).
 constexpr int kDiaRows = 256;  // rows per DIA row block (== kBlock)
+// flag[0] = 1 unless every stored lower entry dia(i, k) (M[k] < 0, M symmetric)
+// equals dia(i + M[k], nm-1-k) bitwise wherever i + M[k] >= 0.
+void launch_dia_symcheck(const void* mask, int mw, int64_t n, const int32_t* M, int nm,
+                         const double* dia, int64_t bs, int64_t ks, int* flag, hipStream_t s);
 void launch_dia_fill(const void* rowptr, int rowptr64, int64_t n, const int32_t* col,
                      const double* val, int64_t base, const int32_t* M, int nm, double* dia,
                      int64_t bs, int64_t ks, hipStream_t s);

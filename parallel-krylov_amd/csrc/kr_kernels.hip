@@ -1345,6 +1345,37 @@ void launch_stencil_pack(const uint64_t* in, int64_t n, int cb, void* out, hipSt
   KR_HIP_CHECK(hipGetLastError());
 }
 
+namespace {
+__global__ void dia_symcheck_kernel(const uint8_t* __restrict__ mask, int mb, int64_t n,
+                                    const int32_t* __restrict__ M, int nm,
+                                    const double* __restrict__ dia, int64_t bs, int64_t ks,
+                                    int* flag) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    for (int k = 0; k < nm / 2; ++k) {
+      if (!((mask[i * mb + k / 8] >> (k % 8)) & 1)) continue;
+      const int64_t j = i + M[k];
+      if (j < 0) continue;
+      const int km = nm - 1 - k;
+      const bool there = (mask[j * mb + km / 8] >> (km % 8)) & 1;
+      const double lo = dia[(i / kDiaRows) * bs + k * ks + i % kDiaRows];
+      const double up = dia[(j / kDiaRows) * bs + km * ks + j % kDiaRows];
+      if (!there || __double_as_longlong(lo) != __double_as_longlong(up))
+        *flag = 1;  // plain vector store: every writer stores 1
+    }
+  }
+}
+}  // namespace
+
+void launch_dia_symcheck(const void* mask, int mw, int64_t n, const int32_t* M, int nm,
+                         const double* dia, int64_t bs, int64_t ks, int* flag, hipStream_t s) {
+  if (n <= 0) return;
+  const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 65535);
+  dia_symcheck_kernel<<<g, 256, 0, s>>>(static_cast<const uint8_t*>(mask), mw / 8, n, M, nm, dia,
+                                        bs, ks, flag);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
 void launch_dia_fill(const void* rowptr, int rowptr64, int64_t n, const int32_t* col,
                      const double* val, int64_t base, const int32_t* M, int nm, double* dia,
                      int64_t bs, int64_t ks, hipStream_t s) {

@@ -1713,7 +1713,20 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(SpmvArgs a) {
       for (int u = 0; u < CH; ++u) {
         const int k = min(k0 + u, nm - 1);
         const bool ok = k0 + u < nm && ((m >> k) & 1);
-        v[u] = __builtin_nontemporal_load(dia_row + (int64_t)k * a.dia_ks);
+        if (a.dia_sym) {
+          // lower entry k of row rr = upper entry nm-1-k of row rr + M[k]
+          // (bitwise equal, checked at finalize): that row block's workgroup
+          // streams it now, so it comes from L2; temporal loads keep the
+          // upper values there for it
+          const int64_t jm = rr + load_uniform(a.moff, k);
+          const bool mir = ok && 2 * k < nm - 1 && jm >= 0;
+          const double* src = mir ? dia + (jm / kDiaRows) * a.dia_bs +
+                                        (int64_t)(nm - 1 - k) * a.dia_ks + jm % kDiaRows
+                                  : dia_row + (int64_t)k * a.dia_ks;
+          v[u] = *src;
+        } else {
+          v[u] = __builtin_nontemporal_load(dia_row + (int64_t)k * a.dia_ks);
+        }
         if constexpr (XL) {
           const int lc = lx + load_uniform(a.woff, k);  // inside the window even if absent
           p1[u] = s_xw[lc];

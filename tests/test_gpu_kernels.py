@@ -534,3 +534,34 @@ def test_value_dictionary_spmv_bitwise(torch_dev, monkeypatch, name, shards):
         np.testing.assert_array_equal(y, ref)
         assert np.array_equal(np.signbit(y), np.signbit(ref))
         sysm.close()
+
+
+@pytest.mark.parametrize("shards", [1, 3])
+@pytest.mark.parametrize("spec", [["banded", 3001, 13, 64, 0], ["banded", 2000, 31, 256, 0]])
+def test_dia_symmetric_values_read_mirrored(torch_dev, monkeypatch, spec, shards):
+    """Symmetric banded values: the DIA SpMV reads every lower entry as the
+    mirrored upper entry of an earlier row (kr_system_shard_dia_sym = 1) and
+    stays bitwise scipy's; one perturbed value (pattern still symmetric)
+    turns it off for the shard holding it, and KR_DIA_SYM=0 everywhere."""
+    from parallel_krylov_amd.system import KrylovSystem, balanced_partition
+    A = golden_matrix(spec).tocsr()
+    n = A.shape[0]
+    B = A.copy()
+    B.data = B.data.copy()
+    r = 10
+    B.data[B.indptr[r + 1] - 1] += 1e-3  # an upper entry of row 10, its mirror unchanged
+    x = np.random.default_rng(3).standard_normal(n)
+    # (the check is per shard: only the shard holding row 10 loses it)
+    for M, env, want in ((A, "1", [1] * shards), (B, "1", [0] + [1] * (shards - 1)),
+                         (A, "0", [0] * shards)):
+        monkeypatch.setenv("KR_DIA_SYM", env)
+        sysm = KrylovSystem(n, balanced_partition(n, shards), [0] * shards)
+        try:
+            sysm.set_matrix(M)
+            sysm.finalize()
+            assert [sysm.shard_format(s) for s in range(shards)] == ["dia"] * shards
+            assert [sysm.shard_layout(s)["dia_sym"] for s in range(shards)] == want
+            y = sysm.gather(sysm.spmv(sysm.split(x)))
+            np.testing.assert_array_equal(y.cpu().numpy(), M.dot(x))
+        finally:
+            sysm.close()
