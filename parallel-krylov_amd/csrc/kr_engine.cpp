@@ -1098,11 +1098,12 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
   // boundary launches ADD their reduction partials to the interior launch's
   // (same stream, fixed order: deterministic).
   const bool split = exchange && overlap && all_interior;
-  // products only: the stencil kernel skips the y1/y2 stores (its own stat
-  // name, and 16 N fewer bytes)
+  // products only: the stencil kernel and the windowed diagonal-offset
+  // kernel skip the y1/y2 stores (own stat name, and 16 N fewer bytes)
   bool po = products_only && products_only_on && dual;
+  auto po_shard = [&](const Shard& s) { return po && (s.scode || (s.dia && s.dia_wlen > 0)); };
   bool po_any = false;
-  for (auto& s : shards) po_any = po_any || (po && s.scode);
+  for (auto& s : shards) po_any = po_any || po_shard(s);
   const char* nm = po_any ? epi_name_po(epi) : epi_name(epi);
 
   auto args_for = [&](Shard& s, int64_t r_begin, int64_t rows, int grid, int acc) {
@@ -1170,7 +1171,7 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
       a.scratch = s.scratch;
     }
     a.epi_late = epi_late;
-    a.products_only = po && s.scode ? 1 : 0;
+    a.products_only = po_shard(s) ? 1 : 0;
     a.stop = dev_stop ? s.st + ST_STOP : nullptr;
     a.nnz_total = s.nnz;
     if (s.dense) {
@@ -1221,7 +1222,7 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
                          : step ? (step_x ? 48.0 : 32.0) * s.n
                                 : (b >= 0 || e >= 0) ? 8.0 * s.n : 0.0;
     if (s.dense) return 8.0 * s.nnz + nv * 8.0 * (n_global + s.n) + extra;
-    const double stores = (po && s.scode) ? 0.0 : nv * 8.0 * s.n;  // y1 (, y2)
+    const double stores = po_shard(s) ? 0.0 : nv * 8.0 * s.n;  // y1 (, y2)
     return 12.0 * s.nnz + (s.rowptr64 ? 8.0 : 4.0) * (s.n + 1) + nv * 8.0 * s.n + stores + extra;
   };
   // The partial stride is s.pstride for every launch; the full / interior

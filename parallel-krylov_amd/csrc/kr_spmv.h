@@ -396,6 +396,10 @@ __device__ __forceinline__ void epi_store_row(const SpmvArgs& a, int64_t row, co
     a.u2[row] = o.u2;
     a.y1[row] = o.y1;
   } else {
+    // a two-vector SpMV whose outputs nobody reads (SpmvArgs::products_only:
+    // the windowed diagonal-offset kernel; the stencil kernel stores pairs)
+    if constexpr (EpiTraits<EPI>::NV == 2)
+      if (a.products_only) return;
     a.y1[row] = o.y1;
     if constexpr (EpiTraits<EPI>::NV == 2) a.y2[row] = o.y2;
     if constexpr (EPI == EPI_XY_VP) a.u1[row] = o.u1;
