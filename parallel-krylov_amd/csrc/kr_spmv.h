@@ -1643,7 +1643,13 @@ __device__ __forceinline__ double2 window_pair(const double* __restrict__ x, int
   return make_double2(x[i0], x[i1]);
 }
 
-template <int EPI, int MW, int CH, bool XL>  // CH: offsets per load batch; XL: x window in LDS
+// SYMUP > 0 (SpmvArgs::dia_sym, at most SYMUP diagonal + upper slots): the
+// row's own diagonal and upper values are loaded first, all at once, then the
+// lower entries as the mirrored upper entries of earlier rows -- which the
+// neighbouring row block's workgroup, at the same point of its own row
+// block, is loading at that moment (its upper values come first too), so
+// one of the two reads hits L2. The sums keep the stored (ascending) order.
+template <int EPI, int MW, int CH, bool XL, int SYMUP = 0>
 __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(SpmvArgs a) {
   if (!spmv_entry<EPI>(a)) return;  // converged / the fused scalar step's test fired
   using T = EpiTraits<EPI>;
@@ -1711,50 +1717,88 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(SpmvArgs a) {
     const int lx = (int)(rr - rb0);  // own row in the block
     const double* dia_row = dia + (rr / kDiaRows) * a.dia_bs + (rr % kDiaRows);
     double sum1 = 0.0, sum2 = 0.0;
-    for (int k0 = 0; k0 < nm; k0 += CH) {
-      double v[CH], p1[CH], p2[CH], p3[VIRT ? CH : 1];
-#pragma unroll
-      for (int u = 0; u < CH; ++u) {
-        const int k = min(k0 + u, nm - 1);
-        const bool ok = k0 + u < nm && ((m >> k) & 1);
-        if (a.dia_sym) {
-          // lower entry k of row rr = upper entry nm-1-k of row rr + M[k]
-          // (bitwise equal, checked at finalize): that row block's workgroup
-          // streams it now, so it comes from L2; temporal loads keep the
-          // upper values there for it
-          const int64_t jm = rr + load_uniform(a.moff, k);
-          const bool mir = ok && 2 * k < nm - 1 && jm >= 0;
-          const double* src = mir ? dia + (jm / kDiaRows) * a.dia_bs +
-                                        (int64_t)(nm - 1 - k) * a.dia_ks + jm % kDiaRows
-                                  : dia_row + (int64_t)k * a.dia_ks;
-          v[u] = *src;
-        } else {
-          v[u] = __builtin_nontemporal_load(dia_row + (int64_t)k * a.dia_ks);
+    // x of offset slot k at this row (window or gather) and the sum of one
+    // entry, rounded as everywhere (product, then the add; absent: skipped)
+    auto fetch_x = [&](int k, bool ok, double& p1, double& p2, double& p3) {
+      if constexpr (XL) {
+        const int lc = lx + load_uniform(a.woff, k);  // inside the window even if absent
+        p1 = s_xw[lc];
+        if constexpr (NV == 2) p2 = s_xw[wlen + lc];
+      } else {
+        const int64_t c = ok ? xrow + load_uniform(a.moff, k) : xrow;
+        p1 = x1[c];
+        if constexpr (NV == 2 || VIRT) p2 = x2[c];
+        if constexpr (VIRT) p3 = a.x3[c];
+      }
+    };
+    auto add_entry = [&](bool ok, double v, double p1, double p2, double p3) {
+      if constexpr (VIRT && !XL) {
+        const double t = sum1 + v * virt_in<EPI>(a, p1, p2, p3);
+        sum1 = ok ? t : sum1;
+      } else {
+        const double t1 = sum1 + v * p1;
+        sum1 = ok ? t1 : sum1;
+        if constexpr (NV == 2) {
+          const double t2 = sum2 + v * p2;
+          sum2 = ok ? t2 : sum2;
         }
-        if constexpr (XL) {
-          const int lc = lx + load_uniform(a.woff, k);  // inside the window even if absent
-          p1[u] = s_xw[lc];
-          if constexpr (NV == 2) p2[u] = s_xw[wlen + lc];
-        } else {
-          const int64_t c = ok ? xrow + load_uniform(a.moff, k) : xrow;
-          p1[u] = x1[c];
-          if constexpr (NV == 2 || VIRT) p2[u] = x2[c];
-          if constexpr (VIRT) p3[u] = a.x3[c];
+      }
+    };
+    if constexpr (SYMUP > 0) {
+      const int h = nm / 2;  // lower slots 0..h-1, the diagonal h, upper h+1..nm-1
+      double up[SYMUP];
+#pragma unroll
+      for (int u = 0; u < SYMUP; ++u) up[u] = dia_row[(int64_t)min(h + u, nm - 1) * a.dia_ks];
+      for (int k0 = 0; k0 < h; k0 += CH) {
+        double v[CH], p1[CH], p2[CH], p3[CH];
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+          const int k = min(k0 + u, h - 1);
+          const bool ok = k0 + u < h && ((m >> k) & 1);
+          // lower entry k of row rr = upper entry nm-1-k of row rr + M[k]
+          // (bitwise equal, checked at finalize); own copy before the launch's rows
+          const int64_t jm = rr + load_uniform(a.moff, k);
+          v[u] = ok && jm >= 0 ? dia[(jm / kDiaRows) * a.dia_bs +
+                                     (int64_t)(nm - 1 - k) * a.dia_ks + jm % kDiaRows]
+                               : dia_row[(int64_t)k * a.dia_ks];
+          fetch_x(k, ok, p1[u], p2[u], p3[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+          const bool ok = k0 + u < h && ((m >> min(k0 + u, h - 1)) & 1);
+          add_entry(ok, v[u], p1[u], p2[u], p3[u]);
         }
       }
 #pragma unroll
-      for (int u = 0; u < CH; ++u) {
-        const bool ok = k0 + u < nm && ((m >> min(k0 + u, nm - 1)) & 1);
-        if constexpr (VIRT && !XL) {
-          const double t = sum1 + v[u] * virt_in<EPI>(a, p1[u], p2[u], p3[u]);
-          sum1 = ok ? t : sum1;
-        } else {
-          const double t1 = sum1 + v[u] * p1[u];
-          sum1 = ok ? t1 : sum1;
-          if constexpr (NV == 2) {
-            const double t2 = sum2 + v[u] * p2[u];
-            sum2 = ok ? t2 : sum2;
+      for (int u = 0; u < SYMUP; ++u) {
+        const int k = min(h + u, nm - 1);
+        const bool ok = h + u < nm && ((m >> k) & 1);
+        double p1 = 0.0, p2 = 0.0, p3 = 0.0;
+        fetch_x(k, ok, p1, p2, p3);
+        add_entry(ok, up[u], p1, p2, p3);
+      }
+    } else {
+      for (int k0 = 0; k0 < nm; k0 += CH) {
+        double v[CH], p1[CH], p2[CH], p3[CH];
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+          const int k = min(k0 + u, nm - 1);
+          const bool ok = k0 + u < nm && ((m >> k) & 1);
+          if (a.dia_sym) {  // mirrored lower entries in stored order (KR_DIA_SYMUP=0)
+            const int64_t jm = rr + load_uniform(a.moff, k);
+            v[u] = ok && 2 * k < nm - 1 && jm >= 0
+                       ? dia[(jm / kDiaRows) * a.dia_bs + (int64_t)(nm - 1 - k) * a.dia_ks +
+                             jm % kDiaRows]
+                       : dia_row[(int64_t)k * a.dia_ks];
+          } else {
+            v[u] = __builtin_nontemporal_load(dia_row + (int64_t)k * a.dia_ks);
           }
+          fetch_x(k, ok, p1[u], p2[u], p3[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+          const bool ok = k0 + u < nm && ((m >> min(k0 + u, nm - 1)) & 1);
+          add_entry(ok, v[u], p1[u], p2[u], p3[u]);
         }
       }
     }
@@ -1764,15 +1808,30 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(SpmvArgs a) {
   block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
 }
 
-template <int E, bool XL>
-void spmv_dia_launch_xl(const SpmvArgs& a, int nblocks, hipStream_t s) {
+template <int E, bool XL, int SYMUP>
+void spmv_dia_launch_sym(const SpmvArgs& a, int nblocks, hipStream_t s) {
   const size_t lds = XL ? sizeof(double) * a.dia_wlen * EpiTraits<E>::NV : 0;  // virtual: NV 1
   switch (a.mw) {
-    case 8: spmv_dia_kernel<E, 8, 8, XL><<<nblocks, kBlock, lds, s>>>(a); return;
-    case 16: spmv_dia_kernel<E, 16, 8, XL><<<nblocks, kBlock, lds, s>>>(a); return;
-    case 32: spmv_dia_kernel<E, 32, 8, XL><<<nblocks, kBlock, lds, s>>>(a); return;
-    default: spmv_dia_kernel<E, 64, 8, XL><<<nblocks, kBlock, lds, s>>>(a); return;
+    case 8: spmv_dia_kernel<E, 8, 8, XL, SYMUP><<<nblocks, kBlock, lds, s>>>(a); return;
+    case 16: spmv_dia_kernel<E, 16, 8, XL, SYMUP><<<nblocks, kBlock, lds, s>>>(a); return;
+    case 32: spmv_dia_kernel<E, 32, 8, XL, SYMUP><<<nblocks, kBlock, lds, s>>>(a); return;
+    default: spmv_dia_kernel<E, 64, 8, XL, SYMUP><<<nblocks, kBlock, lds, s>>>(a); return;
   }
+}
+
+template <int E, bool XL>
+void spmv_dia_launch_xl(const SpmvArgs& a, int nblocks, hipStream_t s) {
+  // symmetric values: diagonal + upper slots = nm - nm/2 <= 16 or 32 registers
+  // (KR_DIA_SYMUP=0: mirrored lower entries read in stored order instead)
+  static const int upfirst = [] {
+    const char* e = getenv("KR_DIA_SYMUP");
+    return e ? atoi(e) : 1;
+  }();
+  if (a.dia_sym && upfirst && a.nm - a.nm / 2 <= 16)
+    return spmv_dia_launch_sym<E, XL, 16>(a, nblocks, s);
+  if (a.dia_sym && upfirst && a.nm - a.nm / 2 <= 32)
+    return spmv_dia_launch_sym<E, XL, 32>(a, nblocks, s);
+  spmv_dia_launch_sym<E, XL, 0>(a, nblocks, s);
 }
 
 template <int E>
