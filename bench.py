@@ -46,6 +46,10 @@ CONFIGS = {
 }
 
 
+# Per-kernel event sampling per config (bench --profile-every default).
+PROFILE_EVERY = {"C1": 64, "C2": 8, "C3": 8}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -65,8 +69,10 @@ def parse():
                    help="grid side of the CPU-baseline sample (512 = the benchmark system)")
     p.add_argument("--no-profile", action="store_true",
                    help="skip the per-kernel HIP-event timing")
-    p.add_argument("--profile-every", type=int, default=4,
-                   help="per-kernel HIP events on every N-th step (1 = all)")
+    p.add_argument("--profile-every", type=int, default=None,
+                   help="per-kernel HIP events on every N-th step (1 = all); default 4, "
+                        "64 for C1 and 8 for C2/C3, whose steps are 16-600 us long and "
+                        "would pay the ~10 us per event pair too often")
     return p.parse_args()
 
 
@@ -226,7 +232,8 @@ def run_system(args, cfg, mat, n, world, rank, local, comm, method, k, env=None)
     # per-kernel HIP events on every 4th step (each event pair costs ~10 us of
     # launch gap; sampled, the timing costs <1 % at the 8-GPU shard size)
     sysm.begin(method, b, None, tol=0.0, maxiter=maxiter, k=k,
-               profile=0 if args.no_profile else args.profile_every)
+               profile=0 if args.no_profile else (args.profile_every or PROFILE_EVERY.get(
+                   args.config, 4)))
     sysm.step(args.warmup)
     sysm.reset_kernel_stats()
 

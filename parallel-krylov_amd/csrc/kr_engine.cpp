@@ -1484,6 +1484,11 @@ void System::ew_pro(EwOp op, ScalarOp sop, std::array<int, 6> ids, int slot0, in
   a.pro_thr = thr;
   a.pro_s1 = s1;
   a.pro_alpha = alpha;
+  static const int pre = [] {
+    const char* e = getenv("KR_EW_PREFETCH");
+    return e ? atoi(e) : 1;
+  }();
+  a.pro_pre = pre;
   for (int p = 0; p < ew_products(op); ++p) s.slot_n[slot0 + p] = s.grid;
   hipEvent_t t0 = nullptr;
   const char* nm = ew_name(op);

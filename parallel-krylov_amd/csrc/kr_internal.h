@@ -275,6 +275,7 @@ struct EwArgs {
   double pro_thr = 0;
   int pro_s1 = 1;                  // SC_CG_ALPHA: sigma's slot (EPI_XY: 1, EPI_XY_VP: 4)
   int pro_alpha = 0;               // SC_CG_ALPHA: 1 save alpha to ST_ALPHA, 2 c1 = ST_ALPHA
+  int pro_pre = 1;                 // VEC: the first operands loaded before the prologue
 };
 void launch_ew(EwOp op, const EwArgs& a, hipStream_t s);
 

@@ -368,7 +368,6 @@ __global__ __launch_bounds__(kBlock) void ew_kernel(EwArgs a) {
   if (a.stop && *a.stop != 0.0) return;
   double c0 = a.cdev ? a.cdev[0] : a.c0;
   double c1 = a.cdev ? a.cdev[1] : a.c1;
-  if (a.pro && !ew_prologue(a, s_red, c0, c1)) return;
   double acc[NP > 0 ? NP : 1];
 #pragma unroll
   for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;
@@ -379,8 +378,8 @@ __global__ __launch_bounds__(kBlock) void ew_kernel(EwArgs a) {
     // before any store (the operands may alias, so the compiler cannot hoist
     // the next iteration's loads above this iteration's stores by itself).
     const int64_t npairs = a.n >> 1;
-    for (int64_t q0 = t0; q0 < npairs; q0 += U * stride) {
-      double va[U][kEwOps], vb[U][kEwOps];
+    double va[U][kEwOps], vb[U][kEwOps];
+    auto load = [&](int64_t q0) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t q = q0 + u * stride;
@@ -395,6 +394,15 @@ __global__ __launch_bounds__(kBlock) void ew_kernel(EwArgs a) {
           }
         }
       }
+    };
+    // The first pairs' operands do not depend on the fused scalar step, so
+    // they are in flight while the prologue sums the partials (one memory
+    // latency instead of two; the small systems are latency-bound).
+    // KR_EW_PREFETCH=0 (a.pro_pre = 0): after it (A/B).
+    if (a.pro && a.pro_pre) load(t0);
+    if (a.pro && !ew_prologue(a, s_red, c0, c1)) return;
+    for (int64_t q0 = t0; q0 < npairs; q0 += U * stride) {
+      if (!(a.pro && a.pro_pre) || q0 != t0) load(q0);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t q = q0 + u * stride;
@@ -425,6 +433,7 @@ __global__ __launch_bounds__(kBlock) void ew_kernel(EwArgs a) {
         if (T::W & (1 << k)) a.p[k][i] = v[k];
     }
   } else {
+    if (a.pro && !ew_prologue(a, s_red, c0, c1)) return;
     for (int64_t i = t0; i < a.n; i += stride) {
       double v[kEwOps];
 #pragma unroll
