@@ -15,7 +15,7 @@ from conftest import REPO
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("ranks", [2, 3])
+@pytest.mark.parametrize("ranks", [2, 3, 4])
 def test_mpi_family_over_rccl(ranks):
     env = dict(os.environ, NCCL_DEBUG="ERROR")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
