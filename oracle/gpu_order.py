@@ -96,7 +96,7 @@ def stencil_grid(rows, P):
     cols = P if pm else 8 * P
     Z = 1
     if pm:
-        while cols * Z < 4096 and planes // (Z * 2) >= 16:
+        while cols * Z < 16384 and planes // (Z * 2) >= 16:
             Z *= 2
         while cols * Z < 1024 and planes // (Z * 2) >= 8:
             Z *= 2

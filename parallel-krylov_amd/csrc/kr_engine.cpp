@@ -447,10 +447,12 @@ int stencil_grid(int64_t rows, int P) {
   if (env && atoi(env) > 0) {
     Z = atoi(env);
   } else if (pm) {
-    // walks of >= 16 planes up to 4096 workgroups (512^3: 4096 x 64 planes;
-    // an 8-GPU slab of 64 planes: 2048 x 16, +3 % over plane-major), then
-    // >= 8 planes up to 1024 workgroups (mid-size cubes keep their parallelism)
-    while (cols * Z < 4096 && planes / (Z * 2) >= 16) Z *= 2;
+    // walks of >= 16 planes up to 16384 workgroups (512^3: 16384 x 16 planes,
+    // +1.9 % over 4096 x 64 on C4 -- dual, head and step SpMVs faster, the
+    // products-only dual slower; an 8-GPU slab of 64 planes: 2048 x 16, +3 %
+    // over plane-major), then >= 8 planes up to 1024 workgroups (mid-size
+    // cubes keep their parallelism)
+    while (cols * Z < 16384 && planes / (Z * 2) >= 16) Z *= 2;
     while (cols * Z < 1024 && planes / (Z * 2) >= 8) Z *= 2;
   } else {
     while (cols * Z < 2048 && planes / (8 * Z * 2) >= 8) Z *= 2;
