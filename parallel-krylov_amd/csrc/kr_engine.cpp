@@ -89,6 +89,7 @@ const char* epi_name(SpmvEpi e) {
     case EPI_STEP_KCG: return "spmv_step_kcg";
     case EPI_STEP_MRR_FIRST2: return "spmv_step_mrr_first2";
     case EPI_XY_VP: return "spmv_xy_vp";
+    case EPI_MRR_V: return "spmv_mrr_v";
   }
   return "spmv?";
 }
@@ -1076,7 +1077,7 @@ void System::halo_async(int id1, int id2, int id3) {
 void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int b,
                   int slot0, const StepOps* st) {
   const bool dual = (epi == EPI_DUAL_NONE || epi == EPI_DUAL_MRR || epi == EPI_DUAL_KCG);
-  const bool virt = epi == EPI_STEP_MRR_FIRST2;
+  const bool virt = epi == EPI_STEP_MRR_FIRST2 || epi == EPI_MRR_V;
   const bool vp = epi == EPI_XY_VP;  // CG's virtual p (System::spmv_vp)
   KR_REQUIRE(!vp || (in2 >= 0 && st && st->u1 >= 0 && st->u1 != in1 && st->u1 != in2 &&
                      vp_pro.sop == SC_CG_BETA),
@@ -1120,7 +1121,7 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
     a.x2 = (dual || virt || vp) ? s.vec[in2] : nullptr;
     a.xoff = s.pad + r_begin;
     a.y1 = s.own(out1) + r_begin;
-    a.y2 = dual ? s.own(out2) + r_begin : nullptr;
+    a.y2 = (dual || epi == EPI_MRR_V) ? s.own(out2) + r_begin : nullptr;
     a.b = b >= 0 ? s.own(b) + r_begin : nullptr;
     a.e = e >= 0 ? s.own(e) + r_begin : nullptr;
     a.partials = s.partials + (size_t)slot0 * s.pstride;
@@ -1210,6 +1211,13 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
         a.c2 = st->c2;
         a.c3 = st->c3;
         a.xpend = st->xpend;
+      }
+      if (epi == EPI_MRR_V && st->pro) {  // SC_MRR_ZETA from the EW_MRR_S partials
+        a.pro = (int)SC_MRR_ZETA + 1;
+        a.pro_part = s.partials;
+        a.pro_stride = s.pstride;
+        for (int q = 0; q < 5; ++q) a.pro_cnt[q] = s.slot_n[q];
+        a.st = s.st;
       }
     }
     return a;
@@ -1860,7 +1868,10 @@ class CgSession : public Base {
 // --------------------------------------------------------------------- MrR
 // v3/gpu/mrr.py:8-65 (oracle v3/cpu/mrr.py:7-61)
 class MrrSession : public Base {
-  enum { X, B, R, Y, Z, AR, NV };
+  enum { X, B, R, Y, Z, AR, R2, Y2, AR2, NV };
+  // r, y, Ar alternate with r2, y2, Ar2 when the vector step runs inside the
+  // next SpMV (EPI_MRR_V): other rows still gather the old ones
+  int r = R, y = Y, ar = AR, r2 = R2, y2 = Y2, ar2 = AR2;
   bool dev = false;
   double thr = 0;
   std::vector<double> q;  // <r,r> at the top of the iterations of the batch
@@ -1872,12 +1883,21 @@ class MrrSession : public Base {
                                          prm.maxiter - i});
     sys->dev_stop = true;
     const bool fused = sys->fused_scalars();
+    // One shard, fused scalars, a kernel with virtual inputs (sys->fuse_first):
+    // iteration j's vector step runs inside iteration j+1's SpMV (EPI_MRR_V):
+    // 2 launches per iteration, r / y / Ar read once for both. Stencil / row
+    // walk shards: MrR 256^3 +7 %, 256^2 +15-29 %. Not on diagonal-offset
+    // shards, whose kernel with three gathered inputs and the five-vector
+    // epilogue runs at 2 waves/SIMD (C3: 1.27 ms vs 0.40 + 0.12). KR_MRR_V=0: off.
+    const char* venv = getenv("KR_MRR_V");
+    const bool vfuse = fused && sys->fuse_first && !sys->shards[0].dia &&
+                       !(venv && atoi(venv) == 0);
     // x -= z deferred in pairs of iterations (x is not read inside the loop):
     // step j (even, j+1 < m) EW_MRR_NOX, step j+1 EW_MRR_X2 with
     // x = (x - z_j+1) - z_j+2 -- its z input is z_j+1 -- the same roundings,
     // one x read and write fewer per pair. KR_MRR_XDEFER=0 disables (A/B).
     const char* xenv = getenv("KR_MRR_XDEFER");
-    const bool defer = !(xenv && atoi(xenv) == 0);
+    const bool defer = !vfuse && !(xenv && atoi(xenv) == 0);
     auto step_op = [&](int64_t j) {
       if (defer && j % 2 == 0 && j + 1 < m) return EW_MRR_NOX;
       if (defer && j % 2 == 1) return EW_MRR_X2;
@@ -1885,23 +1905,43 @@ class MrrSession : public Base {
     };
     for (int64_t j = 0; j < m; ++j) {
       if (j > 0) sys->prof_active = (sys->prof_tick++ % sys->profile_every) == 0;
-      sys->spmv(EPI_MRR_LOOP, R, -1, AR, -1, Y, -1, 0);            // Ar = A r ; <r,r> mu nu
+      if (vfuse) {
+        if (j == 0) sys->spmv(EPI_MRR_LOOP, r, -1, ar, -1, y, -1, 0);  // Ar = A r ; <r,r> mu nu
+        sys->ew_pro(EW_MRR_S, SC_MRR_GAMMA, {ar, y, r, -1, -1, -1}, 3, i + j, (int)j, 0, thr);
+        if (j + 1 < m) {  // step j, then Ar = A r of iteration j+1 ; <r,r> mu nu
+          StepOps st;
+          st.u1 = y2;
+          st.u2 = Z;
+          st.us = X;
+          st.ud = X;
+          st.x3 = ar;
+          st.pro = 1;
+          sys->spmv(EPI_MRR_V, r, y, ar2, r2, -1, -1, 0, &st);
+          std::swap(r, r2);
+          std::swap(y, y2);
+          std::swap(ar, ar2);
+        } else {
+          sys->ew_pro(EW_MRR, SC_MRR_ZETA, {y, ar, Z, r, X, X}, 0, i + j, (int)j, 0, thr);
+        }
+        continue;
+      }
+      sys->spmv(EPI_MRR_LOOP, r, -1, ar, -1, y, -1, 0);            // Ar = A r ; <r,r> mu nu
       if (fused) {  // the scalar steps inside the vector kernels: 3 launches
-        sys->ew_pro(EW_MRR_S, SC_MRR_GAMMA, {AR, Y, R, -1, -1, -1}, 3, i + j, (int)j, 0, thr);
-        sys->ew_pro(step_op(j), SC_MRR_ZETA, {Y, AR, Z, R, X, X}, 0, i + j, (int)j, 0, thr);
+        sys->ew_pro(EW_MRR_S, SC_MRR_GAMMA, {ar, y, r, -1, -1, -1}, 3, i + j, (int)j, 0, thr);
+        sys->ew_pro(step_op(j), SC_MRR_ZETA, {y, ar, Z, r, X, X}, 0, i + j, (int)j, 0, thr);
         continue;
       }
       sys->scalar(SC_MRR_GAMMA, 0x7, i + j, (int)j, thr);          // test ; gamma = nu / mu
-      sys->ew_dev(EW_MRR_S, ST_C0, {AR, Y, R, -1, -1, -1}, 3);     // s ; <r,s> <s,s>
+      sys->ew_dev(EW_MRR_S, ST_C0, {ar, y, r, -1, -1, -1}, 3);     // s ; <r,s> <s,s>
       sys->scalar(SC_MRR_ZETA, 0x18, i + j, (int)j, thr);          // zeta, eta
-      sys->ew_dev(step_op(j), ST_C2, {Y, AR, Z, R, X, X}, 0);
+      sys->ew_dev(step_op(j), ST_C2, {y, ar, Z, r, X, X}, 0);
     }
     sys->dev_stop = false;
     sys->scalar_state_read();
     const double* h = sys->shards[0].hst;
     if (h[ST_STOP] != 0.0) {  // stopped right after a NOX step: its x -= z
       const int64_t jl = (int64_t)h[ST_STOP_AT] - 1 - i;  // the last update that ran
-      if (jl >= 0 && jl < m && step_op(jl) == EW_MRR_NOX)
+      if (jl >= 0 && jl < m && defer && step_op(jl) == EW_MRR_NOX)
         sys->ew(EW_AXPY, -1.0, 0, {X, Z, -1, -1, -1, -1}, 0);  // x + (-1) z == x - z
     }
     q.assign(h + ST_HIST, h + ST_HIST + m);
@@ -1942,7 +1982,7 @@ class MrrSession : public Base {
   }
   bool step_once() override {
     if (i >= prm.maxiter) {
-      sys->ew(EW_DOT, 0, 0, {R, R, -1, -1, -1, -1}, 0);
+      sys->ew(EW_DOT, 0, 0, {r, r, -1, -1, -1, -1}, 0);
       set_entry(i, rel(sys->reduce(1)[0]));
       index = i;
       return done = true;
@@ -1956,7 +1996,7 @@ class MrrSession : public Base {
         return done = true;
       }
     } else {
-      sys->spmv(EPI_MRR_LOOP, R, -1, AR, -1, Y, -1, 0);  // Ar = A r ; <r,r> mu nu
+      sys->spmv(EPI_MRR_LOOP, r, -1, ar, -1, y, -1, 0);  // Ar = A r ; <r,r> mu nu
       const auto g = sys->reduce(3);
       set_entry(i, rel(g[0]));
       index = i;
@@ -1966,11 +2006,11 @@ class MrrSession : public Base {
       }
       if (guard_stop(i)) return true;
       const double gamma = g[2] / g[1];  // nu / mu
-      sys->ew(EW_MRR_S, gamma, 0, {AR, Y, R, -1, -1, -1}, 0);
+      sys->ew(EW_MRR_S, gamma, 0, {ar, y, r, -1, -1, -1}, 0);
       const auto h = sys->reduce(2);
       const double zeta = h[0] / h[1];
       const double eta = (-zeta) * gamma;
-      sys->ew(EW_MRR, eta, zeta, {Y, AR, Z, R, X, X}, 0);
+      sys->ew(EW_MRR, eta, zeta, {y, ar, Z, r, X, X}, 0);
     }
     i += 1;
     set_nosl(i, i);

@@ -141,6 +141,7 @@ struct StepOps {
   int x3 = -1;          // EPI_STEP_MRR_FIRST2: Ar1 (gathered with r0 = in1, y0 = in2)
   double c2 = 0, c3 = 0;
   int xpend = 0;        // EPI_STEP_MRR_FIRST2: SpmvArgs::xpend
+  int pro = 0;          // EPI_MRR_V: run the SC_MRR_ZETA step in the prologue
 };
 
 // Exchange plan of global shard `me`: the rows it receives from / sends to

@@ -77,6 +77,14 @@ enum SpmvEpi : int {
   // different buffer than x1: other rows still gather p_old), y1 = A p,
   // products <p,p> <p,y> <y,y> as EPI_XY. Replaces EW_CG_P + EPI_XY.
   EPI_XY_VP,
+  // MrR with device-resident scalars on one shard: the previous iteration's
+  // vector step runs inside this SpMV. Its SC_MRR_ZETA scalar step is the
+  // prologue (c0 = eta, c1 = zeta), the input r_new = r - (eta*y + zeta*Ar)
+  // is formed at every gathered column from x1 = r, x2 = y, x3 = Ar (the
+  // EW_MRR rounding), the own rows store u1 = y_new, u2 = z_new (in place),
+  // ud = x - z_new, y2 = r_new, y1 = A r_new, and the products are
+  // EPI_MRR_LOOP's (<r,r> mu nu of the new vectors). Replaces EW_MRR + EPI_MRR_LOOP.
+  EPI_MRR_V,
 };
 int spmv_products(SpmvEpi epi);
 

@@ -35,6 +35,8 @@ extern template void spmv_launch_epi<EPI_STEP_MRR_X2>(const SpmvArgs&, int, hipS
 extern template void spmv_launch_epi<EPI_STEP_MRR_X>(const SpmvArgs&, int, hipStream_t);
 extern template void spmv_launch_epi<EPI_STEP_KCG>(const SpmvArgs&, int, hipStream_t);
 extern template void spmv_launch_epi<EPI_STEP_MRR_FIRST2>(const SpmvArgs&, int, hipStream_t);
+extern template void spmv_launch_epi<EPI_MRR_V>(const SpmvArgs&, int, hipStream_t);
+extern template void spmv_launch_epi<EPI_XY_VP>(const SpmvArgs&, int, hipStream_t);
 
 namespace {
 
@@ -909,6 +911,7 @@ int spmv_products(SpmvEpi epi) {
     case EPI_STEP_KCG:
     case EPI_STEP_MRR_FIRST2: return 0;
     case EPI_XY_VP: return EpiTraits<EPI_XY_VP>::NP;
+    case EPI_MRR_V: return EpiTraits<EPI_MRR_V>::NP;
   }
   return 0;
 }
@@ -938,6 +941,7 @@ void launch_spmv_grid(SpmvEpi epi, const SpmvArgs& a, int nblocks, hipStream_t s
     KR_CASE(EPI_STEP_KCG)
     KR_CASE(EPI_STEP_MRR_FIRST2)
     KR_CASE(EPI_XY_VP)
+    KR_CASE(EPI_MRR_V)
 #undef KR_CASE
     default:
       throw Failure(KR_ERR_INVALID, "unknown SpMV epilogue");

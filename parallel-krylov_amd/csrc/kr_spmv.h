@@ -124,15 +124,26 @@ struct EpiTraits<EPI_XY_VP> {  // x = p_old, x2 = r at the row (p formed from th
   static constexpr int NP = 3, NV = 1;
   static constexpr bool kX = true, kX2 = true, kE = false;
 };
+template <>
+struct EpiTraits<EPI_MRR_V> {  // products of EPI_MRR_LOOP over the new vectors
+  static constexpr int NP = 3, NV = 1;
+  static constexpr bool kX = false, kX2 = false, kE = false;
+};
 template <int EPI>
 constexpr bool is_step() {
   return EPI == EPI_STEP_MRR_NOX || EPI == EPI_STEP_MRR_X2 || EPI == EPI_STEP_MRR_X ||
-         EPI == EPI_STEP_KCG || EPI == EPI_STEP_MRR_FIRST2;
+         EPI == EPI_STEP_KCG || EPI == EPI_STEP_MRR_FIRST2 || EPI == EPI_MRR_V;
 }
 // The SpMV input is virtual: r1 = r0 - (c0*y0 + c1*Ar1) at every column.
 template <int EPI>
 constexpr bool is_virtual() {
-  return EPI == EPI_STEP_MRR_FIRST2 || EPI == EPI_XY_VP;
+  return EPI == EPI_STEP_MRR_FIRST2 || EPI == EPI_XY_VP || EPI == EPI_MRR_V;
+}
+// Epilogues whose own-row operands include r, y, Ar of the virtual input
+// (x1, x2, x3 at the row) and the x source (us).
+template <int EPI>
+constexpr bool is_vstep() {
+  return EPI == EPI_STEP_MRR_FIRST2 || EPI == EPI_MRR_V;
 }
 // r1 at one column, rounded exactly like ew_kernel<EW_MRR_NOX>'s step 0:
 // y1 = fl(fl(c0*y0) + fl(c1*ar1)), r1 = fl(r0 - y1).
@@ -218,6 +229,18 @@ __device__ __forceinline__ bool spmv_entry(SpmvArgs& a) {
   if constexpr (EPI == EPI_XY_VP) {
     if (a.pro && !spmv_prologue_beta(a)) return false;
   }
+  if constexpr (EPI == EPI_MRR_V) {
+    // SC_MRR_ZETA (v3/gpu/mrr.py:47-49) from the EW_MRR_S partials, summed in
+    // the finalize order like ew_prologue: zeta = <r,s>/<s,s>, eta = -zeta*gamma
+    if (a.pro) {
+      __shared__ double s_r[4];
+      const double rs = 0.0 + slot_sum(a.pro_part + (int64_t)3 * a.pro_stride, a.pro_cnt[3], s_r);
+      const double ss = 0.0 + slot_sum(a.pro_part + (int64_t)4 * a.pro_stride, a.pro_cnt[4], s_r);
+      const double zeta = rs / ss;
+      a.c0 = (-zeta) * a.st[ST_GAMMA];
+      a.c1 = zeta;
+    }
+  }
   return true;
 }
 
@@ -290,10 +313,9 @@ __device__ __forceinline__ EpiIn epi_load(const SpmvArgs& a, int64_t row) {
   if constexpr (is_step<EPI>()) {
     in.u1 = a.u1[row];
     in.u2 = a.u2[row];
-    if constexpr (EPI == EPI_STEP_MRR_X2 || EPI == EPI_STEP_MRR_X ||
-                  EPI == EPI_STEP_MRR_FIRST2)
+    if constexpr (EPI == EPI_STEP_MRR_X2 || EPI == EPI_STEP_MRR_X || is_vstep<EPI>())
       in.us = a.us[row];
-    if constexpr (EPI == EPI_STEP_MRR_FIRST2) {
+    if constexpr (is_vstep<EPI>()) {
       in.x2 = a.x2[a.xoff + row];  // y0
       in.e = a.x3[a.xoff + row];   // Ar1
     }
@@ -313,7 +335,7 @@ struct EpiVals {
 };
 template <int EPI>
 constexpr bool epi_writes_ud() {
-  return EPI == EPI_STEP_MRR_X2 || EPI == EPI_STEP_MRR_X || EPI == EPI_STEP_MRR_FIRST2;
+  return EPI == EPI_STEP_MRR_X2 || EPI == EPI_STEP_MRR_X || is_vstep<EPI>();
 }
 
 template <int EPI>
@@ -346,6 +368,23 @@ __device__ __forceinline__ EpiVals epi_values(const SpmvArgs& a, double sum1, do
     o.u1 = y2;
     o.u2 = z2;
     o.y1 = r1 - y2;  // Ar0 of step 2
+  } else if constexpr (EPI == EPI_MRR_V) {
+    // the previous iteration's EW_MRR step at the own row (c0 = eta,
+    // c1 = zeta; x = r, x2 = y, e = Ar, u2 = z, us = x), statement for
+    // statement as ew_kernel<EW_MRR>; sum1 = (A r_new)[row]
+    const double t1 = a.c0 * in.x2;
+    const double t2 = a.c1 * in.e;
+    const double y = t1 + t2;
+    const double t3 = a.c0 * in.u2;
+    const double t4 = a.c1 * in.x;
+    const double z = t3 - t4;
+    const double r = in.x - y;
+    o.ud = in.us - z;
+    o.u1 = y;
+    o.u2 = z;
+    o.y2 = r;
+    o.y1 = sum1;
+    epi_products<EPI_MRR_LOOP>(r, 0.0, sum1, 0.0, y, acc);  // <r,r> mu nu
   } else if constexpr (EPI == EPI_XY_VP) {
     const double pv = virtual_p(a.c0, in.x, in.x2);  // p at the own row
     o.u1 = pv;
@@ -395,6 +434,7 @@ __device__ __forceinline__ void epi_store_row(const SpmvArgs& a, int64_t row, co
     a.u1[row] = o.u1;
     a.u2[row] = o.u2;
     a.y1[row] = o.y1;
+    if constexpr (EPI == EPI_MRR_V) a.y2[row] = o.y2;
   } else {
     // a two-vector SpMV whose outputs nobody reads (SpmvArgs::products_only:
     // the windowed diagonal-offset kernel; the stencil kernel stores pairs)
@@ -424,6 +464,7 @@ __device__ __forceinline__ void epi_store_pair(const SpmvArgs& a, int64_t row, c
     st2(a.u1, lo.u1, hi.u1);
     st2(a.u2, lo.u2, hi.u2);
     st2(a.y1, lo.y1, hi.y1);
+    if constexpr (EPI == EPI_MRR_V) st2(a.y2, lo.y2, hi.y2);
   } else {
     st2(a.y1, lo.y1, hi.y1);
     if constexpr (EpiTraits<EPI>::NV == 2) st2(a.y2, lo.y2, hi.y2);

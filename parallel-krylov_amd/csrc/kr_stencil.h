@@ -159,7 +159,7 @@ __device__ __forceinline__ void st_issue(SStage<NX, NFAR, CB>& st, const SpmvArg
   if constexpr (is_step<EPI>()) {
     st.u1 = *reinterpret_cast<const dbl2v*>(a.u1 + rr);
     st.u2 = *reinterpret_cast<const dbl2v*>(a.u2 + rr);
-    if constexpr (EPI == EPI_STEP_MRR_X2 || EPI == EPI_STEP_MRR_X || EPI == EPI_STEP_MRR_FIRST2)
+    if constexpr (EPI == EPI_STEP_MRR_X2 || EPI == EPI_STEP_MRR_X || is_vstep<EPI>())
       st.us = *reinterpret_cast<const dbl2v*>(a.us + rr);
   } else if constexpr (EPI == EPI_BMINUS) {
     st.e = *reinterpret_cast<const dbl2v*>(a.b + rr);
@@ -199,7 +199,7 @@ __device__ __forceinline__ EpiIn st_epi_in(double c0, double c1, double c2, doub
     in.u1 = u1;
     in.u2 = u2;
     in.us = us;
-    if constexpr (EPI == EPI_STEP_MRR_FIRST2) in.e = c2;
+    if constexpr (is_vstep<EPI>()) in.e = c2;
   } else {
     in.e = e;
   }

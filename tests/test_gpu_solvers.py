@@ -240,7 +240,8 @@ def test_fused_steps_bitwise_equal_unfused(monkeypatch, shards, method, matrix, 
     ("cg", ["banded", 3000, 13, 64, 0], 1e-10, 400), ("mrr", ["poisson", 16, 2], 1e-10, 400),
     ("mrr", ["poisson", 12, 3], 1e-8, 9), ("mrr", ["banded", 3000, 13, 64, 0], 1e-9, 400),
     ("cg", ["poisson", 8, 2], 0.0, 40), ("mrr", ["poisson", 8, 2], 0.5, 40),
-    ("cg", ["poisson", 64, 3], 1e-9, 90), ("cg", ["poisson", 64, 3], 0.0, 70)])
+    ("cg", ["poisson", 64, 3], 1e-9, 90), ("cg", ["poisson", 64, 3], 0.0, 70),
+    ("mrr", ["poisson", 64, 3], 1e-9, 90), ("mrr", ["poisson", 64, 3], 0.0, 37)])
 @pytest.mark.parametrize("shards", ["0", "0,0,0"])
 def test_device_scalars_bitwise_equal_host(monkeypatch, shards, method, matrix, tol, maxiter):
     """CG / MrR with device-resident scalars (batches of iterations, the
@@ -252,9 +253,10 @@ def test_device_scalars_bitwise_equal_host(monkeypatch, shards, method, matrix, 
     steps fused into the vector kernels, or separate) and on three in-process
     shards (slot totals gathered on the first shard, summed in shard order;
     coefficients and stop flag copied to the others). One-shard CG folds
-    the p update into the next SpMV (EPI_XY_VP) unless KR_CG_VP=0: the same
-    bits either way (64^3: the stencil kernel; 2-D: the row walk; banded:
-    the diagonal-offset kernel)."""
+    the p update into the next SpMV (EPI_XY_VP) unless KR_CG_VP=0, and
+    one-shard MrR its vector step (EPI_MRR_V, stencil and row-walk shards):
+    the same bits either way (64^3: the stencil kernel; 2-D: the row walk;
+    banded: the diagonal-offset kernel)."""
     A = golden_matrix(matrix)
     b = np.random.default_rng(11).standard_normal(A.shape[0])
     kw = dict(tol=tol, maxiter=maxiter)

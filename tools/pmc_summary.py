@@ -18,7 +18,7 @@ import sys
 # Names follow kr_internal.h's SpmvEpi / EwOp enums (and kr_engine's epi_name/ew_name).
 EPI = ["spmv", "spmv_bminus", "spmv_xy", "spmv_head_mrr", "spmv_head_kcg", "spmv_mrr_loop",
        "spmv2", "spmv2_gram_mrr", "spmv2_gram_kcg", "spmv_step_mrr_nox", "spmv_step_mrr_x2",
-       "spmv_step_mrr_x", "spmv_step_kcg", "spmv_step_mrr_first2", "spmv_xy_vp"]
+       "spmv_step_mrr_x", "spmv_step_kcg", "spmv_step_mrr_first2", "spmv_xy_vp", "spmv_mrr_v"]
 EW = ["dot", "update_mrr_first", "update_mrr", "update_cg", "update_cg_p", "update_kcg",
       "mrr_s", "copy", "update_mrr_nox", "update_mrr_x2", "fill_one", "precond", "update_pcg",
       "update_cg_gear", "update_gropp_xru", "update_gropp_ps", "precond_div", "update_cg_nox",
