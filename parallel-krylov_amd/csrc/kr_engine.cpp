@@ -1885,13 +1885,10 @@ class MrrSession : public Base {
     const bool fused = sys->fused_scalars();
     // One shard, fused scalars, a kernel with virtual inputs (sys->fuse_first):
     // iteration j's vector step runs inside iteration j+1's SpMV (EPI_MRR_V):
-    // 2 launches per iteration, r / y / Ar read once for both. Stencil / row
-    // walk shards: MrR 256^3 +7 %, 256^2 +15-29 %. Not on diagonal-offset
-    // shards, whose kernel with three gathered inputs and the five-vector
-    // epilogue runs at 2 waves/SIMD (C3: 1.27 ms vs 0.40 + 0.12). KR_MRR_V=0: off.
+    // 2 launches per iteration, r / y / Ar read once for both. MrR 256^3
+    // +7 %, 256^2 +15-29 %, C3 (symmetric DIA) +8-9 %. KR_MRR_V=0: off.
     const char* venv = getenv("KR_MRR_V");
-    const bool vfuse = fused && sys->fuse_first && !sys->shards[0].dia &&
-                       !(venv && atoi(venv) == 0);
+    const bool vfuse = fused && sys->fuse_first && !(venv && atoi(venv) == 0);
     // x -= z deferred in pairs of iterations (x is not read inside the loop):
     // step j (even, j+1 < m) EW_MRR_NOX, step j+1 EW_MRR_X2 with
     // x = (x - z_j+1) - z_j+2 -- its z input is z_j+1 -- the same roundings,

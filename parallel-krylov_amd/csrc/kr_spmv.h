@@ -1733,7 +1733,12 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(SpmvArgs a) {
     const int64_t xrow = a.xoff + rr;
     if constexpr (XL) {
       __syncthreads();  // the previous row block is done with the window
-      for (int g = 0; g < a.nseg; ++g) {
+      // unrolled: constant indices into a.seg_* (a runtime index into the
+      // kernel argument, once a prologue has written a.c0, puts the whole
+      // SpmvArgs copy in scratch)
+#pragma unroll
+      for (int g = 0; g < SpmvArgs::kMaxSeg; ++g) {
+        if (g >= a.nseg) break;
         // segment starts are even (host), xoff and rb0 too: 16-byte loads
         const int64_t src = a.xoff + rb0 + a.seg_lo[g];
         const int half = a.seg_len[g] >> 1;

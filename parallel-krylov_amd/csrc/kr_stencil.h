@@ -391,12 +391,17 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
         dbl2v g[NX];
 #pragma unroll
         for (int v = 0; v < NX; ++v) g[v] = cur.nxt[v];
+        // selects on values (a branch per f let the compiler index cur.far
+        // with the run-time kind: the stage sets went to scratch, PAT = 0)
 #pragma unroll
-        for (int f = 0; f < NFAR; ++f)
-          if (kind == SK_FAR + f) {
+        for (int f = 0; f < NFAR; ++f) {
+          const bool s = kind == SK_FAR + f;
 #pragma unroll
-            for (int v = 0; v < NX; ++v) g[v] = cur.far[f][v];
+          for (int v = 0; v < NX; ++v) {
+            g[v].x = s ? cur.far[f][v].x : g[v].x;
+            g[v].y = s ? cur.far[f][v].y : g[v].y;
           }
+        }
         if constexpr (VIRT) {
           xlo[0] = virt_in<EPI>(a, g[0].x, g[1].x, g[NX - 1].x);
           xhi[0] = virt_in<EPI>(a, g[0].y, g[1].y, g[NX - 1].y);
