@@ -87,9 +87,14 @@ def stencil_pm(P):
     return P % 8 == 0
 
 
-def stencil_grid(rows, P):
+def stencil_grid(rows, P, zmax=0):
     """kr_engine.cpp stencil_grid: position-major P x Zt segments, or
-    plane-major 8 XCDs x P positions x Z segments."""
+    plane-major 8 XCDs x P positions x Z segments. zmax > 0 caps Z: the
+    products-only dual's grid on position-major shards (Shard::spmv_grid_po,
+    zmax 16), which differs from the general grid only on shards of >= 512
+    planes; the emulation below
+    sums every SpMV's products over the general grid, so it is exact for
+    shards under that size (test_products_only_grid_matches_below_512_planes)."""
     nrb = -(-rows // 512)
     planes = -(-nrb // P)
     pm = stencil_pm(P)
@@ -103,6 +108,8 @@ def stencil_grid(rows, P):
     else:
         while cols * Z < 2048 and planes // (8 * Z * 2) >= 8:
             Z *= 2
+    if zmax > 0 and Z > zmax:
+        Z = zmax
     return cols * Z
 
 

@@ -438,7 +438,7 @@ bool stencil_pm(int P) {
   return P % 8 == 0;
 }
 
-int stencil_grid(int64_t rows, int P) {
+int stencil_grid(int64_t rows, int P, int zmax = 0) {
   const int64_t nrb = (rows + kStencilBlock - 1) / kStencilBlock;
   const int64_t planes = (nrb + P - 1) / P;
   const bool pm = stencil_pm(P);
@@ -458,6 +458,7 @@ int stencil_grid(int64_t rows, int P) {
   } else {
     while (cols * Z < 2048 && planes / (8 * Z * 2) >= 8) Z *= 2;
   }
+  if (zmax > 0 && Z > zmax) Z = zmax;
   return (int)(cols * Z);
 }
 
@@ -684,6 +685,17 @@ void System::finalize() {
                                                                          (int64_t)grid_cap() * 4))
                   : s.scode ? stencil_grid(s.n, s.st_P)
                             : spmv_grid_for(s.n, s.reach);
+    // The products-only dual (a read-only stream: codes and two x vectors)
+    // runs faster on fewer, longer walks: 512^3 0.69 -> 0.59 ms at Z <= 16
+    // (16 or 8 alike, 32 is the general grid's). Smaller shards already have
+    // Z <= 16, so only >= 512-plane shards change; position-major walks
+    // (3-D stencils) only, the measured case. KR_PO_ZMAX=0: the general grid.
+    {
+      const char* ze = getenv("KR_PO_ZMAX");
+      const int zmax = ze ? atoi(ze) : 16;
+      s.spmv_grid_po = s.scode && zmax > 0 && stencil_pm(s.st_P)
+                           ? stencil_grid(s.n, s.st_P, zmax) : s.spmv_grid;
+    }
     s.pstride = std::max(s.grid, s.spmv_grid);
     s.slot_n.fill(0);
     KR_HIP_CHECK(hipMalloc(&s.partials, sizeof(double) * (size_t)kMaxSlots * s.pstride));
@@ -1239,9 +1251,10 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
   // launch writes s.spmv_grid partials per product, the boundary launch (fewer
   // blocks) adds into the first entries.
   const int np = spmv_products(epi);
+  auto grid_of = [&](const Shard& s) { return po_shard(s) ? s.spmv_grid_po : s.spmv_grid; };
   auto launch_full = [&](Shard& s, int64_t r_begin, int64_t rows) {
-    launch_spmv_grid(epi, args_for(s, r_begin, rows, s.pstride, 0), s.spmv_grid, s.stream);
-    for (int p = 0; p < np; ++p) s.slot_n[slot0 + p] = s.spmv_grid;
+    launch_spmv_grid(epi, args_for(s, r_begin, rows, s.pstride, 0), grid_of(s), s.stream);
+    for (int p = 0; p < np; ++p) s.slot_n[slot0 + p] = grid_of(s);
   };
 
   if (!split) {
@@ -1287,7 +1300,7 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
       ab.rb_gap_at = nb_lo;
       ab.rb_gap = nb_gap;
       // (the stencil kernel's boundary launch spreads its blocks over the grid)
-      const int g = (int)std::min<int64_t>(s.spmv_grid, nb_all - nb_gap);
+      const int g = (int)std::min<int64_t>(grid_of(s), nb_all - nb_gap);
       launch_spmv_grid(epi, ab, g, s.stream);
     }
     prof_end(s, nm, t0s[li], bytes_of(s));

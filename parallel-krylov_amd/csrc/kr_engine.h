@@ -106,6 +106,7 @@ struct Shard {
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   int grid = 1;                 // workgroups of the vector kernels
   int spmv_grid = 1;            // workgroups of the SpMV kernels
+  int spmv_grid_po = 1;         // ... of a products-only stencil launch (<= spmv_grid)
   int pstride = 1;              // partial stride per slot: max(grid, spmv_grid)
   std::array<int, kMaxSlots> slot_n{};  // partials written per slot by its last producer
   // reductions

@@ -68,6 +68,19 @@ def test_gpu_order_oracle_rolls_back(case):
     assert info["residual"][-1] < 1e-10
 
 
+@pytest.mark.parametrize("n", [8, 16, 24, 32, 64, 96, 128, 256])
+def test_products_only_grid_matches_below_512_planes(n):
+    """The products-only dual's capped grid (KR_PO_ZMAX, 16) equals the
+    general grid on every cube below 512^3 (so the emulation, which sums over
+    the general grid, stays exact there) and differs at 512^3 (P x 16 vs
+    P x 32 workgroups)."""
+    rows = n ** 3
+    P = max(1, n * n // 512)
+    assert gpu_order.stencil_grid(rows, P, 16) == gpu_order.stencil_grid(rows, P)
+    assert gpu_order.stencil_grid(512 ** 3, 512, 16) == 512 * 16
+    assert gpu_order.stencil_grid(512 ** 3, 512) == 512 * 32
+
+
 def test_gpu_order_dot_is_a_dot():
     """Same products, another order: within rounding of numpy's dot, and
     exactly the lane/wave/block order on a case small enough to spell out."""
