@@ -76,14 +76,33 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(n_side: int, k: int, method: str, return_info: bool = False):
+def cpu_model():
+    """Host CPU model name (/proc/cpuinfo), or the platform string."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or platform.machine()
+
+
+def cpu_baseline(n_side: int, k: int, method: str, return_info: bool = False, outer: int = 2):
     """The oracle (numpy/scipy restatement of v3/cpu, bitwise the reference) on
-    the host cores, on a bounded sample: the initial MrR step plus ONE outer
-    k-skip iteration (k+2 solver iterations) of the same system (512^3 by
-    default; a smaller n_side is scaled to 512^3 by the row ratio, since SpMV
-    and dots are linear in N). Timed region = the reference's info['time'].
-    With return_info, also the oracle's (x-free) info dict: its residual
-    history is the full-size parity check of the GPU run (bench `parity`)."""
+    the host cores, on a bounded sample: the initial MrR step plus `outer`
+    outer k-skip iterations (1 + outer (k+1) solver iterations, 11 at k = 4)
+    of the same system (512^3 by default; a smaller n_side is scaled to 512^3
+    by the row ratio, since SpMV and dots are linear in N). Timed region = the
+    reference's info['time']. With return_info, also the oracle's (x-free)
+    info dict: its residual history is the full-size parity check of the GPU
+    run (bench `parity`, outer + 2 entries).
+
+    Threads: scipy's csr_matvec is single-threaded; numpy's dots run on
+    OpenBLAS with its default pool, which follows OPENBLAS_NUM_THREADS /
+    OMP_NUM_THREADS (the GPU box sets 16: the CPU share of one GPU of the
+    node, although the process may be scheduled on more affinity cores)."""
     import numpy as np
     from oracle import matrices, v3cpu
     try:
@@ -95,7 +114,7 @@ def cpu_baseline(n_side: int, k: int, method: str, return_info: bool = False):
     A = matrices.poisson(n_side, 3)
     b = matrices.rhs(A.shape[0], 1)
     fn = v3cpu.METHODS[method]
-    kw = dict(tol=0.0, maxiter=(k + 2) if "kskip" in method else 6)
+    kw = dict(tol=0.0, maxiter=(outer * (k + 1) + 1) if "kskip" in method else 6)
     if "kskip" in method:
         kw["k"] = k
     t0 = time.perf_counter()
@@ -107,14 +126,21 @@ def cpu_baseline(n_side: int, k: int, method: str, return_info: bool = False):
     cores = len(os.sched_getaffinity(0))
     scale = (n_side ** 3) / (512 ** 3)
     scaled = "" if n_side == 512 else f", scaled x{scale:.4f} to 512^3"
+    env_threads = {v: os.environ[v] for v in ("OPENBLAS_NUM_THREADS", "OMP_NUM_THREADS")
+                   if v in os.environ}
     rec = dict(value=rate * scale, unit="iterations/s",
                cores=blas_threads if blas_threads else cores,
                kind="port",
+               cpu_model=cpu_model(), affinity_cores=cores, blas_threads=blas_threads,
+               thread_env=env_threads,
                sample=(f"oracle.v3cpu.{method} (numpy/scipy restatement of v3/cpu, bitwise "
-                       f"the reference) on {n_side}^3 Poisson, {its} iterations in "
+                       f"the reference) on {n_side}^3 Poisson, {its} iterations "
+                       f"(initial step + {outer} outer) in "
                        f"{info['time']:.2f} s ({rate:.3f} it/s){scaled}; "
-                       f"scipy SpMV 1 thread, OpenBLAS dot {blas_threads} threads, "
-                       f"{cores} affinity cores; wall {wall:.1f} s"))
+                       f"scipy SpMV 1 thread, OpenBLAS dot {blas_threads} threads "
+                       f"({', '.join(f'{k_}={v}' for k_, v in env_threads.items()) or 'no thread env'}), "
+                       f"{cores} affinity cores, {cpu_model()}; wall {wall:.1f} s; "
+                       f"cores = the BLAS threads (the SpMV, most of the time, uses one)"))
     return (rec, info) if return_info else rec
 
 
@@ -127,17 +153,23 @@ def history_parity(gpu_info, ref_info, rtol=PARITY_RTOL):
     """Full-size parity: the GPU run's first history entries against the
     oracle's run of the SAME system (same b, x0 = 0) in the cpu_baseline leg.
     The oracle stops at maxiter (its last entry is the exit branch's
-    recomputed norm of the same r), so entries are compared by index."""
+    recomputed norm of the same r), so entries are compared by index. A GPU
+    history shorter than the oracle's is a parity failure (ok false, both
+    lengths recorded), never an exception."""
     import numpy as np
     m = len(ref_info["residual"])
-    g_res = np.asarray(gpu_info["residual"][:m], dtype=np.float64)
+    g_all = np.asarray(gpu_info["residual"], dtype=np.float64)
     r_res = np.asarray(ref_info["residual"], dtype=np.float64)
-    nosl_eq = bool(np.array_equal(np.asarray(gpu_info["nosl"][:m]), ref_info["nosl"]))
-    big = r_res >= 1e-8
-    rel = np.abs(g_res - r_res) / np.abs(r_res)
+    c = min(m, len(g_all))
+    g_res = g_all[:c]
+    nosl_eq = bool(len(gpu_info["nosl"]) >= m and
+                   np.array_equal(np.asarray(gpu_info["nosl"][:m]), ref_info["nosl"]))
+    big = r_res[:c] >= 1e-8
+    rel = np.abs(g_res - r_res[:c]) / np.abs(r_res[:c])
     max_rel = float(rel[big].max()) if big.any() else 0.0
-    ok = nosl_eq and len(g_res) == m and max_rel <= rtol
-    return dict(ok=bool(ok), entries=int(m), nosl_equal=nosl_eq, max_rel=max_rel, rtol=rtol,
+    ok = nosl_eq and c == m and max_rel <= rtol
+    return dict(ok=bool(ok), entries=int(c), oracle_entries=int(m), nosl_equal=nosl_eq,
+                max_rel=max_rel, rtol=rtol,
                 reference="oracle.v3cpu (bitwise the reference's v3/cpu), same b, x0 = 0",
                 gpu=[float(v) for v in g_res], oracle=[float(v) for v in r_res])
 
@@ -261,11 +293,31 @@ def run_system(args, cfg, mat, n, world, rank, local, comm, method, k, env=None)
                 history=out.info)
 
 
+METHOD_NAMES = {"cg": "CG", "mrr": "MrR", "kskipcg": "k-skip CG", "kskipmrr": "k-skip MrR",
+                "adaptivekskipmrr": "Adaptive k-skip MrR"}
+
+
+def workload_label(config, method, k, mat, n):
+    """The workload actually run (method, k, matrix, N), not the config's
+    default label: --n-side / --nz / --method / --k change it."""
+    m = METHOD_NAMES.get(method, method) + (f" k={k}" if "kskip" in method else "")
+    if mat[0] == "poisson":
+        side, dim = mat[1], mat[2]
+        pts = 5 if dim == 2 else 7
+        grid = f"{side}^{dim}" if len(mat) == 3 else f"{side}^{dim - 1} x {mat[3]} planes"
+        a = f"{dim}D {pts}-point Poisson {grid}"
+    else:
+        a = f"random banded CSR N={mat[1]}, {2 * mat[2] + 1} nnz/row (band {mat[3]})"
+    return f"{config}: {m} on {a} (N={n})"
+
+
 def kernel_table(stats, delta):
     """Per kernel: launches, average ms (HIP events on the solver's stream),
     GB/s on the stored format's bytes and on SURVEY.md 8(d)'s CSR bytes."""
     kernels, stored = {}, {}
     for s_ in stats:
+        if s_["name"].startswith("host_"):  # host-side timing (host_table)
+            continue
         if s_["launches"]:
             avg = s_["total_ms"] / s_["launches"]
             csr = s_["bytes_per_launch"]
@@ -276,6 +328,37 @@ def kernel_table(stats, delta):
                                        csr_gbs=round(csr / avg / 1e6, 1),
                                        total_ms=round(s_["total_ms"], 3))
     return kernels, stored
+
+
+def host_table(stats):
+    """Host time per outer iteration (every iteration, not sampled): enqueue =
+    the launch / copy / event calls the host thread issues, wait = blocked in
+    the sync point's device-to-host read (kr_solve_step, System::reduce)."""
+    out = {}
+    for s_ in stats:
+        if s_["name"].startswith("host_") and s_["launches"]:
+            out[s_["name"][5:] + "_ms_per_step"] = round(s_["total_ms"] / s_["launches"], 4)
+    return out or None
+
+
+def kernel_sampling(kernels, run, args):
+    """How the per-kernel table was measured, and its overhead: HIP events
+    around every kernel of every N-th outer iteration only; the event pairs
+    delay the launches they bracket, so the sampled steps run slower than the
+    unsampled ones (sum of per-kernel averages per step vs ms_per_step)."""
+    if not kernels:
+        return None
+    every = args.profile_every or PROFILE_EVERY.get(args.config, 4)
+    per_launch = {n_: v["total_ms"] / v["launches"] for n_, v in kernels.items()}
+    sampled_steps = max(1, -(-args.steps // every))
+    per_step = sum(v["total_ms"] for v in kernels.values()) / sampled_steps
+    step_ms = run["elapsed"] / args.steps * 1e3
+    return dict(every=every, sampled_steps=sampled_steps,
+                kernel_sum_ms_per_step=round(per_step, 4),
+                over_ms_per_step=round(per_step / step_ms - 1.0, 4),
+                note="kernel times are HIP events on the solver stream around every kernel of "
+                     "every N-th step; the sum per sampled step exceeds ms_per_step by the "
+                     "event pairs' launch gaps (not counted in value)")
 
 
 def dominant(kernels):
@@ -373,8 +456,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (CSR matrix and b = 2u-1 generated on device)",
-            "config": {"workload": f"{args.config}: {cfg['label']} (N={n}, "
-                                   f"nnz/shard={info['nnz']}), tol=0 fixed iterations",
+            "config": {"workload": workload_label(args.config, method, k, mat, n)
+                                   + f", nnz/shard={info['nnz']}, tol=0 fixed iterations",
                        "method": method, "k": k, "matrix": mat,
                        "step": f"one outer iteration = {per_step} solver iterations",
                        "parallelism": f"row-partitioned x{world}, RCCL halo + Gram all-gather"},
@@ -383,6 +466,8 @@ def main():
             "parity": parity,
             "csr": csr_rec,
             "kernels": kernels,
+            "kernel_sampling": kernel_sampling(kernels, run, args),
+            "host": host_table(run["stats"]),
             "residual_tail": [float(v) for v in run["history"]["residual"][-3:-1]],
         }
         print(json.dumps(rec))

@@ -49,7 +49,13 @@ extern "C" {
 #define KR_METHOD_GROPP 7
 #define KR_METHOD_PIPECG 8
 
-/* Library identification. */
+/* Library identification. kr_version() returns KR_ABI_VERSION; a binding
+ * checks it before it uses any struct below (INTEGRATION.md "ABI versions").
+ *   100  round 1
+ *   200  kr_solve_params gained nan_guard and kr_solve_result diverged (both
+ *        structs changed size); maxiter = 0 is honoured instead of meaning
+ *        the default (CG / k-skip CG return r0, the MrR family is refused). */
+#define KR_ABI_VERSION 200
 int kr_version(void);
 const char* kr_last_error(void);
 /* Number of HIP devices visible to this process (0 when none). */
@@ -270,6 +276,10 @@ int kr_system_shard_sched(kr_system* sys, int shard, int* grid, int* spmv_grid,
 #define KR_FORMAT_STENCIL 1 /* stencil codes (kr_stencil.h) */
 #define KR_FORMAT_DIA 2     /* diagonal-offset values (long masked rows) */
 #define KR_FORMAT_DENSE 3   /* dense row block (GEMV) */
+#define KR_FORMAT_DIA_WALK 4 /* symmetric diagonal-offset values, row-block walk with the
+                              mirrored lower entries in LDS (band <= 256 rows): workgroup
+                              g of spmv_grid owns the row blocks [g nb / G, (g+1) nb / G),
+                              block g when nb <= G */
 
 /* Halo exchange plan (pure host arithmetic, no device; test hook and the
  * planner kr_system_finalize uses). part[0..nshards] is the global row

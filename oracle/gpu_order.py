@@ -59,6 +59,7 @@ class ShardSched:
     int_lo: int = 0  # interior rows [int_lo, int_hi) of the split SpMV
     int_hi: int = 0
     stencil_walk: int = 0  # P > 0: the stencil SpMV (512-row blocks), 0: row walk
+    dia_walk: int = 0      # 1: the symmetric DIA walk (kr_spmv.h spmv_diawalk_kernel)
 
 
 def _stencil_walk(blk, r0, nnz_row_mean):
@@ -113,6 +114,52 @@ def stencil_grid(rows, P, zmax=0):
     return cols * Z
 
 
+DIA_WALK_H = (7, 13, 15, 31)  # kr_internal.h dia_walk_h_supported
+
+
+def dia_walk_grid(rows, nm, cus=256):
+    """kr_engine.cpp dia_walk_grid: the resident workgroups of the walk kernel
+    (LDS: h x 2 KiB of mirror buffers + two 6 KiB x windows + 1 KiB, 160 KiB per CU)."""
+    nrb = max(1, -(-rows // BLOCK))
+    lds = 8 * ((nm // 2 + 1) * BLOCK + 2 * 768) + 1024
+    h = nm // 2
+    by_regs = 2 if h >= 16 else 3 if h >= 8 else 4  # waves per SIMD by VGPRs
+    per_cu = max(1, min(by_regs, 160 * 1024 // lds))
+    return min(nrb, cus * per_cu)
+
+
+def _dia_walk(blk, r0, n):
+    """kr_engine.cpp build_masks: 0, or nm of a shard served by the symmetric
+    DIA walk -- diagonal-offset values (mean >= 12 nnz/row, <= 64 distinct
+    offsets), offsets symmetric around 0 with the mirrored values equal
+    (dia_symcheck over the shard's own rows), band <= 256, an upper-slot
+    count the kernel is compiled for (DIA_WALK_H)."""
+    if n == 0 or blk.nnz < 12.0 * n:
+        return 0
+    rows = np.repeat(np.arange(n), np.diff(blk.indptr))
+    offs = np.unique(blk.indices.astype(np.int64) - (r0 + rows))
+    nm = offs.size
+    if nm > 64 or nm % 2 == 0 or offs[nm // 2] != 0 or not np.array_equal(offs, -offs[::-1]):
+        return 0
+    if offs[-1] > 256 or nm // 2 not in DIA_WALK_H:
+        return 0
+    import scipy.sparse as sp
+    sq = sp.coo_matrix(blk[:, r0:r0 + n])  # entries whose column is one of the shard's rows
+    lo = sq.col < sq.row
+    up = sq.col > sq.row
+    # every stored lower entry (i, j) needs a stored mirror (j, i) with the same bits
+    lkey = sq.row[lo].astype(np.int64) * n + sq.col[lo]
+    ukey = sq.col[up].astype(np.int64) * n + sq.row[up]  # (j, i) keyed as (i, j)
+    order = np.argsort(ukey)
+    ukey, uval = ukey[order], sq.data[up][order]
+    pos = np.minimum(np.searchsorted(ukey, lkey), max(ukey.size - 1, 0))
+    if lkey.size and (ukey.size == 0 or not np.array_equal(ukey[pos], lkey) or
+                      not np.array_equal(uval[pos].view(np.uint64),
+                                         sq.data[lo].view(np.uint64))):
+        return 0
+    return nm
+
+
 def shard_scheds(A, part, cus: int = 256):
     """The launch geometry kr_system_finalize gives the row blocks part[s]..
     part[s+1] of A (kr_engine.cpp default_grid / spmv_grid_for /
@@ -139,7 +186,10 @@ def shard_scheds(A, part, cus: int = 256):
         nrb = max(1, -(-n // BLOCK))
         base = min(nrb, cap)
         P = _stencil_walk(blk, r0, blk.nnz / max(n, 1))
-        if P:
+        walk_nm = 0 if P else _dia_walk(blk, r0, n)
+        if walk_nm:
+            g = dia_walk_grid(n, walk_nm, cus)
+        elif P:
             int_lo = min(-(-int_lo // 512) * 512, n)
             int_hi = max(int_hi // 512 * 512, int_lo)
             g = stencil_grid(n, P)
@@ -152,7 +202,7 @@ def shard_scheds(A, part, cus: int = 256):
                 while g // 2 >= base and g > nrb // 16 and (g // 2) % 8 == 0:
                     g //= 2
         out.append(ShardSched(n=n, grid=base, spmv_grid=g, int_lo=int_lo, int_hi=int_hi,
-                              stencil_walk=P))
+                              stencil_walk=P, dia_walk=1 if walk_nm else 0))
     return out
 
 
@@ -174,6 +224,20 @@ def _visits(rows: int, grid: int, gap_at: int = 0, gap: int = 0):
             vis.append(r if r < gap_at else r + gap)
         out.append(vis)
     return out
+
+
+def _visits_dia_walk(rows: int, grid: int, gap_at: int = 0, gap: int = 0):
+    """Row blocks each workgroup of the symmetric DIA walk visits, in order
+    (kr_spmv.h spmv_diawalk_kernel: workgroup g owns the virtual blocks
+    [g nvb / G, (g+1) nvb / G) -- block g when nvb <= G -- physical = v, or
+    v + gap past the gap)."""
+    nvb = -(-rows // BLOCK) - gap
+
+    def run(g):
+        if nvb <= grid:  # workgroup g takes block g
+            return range(min(g, nvb), min(g + 1, nvb))
+        return range(g * nvb // grid, (g + 1) * nvb // grid)
+    return [[v if v < gap_at else v + gap for v in run(g)] for g in range(grid)]
 
 
 def _wave_tree(v):
@@ -231,7 +295,7 @@ def _visits_stencil(rows: int, grid: int, P: int, gap_at: int = 0, gap: int = 0)
     return out
 
 
-def _launch_partials(p, rows, grid, gap_at=0, gap=0, P=0):
+def _launch_partials(p, rows, grid, gap_at=0, gap=0, P=0, walk=0):
     """Per-workgroup partials of one SpMV launch over products p[0:rows]."""
     out = np.zeros(grid, np.float64)
     lanes = np.arange(BLOCK)
@@ -245,7 +309,8 @@ def _launch_partials(p, rows, grid, gap_at=0, gap=0, P=0):
                 acc[act] = acc[act] + p[lo[act] + 1]
             out[b] = _block_total(acc)
         return out
-    for b, vis in enumerate(_visits(rows, grid, gap_at, gap)):
+    visits = _visits_dia_walk if walk else _visits
+    for b, vis in enumerate(visits(rows, grid, gap_at, gap)):
         acc = np.zeros(BLOCK, np.float64)
         for rb in vis:
             r = rb * BLOCK + lanes
@@ -267,16 +332,17 @@ def finalize(partials):
 def spmv_shard_total(p, s: ShardSched, split: bool):
     """One shard's total of the epilogue products p (length s.n)."""
     P = s.stencil_walk
+    W = s.dia_walk
     if not split:
-        return finalize(_launch_partials(p, s.n, s.spmv_grid, P=P))
-    part = _launch_partials(p[s.int_lo:s.int_hi], s.int_hi - s.int_lo, s.spmv_grid, P=P)
+        return finalize(_launch_partials(p, s.n, s.spmv_grid, P=P, walk=W))
+    part = _launch_partials(p[s.int_lo:s.int_hi], s.int_hi - s.int_lo, s.spmv_grid, P=P, walk=W)
     rbs = 512 if P else BLOCK
     nb_lo = s.int_lo // rbs
     nb_gap = (s.int_hi - s.int_lo) // rbs
     nb_all = -(-s.n // rbs)
     if nb_all - nb_gap > 0:
         g = min(s.spmv_grid, nb_all - nb_gap)
-        bnd = _launch_partials(p, s.n, g, nb_lo, nb_gap, P=P)
+        bnd = _launch_partials(p, s.n, g, nb_lo, nb_gap, P=P, walk=W)
         part[:g] = part[:g] + bnd
     return finalize(part)
 

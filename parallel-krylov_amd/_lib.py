@@ -18,7 +18,10 @@ _lib = None
 KR_METHOD = {"cg": 0, "mrr": 1, "kskipcg": 2, "kskipmrr": 3, "adaptivekskipmrr": 4,
              # v1/threads/pipeline/*.py (include/krylov_amd.h KR_METHOD_PCG ..)
              "pcg": 5, "chronopoulos_gear": 6, "gropp": 7, "pipeline": 8}
-KR_FORMAT = {0: "csr", 1: "stencil", 2: "dia", 3: "dense"}  # kr_system_shard_sched
+# include/krylov_amd.h KR_ABI_VERSION: the struct layouts below (SolveParams,
+# SolveResult) are this version's; a library of another version is refused.
+KR_ABI_VERSION = 200
+KR_FORMAT = {0: "csr", 1: "stencil", 2: "dia", 3: "dense", 4: "dia_walk"}  # kr_system_shard_sched
 
 
 class KrylovError(RuntimeError):
@@ -131,6 +134,10 @@ def library() -> ctypes.CDLL:
             fn = getattr(lib, name)
             fn.argtypes = argtypes
             fn.restype = _RESTYPE.get(name, ctypes.c_int)
+        got = lib.kr_version()
+        if got != KR_ABI_VERSION:
+            raise RuntimeError(f"{path}: ABI version {got}, this binding needs {KR_ABI_VERSION} "
+                               "(rebuild the library: make -C parallel-krylov_amd/csrc)")
         _lib = lib
         return lib
 

@@ -59,7 +59,7 @@ using namespace kr;
 
 extern "C" {
 
-int kr_version(void) { return 100; }
+int kr_version(void) { return KR_ABI_VERSION; }
 
 const char* kr_last_error(void) { return g_last_error.c_str(); }
 
@@ -680,8 +680,10 @@ int kr_system_shard_sched(kr_system* sys, int shard, int* grid, int* spmv_grid,
     const Shard& s = sys->shards[shard];
     if (stencil_walk) *stencil_walk = s.scode ? s.st_P : 0;
     if (format)
-      *format = s.dense ? KR_FORMAT_DENSE : s.scode ? KR_FORMAT_STENCIL
-                                                     : s.dia ? KR_FORMAT_DIA : KR_FORMAT_CSR;
+      *format = s.dense ? KR_FORMAT_DENSE
+                : s.scode ? KR_FORMAT_STENCIL
+                : s.dia   ? (s.dia_walk ? KR_FORMAT_DIA_WALK : KR_FORMAT_DIA)
+                          : KR_FORMAT_CSR;
   });
 }
 
@@ -768,7 +770,16 @@ int kr_solve_step(kr_system* sys, int64_t max_outer, int* done) {
       // profile = N: per-kernel events on every N-th outer iteration only
       sys->prof_active = (sys->prof_tick++ % sys->profile_every) == 0;
       ss.hint = max_outer - c;
+      const double t0 = now_seconds(), w0 = sys->host_wait_s;
       ss.step_once();
+      if (sys->profile) {  // host side of every outer iteration (profiled or not)
+        const double wait = sys->host_wait_s - w0;
+        auto& st = sys->shards[0].stats;
+        st["host_enqueue"].launches += 1;
+        st["host_enqueue"].total_ms += (now_seconds() - t0 - wait) * 1e3;
+        st["host_wait"].launches += 1;
+        st["host_wait"].total_ms += wait * 1e3;
+      }
     }
     if (done) *done = ss.done ? 1 : 0;
   });

@@ -23,6 +23,20 @@ namespace {
 
 int g_grid_cap = 0;
 
+int cu_count() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, c = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        c > 0)
+      cus = c;
+    else
+      cus = 256;
+  }
+  return cus;
+}
+
 int grid_cap() {
   if (g_grid_cap == 0) {
     int dev = 0, cus = 0;
@@ -154,6 +168,27 @@ int spmv_grid_for(int64_t n, int64_t reach) {
   int64_t g = rb * 8;
   while (g / 2 >= base && g > nrb / 16 && (g / 2) % 8 == 0) g /= 2;
   return (int)g;
+}
+
+// Grid of the symmetric DIA walk (spmv_diawalk_kernel): as many workgroups as
+// are resident at once, which the LDS sets -- the mirror buffers (h x 2 KiB)
+// and the dual SpMV's two x windows (2 x 6 KiB), plus 1 KiB of static LDS
+// -- within 160 KiB per CU, and by registers: C5 (h = 31) 2 per CU, C3 (h = 13)
+// 3 per CU. Every
+// workgroup then walks one run of consecutive row blocks, all concurrently.
+// KR_DIAW_GRID overrides (A/B). oracle/gpu_order.py dia_walk_grid restates it.
+int dia_walk_grid(int64_t n, int nm) {
+  const int64_t nrb = std::max<int64_t>(1, (n + kBlock - 1) / kBlock);
+  const char* env = getenv("KR_DIAW_GRID");
+  if (env && atoi(env) > 0) return (int)std::min<int64_t>(atoi(env), nrb);
+  const int64_t lds = 8 * ((int64_t)(nm / 2 + 1) * kBlock + 2 * 768) + 1024;
+  // ... and the registers: the kernel holds 2 x (h + 1) values per lane (this
+  // block's and the next one's): 2 waves per SIMD for h = 31, 3 for 13 / 15,
+  // 4 for 7
+  const int h = nm / 2;
+  const int64_t by_regs = h >= 16 ? 2 : h >= 8 ? 3 : 4;
+  const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(by_regs, 160 * 1024 / lds));
+  return (int)std::min<int64_t>(nrb, (int64_t)cu_count() * per_cu);
 }
 
 void plan_halo(int P, const int64_t* part, const int64_t* need_lo, const int64_t* need_hi,
@@ -328,6 +363,13 @@ void System::build_masks(Shard& s) {
       KR_HIP_CHECK(hipFree(flag));
       s.dia_sym = h == 0 ? 1 : 0;
     }
+    // the row-block walk with the mirrors in LDS (spmv_diawalk_kernel): every
+    // mirror lies in this row block or the previous one (band <= 256 rows);
+    // KR_DIA_WALK=0 keeps the strided kernel (A/B)
+    const char* we = getenv("KR_DIA_WALK");
+    if (s.dia_sym && M[nm - 1] <= kDiaRows && dia_walk_h_supported(nm / 2) &&
+        !(we && atoi(we) == 0))
+      s.dia_walk = 1;
   }
   KR_HIP_CHECK(hipStreamSynchronize(s.stream));
   s.mask = mask;
@@ -683,8 +725,9 @@ void System::finalize() {
     // dense: one wave per row, 4 rows per workgroup
     s.spmv_grid = s.dense ? (int)std::max<int64_t>(1, std::min<int64_t>((s.n + 3) / 4,
                                                                          (int64_t)grid_cap() * 4))
-                  : s.scode ? stencil_grid(s.n, s.st_P)
-                            : spmv_grid_for(s.n, s.reach);
+                  : s.scode    ? stencil_grid(s.n, s.st_P)
+                  : s.dia_walk ? dia_walk_grid(s.n, s.nm)
+                               : spmv_grid_for(s.n, s.reach);
     // The products-only dual (a read-only stream: codes and two x vectors)
     // runs faster on fewer, longer walks: 512^3 0.69 -> 0.59 ms at Z <= 16
     // (16 or 8 alike, 32 is the general grid's). Smaller shards already have
@@ -1153,6 +1196,7 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
         a.dia_bs = s.dia_bs;
         a.dia_ks = s.dia_ks;
         a.dia_sym = s.dia_sym;
+        a.dia_walk = s.dia_walk;
         a.dia_wlen = s.dia_wlen;
         a.nseg = s.nseg;
         for (int g = 0; g < s.nseg; ++g) {
@@ -1524,7 +1568,9 @@ void System::scalar_state_read() {
   Shard& s = shards[0];
   KR_HIP_CHECK(hipMemcpyAsync(s.hst, s.st, sizeof(double) * kScalarState,
                               hipMemcpyDeviceToHost, s.stream));
+  const double w0 = now_seconds();
   KR_HIP_CHECK(hipStreamSynchronize(s.stream));
+  host_wait_s += now_seconds() - w0;
   size_t pend = s.pending.size();
   if (pend > 512) harvest_profile();
 }
@@ -1602,10 +1648,12 @@ std::vector<double> System::reduce(int nslots) {
     KR_HIP_CHECK(hipMemcpyAsync(hy_host, hy_recv, sizeof(double) * per * comm->nranks,
                                 hipMemcpyDeviceToHost, s0.stream));
   }
+  const double w0 = now_seconds();
   for (auto& s : shards) {
     KR_HIP_CHECK(hipSetDevice(s.dev));
     KR_HIP_CHECK(hipStreamSynchronize(s.stream));
   }
+  host_wait_s += now_seconds() - w0;
   // Fixed order: global shard 0, 1, ... (identical for in-process and RCCL).
   if (hybrid()) {
     const size_t per = (size_t)kMaxLocal * nslots;
@@ -1793,7 +1841,8 @@ class CgSession : public Base {
       sys->scalar_state_read();
       int err = 0;
       KR_HIP_CHECK(hipMemcpy(&err, pbar + 1, sizeof(int), hipMemcpyDeviceToHost));
-      if (err) throw Failure(KR_ERR_HIP, "persistent CG: a grid barrier timed out");
+      if (err) throw Failure(KR_ERR_HIP, "persistent CG: a grid barrier timed out "
+                                          "(x and r are undefined after this error)");
     }
     const double* h = sys->shards[0].hst;
     q.assign(h + ST_HIST, h + ST_HIST + m);

@@ -86,6 +86,7 @@ struct Shard {
   double* dia = nullptr;            // diagonal-offset values (SpmvArgs::dia), owned
   int64_t dia_bs = 0, dia_ks = 0;  // SpmvArgs::dia_bs / dia_ks
   int dia_sym = 0;                  // SpmvArgs::dia_sym
+  int dia_walk = 0;                 // SpmvArgs::dia_walk (spmv_grid = dia_walk_grid)
   int dia_wlen = 0, nseg = 0;       // SpmvArgs x window (dia_wlen, nseg, seg_*, woff)
   int seg_lo[4] = {}, seg_len[4] = {}, seg_base[4] = {};
   int32_t* woff = nullptr;
@@ -176,6 +177,10 @@ struct System {
   int profile_every = 1;            // events on every profile_every-th outer iteration
   int64_t prof_tick = 0;
   bool prof_active = true;
+  // host time blocked in the per-sync-point waits (reduce, scalar_state_read);
+  // kr_solve_step books the rest of each outer iteration's wall time as host
+  // enqueue ("host_enqueue" / "host_wait" in the kernel stats of shard 0)
+  double host_wait_s = 0.0;
   bool overlap = true;              // split SpMV: interior rows || halo exchange
   bool all_interior = false;        // every shard (all ranks) has interior rows
   bool fuse_steps = true;           // k-skip steps fused into the SpMV epilogue

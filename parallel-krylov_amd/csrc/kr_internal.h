@@ -126,6 +126,10 @@ struct SpmvArgs {
   // mirrored upper entry of row i - o, which the workgroup of that row block
   // streams at the same time (an L2 hit), instead of its own copy (HBM).
   int dia_sym = 0;
+  // 1: the row-block walk with the mirrors and an x ring in LDS
+  // (spmv_diawalk_kernel; symmetric shards with a band <= 256 rows). The
+  // grid (the launch's block count) fixes each workgroup's run of blocks.
+  int dia_walk = 0;
   // x window in LDS (spmv_dia_kernel): nseg segments, segment g = rows
   // row0 + seg_lo[g] .. + seg_len[g] - 1 of the row block at s_xw[seg_base[g]]
   // (starts and lengths even), dia_wlen doubles in all (0: gathers from global
@@ -454,5 +458,11 @@ void launch_cg_persist(const CgPersistArgs& a, int grid, hipStream_t s);
 int default_grid(int64_t n);
 // Workgroups of the SpMV kernels for a block of n rows with column reach `reach` rows.
 int spmv_grid_for(int64_t n, int64_t reach);
+// Workgroups of the symmetric DIA walk (spmv_diawalk_kernel) for n rows, nm offsets.
+int dia_walk_grid(int64_t n, int nm);
+// Upper-slot counts h (= nm / 2) the walk kernel is compiled for (its loops
+// over the offsets are straight-line code); other symmetric bands keep the
+// strided DIA kernel. C3 (27 offsets) h = 13, C5 (63) h = 31.
+constexpr bool dia_walk_h_supported(int h) { return h == 7 || h == 13 || h == 15 || h == 31; }
 
 }  // namespace kr

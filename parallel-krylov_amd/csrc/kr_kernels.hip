@@ -1022,7 +1022,12 @@ void launch_ew(EwOp op, const EwArgs& a, hipStream_t s) {
 // that exceeds ~1 s sets *err and gives up, so the grid always drains.
 namespace {
 
-__device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned target, int* err) {
+// Returns false once any workgroup has timed out (*err set): the caller
+// returns at once, so after one stuck barrier every workgroup leaves at its
+// next barrier instead of spinning out its own timeout on every later one.
+// x and r are then undefined (the host raises; kr_solve_* reports the error).
+__device__ __forceinline__ bool grid_barrier(unsigned* bar, unsigned target, int* err) {
+  __shared__ int s_fail;
   __syncthreads();
   if (threadIdx.x == 0) {
     // release once (write back this XCD's dirty L2 lines), arrive, poll with
@@ -1030,17 +1035,22 @@ __device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned target, int
     // invalidating it on every poll), then acquire once
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int fail = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned spins = 0;
-    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    while (!fail && __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(1);
       if (++spins > (1u << 25)) {
-        *err = 1;
-        break;
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fail = 1;
+      } else if ((spins & 255u) == 0) {  // another workgroup gave up
+        fail = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    s_fail = fail;
   }
   __syncthreads();
+  return s_fail == 0;
 }
 
 template <typename RP>
@@ -1080,7 +1090,7 @@ __global__ __launch_bounds__(kBlock) void cg_persist_kernel(CgPersistArgs a) {
     }
     block_reduce_store<1>(acc, a.part, G, s_red);
     target += G;
-    grid_barrier(a.bar, target, a.err);
+    if (!grid_barrier(a.bar, target, a.err)) return;
     const double sigma = 0.0 + slot_sum(a.part, G, s_red);
     const double alpha = gamma / sigma;
     if (j > 0) {
@@ -1101,7 +1111,7 @@ __global__ __launch_bounds__(kBlock) void cg_persist_kernel(CgPersistArgs a) {
     }
     block_reduce_store<1>(acc, a.part + G, G, s_red);
     target += G;
-    grid_barrier(a.bar, target, a.err);
+    if (!grid_barrier(a.bar, target, a.err)) return;
     const double gnew = 0.0 + slot_sum(a.part + G, G, s_red);
     beta = gnew / gamma;
     gamma = gnew;

@@ -1881,9 +1881,266 @@ void spmv_dia_launch_xl(const SpmvArgs& a, int nblocks, hipStream_t s) {
 }
 
 template <int E>
+void spmv_diawalk_launch(const SpmvArgs& a, int nblocks, hipStream_t s);
+
+template <int E>
 void spmv_dia_launch(const SpmvArgs& a, int nblocks, hipStream_t s) {
+  if (a.dia_walk) return spmv_diawalk_launch<E>(a, nblocks, s);
   if (a.dia_wlen > 0) return spmv_dia_launch_xl<E, true>(a, nblocks, s);
   spmv_dia_launch_xl<E, false>(a, nblocks, s);
+}
+
+// ---------------------------------------------------------------------------
+// Symmetric diagonal-offset SpMV as a row-block WALK (SpmvArgs::dia_walk:
+// shards whose values are symmetric, dia_sym, and whose band is at most one
+// row block wide, M[nm-1] <= 256: the banded systems C3 and C5).
+//
+// Workgroup g owns the consecutive virtual row blocks [g nvb / G, (g+1) nvb / G)
+// (block g when nvb <= G) and walks them in order, one lane per row, rows
+// summed in stored order from 0.0 (bitwise scipy, as every SpMV here). Only
+// the diagonal and upper values are streamed from HBM (one non-temporal pass,
+// 8 (h+1) bytes per row). The lower entry of row l at offset -o is the upper
+// entry of row l - o (bitwise equal, dia_symcheck at finalize), which lies in
+// this row block or the previous one, and both are in LDS, PRE-SHIFTED so
+// that row l reads position l: lower slot k (offset -o, o = M[nm-1-k]) has a
+// buffer s_low[k][256] in which the lane of row p stores its upper value of
+// offset o at position (p + o) & 255 -- before the sums when p + o < 256
+// (the reader is row p + o of this block), after them otherwise (the reader
+// is row p + o - 256 of the next block). A segment start (or the boundary
+// launch's gap) stores instead the block's OWN lower values (the same
+// numbers) at positions l < o. The read is then one ds_read_b64 at the lane's
+// own address with a compile-time offset: no index arithmetic per entry.
+// x rows: a window of 768 rows per vector, rows rb0 - 256 .. rb0 + 511
+// (band <= 256), shifted by one block per step inside each lane's own slots
+// (lane t: win[t] <- win[t+256] <- win[t+512] <- the new row, loaded one block
+// ahead), so the shift needs no barrier. One block ahead too: every lane's
+// diagonal + upper values, its mask and its epilogue operands, so the next
+// block's HBM stream is in flight while this block is summed.
+// Rows whose mask is full in the whole workgroup (every block of a band
+// matrix but its first and last) take a path without the absent-entry
+// selects.
+// LDS: 8 (256 h + 768 NV) bytes; the grid is the resident workgroup count
+// (Shard::spmv_grid, dia_walk_grid). Round 2 read the mirrors from global
+// memory (an L2 hit only when the neighbouring workgroup happened to stream
+// them at the same moment): C5's dual moved 21.4 GB per launch against the
+// 14.4 GB it must stream. First versions of this kernel were issue-bound
+// (a scalar load per entry drains every LDS read in flight; wrapped ring
+// indices cost 3 VALU per entry).
+// ---------------------------------------------------------------------------
+constexpr int kWalkWin = 768;  // x window, rows per vector (band <= 256)
+
+// NH = h, the number of upper (= lower) offsets, is a template parameter:
+// every loop over the offsets is then straight-line code, so the compiler
+// keeps up to 15 LDS reads in flight instead of waiting after each one
+// behind a run-time bound (the runtime-h version ran at 3 TB/s on C5).
+// (2 workgroups per CU for NH > 15: at most 256 VGPRs; the LDS allows no
+// more anyway)
+template <int EPI, int NH>
+__global__ __launch_bounds__(kBlock, NH > 15 ? 2 : 1) void spmv_diawalk_kernel(SpmvArgs a) {
+  if (!spmv_entry<EPI>(a)) return;  // converged / the fused scalar step's test fired
+  using T = EpiTraits<EPI>;
+  constexpr int NP = T::NP;
+  constexpr int NV = T::NV;
+  constexpr bool VIRT = is_virtual<EPI>();
+  constexpr int NM = 2 * NH + 1;
+  constexpr int MW = NM <= 8 ? 8 : NM <= 16 ? 16 : NM <= 32 ? 32 : 64;
+  using MT = typename MaskType<MW>::type;
+  using W = typename std::conditional<(MW > 32), uint64_t, uint32_t>::type;
+  constexpr W kFull = NM >= 64 ? ~(W)0 : (((W)1 << NM) - 1);
+  __shared__ double s_red[(NP > 0 ? NP : 1) * 4];
+  __shared__ int s_full[4];
+  extern __shared__ __attribute__((aligned(16))) double s_dyn[];
+  double* s_win = s_dyn;                          // NV x kWalkWin
+  double* s_low = s_dyn + NV * kWalkWin;          // NH x kBlock, lower slot k at k * kBlock
+  double* s_junk = s_low + NH * kBlock;           // kBlock: stores of lanes with nothing to store
+  const MT* __restrict__ mask = static_cast<const MT*>(a.mask);
+  const int tid = threadIdx.x;
+  // The offset table, one entry per lane (lane k: M[k]); offset k is then a
+  // readlane (VALU) -- no scalar memory load inside the block loop: an SMEM
+  // result needs lgkmcnt(0), which would also drain every LDS read in flight.
+  const int mlane = load_uniform(a.moff, min(tid & 63, NM - 1));
+  auto moff = [&](int k) { return __builtin_amdgcn_readlane(mlane, k); };
+  double acc[NP > 0 ? NP : 1];
+#pragma unroll
+  for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;
+
+  const int64_t nvb = (a.n + kBlock - 1) / kBlock - a.rb_gap;
+  const int64_t G = gridDim.x;
+  // runs of consecutive blocks; with no more blocks than workgroups,
+  // workgroup g takes block g (the strided kernels' assignment there)
+  const int64_t gb = blockIdx.x;
+  const int64_t v0 = nvb <= G ? min(gb, nvb) : gb * nvb / G;
+  const int64_t v1 = nvb <= G ? min(gb + 1, nvb) : (gb + 1) * nvb / G;
+  auto phys = [&](int64_t v) { return v < a.rb_gap_at ? v : v + a.rb_gap; };
+  auto xload = [&](const double* __restrict__ x, int64_t xi) {
+    return x[min(max(xi, (int64_t)0), a.xlen - 1)];
+  };
+  auto xform = [&](double r1, double r2, double r3) {  // the window value of vector 0
+    if constexpr (VIRT)
+      return virt_in<EPI>(a, r1, r2, r3);
+    else
+      return r1;
+  };
+  // store v at s_low[slot][pos] when ok, else at the lane's junk slot (no branch)
+  auto low_put = [&](bool ok, int slot, int pos, double v) {
+    double* d = ok ? s_low + slot * kBlock + pos : s_junk + tid;
+    *d = v;
+  };
+
+  // one block ahead: values (diagonal + upper), mask, epilogue operands, the
+  // window's new rows (raw loads; a virtual input is formed when stored)
+  double upn[NH + 1];
+  W mn = 0;
+  EpiIn pinn;
+  double xr1 = 0.0, xr2 = 0.0, xr3 = 0.0;
+  auto prefetch = [&](int64_t bb) {
+    const int64_t rowb = bb * kBlock + tid;
+    const bool act = rowb < a.n;
+    const int64_t rrb = act ? rowb : a.n - 1;
+    mn = act ? (W)mask[rrb] : (W)0;
+    const double* blk = a.dia + bb * a.dia_bs + tid;
+#pragma unroll
+    for (int u = 0; u <= NH; ++u)
+      upn[u] = __builtin_nontemporal_load(blk + (int64_t)(NH + u) * a.dia_ks);
+    pinn = epi_load<EPI>(a, rrb);
+    const int64_t xi = a.xoff + bb * kBlock + kBlock + tid;
+    xr1 = xload(a.x1, xi);
+    if constexpr (NV == 2 || VIRT) xr2 = xload(a.x2, xi);
+    if constexpr (VIRT && EPI != EPI_XY_VP) xr3 = xload(a.x3, xi);
+  };
+
+  double up[NH + 1];
+#pragma unroll
+  for (int u = 0; u <= NH; ++u) up[u] = 0.0;
+  if (v0 < v1) prefetch(phys(v0));
+  int64_t prev = -2;
+  for (int64_t v = v0; v < v1; ++v) {
+    const int64_t b = phys(v);
+    const bool start = b != prev + 1;  // uniform
+    // --- the previous block's tails (its rows p + o >= 256 feed this block)
+    if (!start) {
+#pragma unroll
+      for (int u = 1; u <= NH; ++u) {
+        const int o = moff(NH + u);
+        low_put(tid + o >= kBlock, NH - u, tid + o - kBlock, up[u]);
+      }
+    }
+    prev = b;
+#pragma unroll
+    for (int u = 0; u <= NH; ++u) up[u] = upn[u];
+    const W m = mn;
+    const EpiIn pin = pinn;
+    const double c1 = xr1, c2 = xr2, c3 = xr3;
+    // the next block's loads (the last block re-reads itself: no branch, so
+    // nothing below waits for them)
+    prefetch(phys(min(v + 1, v1 - 1)));
+    const int64_t rb0 = b * kBlock;
+    const int64_t row = rb0 + tid;
+    const bool active = row < a.n;
+    // --- the x window and this block's heads
+    if (start) {
+      for (int t = tid; t < kWalkWin; t += kBlock) {  // rows rb0 - 256 + t
+        const int64_t xi = a.xoff + rb0 - kBlock + t;
+        double r1 = xload(a.x1, xi), r2 = 0.0, r3 = 0.0;
+        if constexpr (NV == 2 || VIRT) r2 = xload(a.x2, xi);
+        if constexpr (VIRT && EPI != EPI_XY_VP) r3 = xload(a.x3, xi);
+        s_win[t] = xform(r1, r2, r3);
+        if constexpr (NV == 2) s_win[kWalkWin + t] = r2;
+      }
+      // positions l < o: the block's own lower values (all loads, then the stores)
+      const double* blk = a.dia + b * a.dia_bs + tid;
+      double lw[NH];
+#pragma unroll
+      for (int k = 0; k < NH; ++k) lw[k] = blk[(int64_t)k * a.dia_ks];
+#pragma unroll
+      for (int k = 0; k < NH; ++k) low_put(tid < -moff(k), k, tid, lw[k]);
+    } else {  // shift by one block inside the lane's own slots, append the new row
+#pragma unroll
+      for (int vv = 0; vv < NV; ++vv) {
+        double* w = s_win + vv * kWalkWin + tid;
+        const double w1 = w[kBlock], w2 = w[2 * kBlock];
+        w[0] = w1;
+        w[kBlock] = w2;
+      }
+      s_win[2 * kBlock + tid] = xform(c1, c2, c3);
+      if constexpr (NV == 2) s_win[kWalkWin + 2 * kBlock + tid] = c2;
+    }
+#pragma unroll
+    for (int u = 1; u <= NH; ++u) {  // heads: rows p + o < 256 of this block
+      const int o = moff(NH + u);
+      low_put(tid + o < kBlock, NH - u, tid + o, up[u]);
+    }
+    const bool lane_full = active && m == kFull;
+    const uint64_t all = __ballot(lane_full);
+    if ((tid & 63) == 0) s_full[tid >> 6] = all == ~0ull ? 1 : 0;
+    __syncthreads();
+    const bool full = (s_full[0] & s_full[1] & s_full[2] & s_full[3]) != 0;  // uniform
+    // --- the row sums: lower entries (mirrors from LDS), diagonal, upper
+    double sum1 = 0.0, sum2 = 0.0;
+    const double* wl = s_win + kBlock + tid;  // the row's x: wl[offset]
+    const double* ll = s_low + tid;           // lower slot k: ll[k * kBlock]
+    if (full) {
+#pragma unroll
+      for (int k = 0; k < NH; ++k) {
+        const double* w = wl + moff(k);
+        const double v = ll[k * kBlock];
+        sum1 = sum1 + v * w[0];
+        if constexpr (NV == 2) sum2 = sum2 + v * w[kWalkWin];
+      }
+#pragma unroll
+      for (int u = 0; u <= NH; ++u) {
+        const double* w = wl + moff(NH + u);
+        sum1 = sum1 + up[u] * w[0];
+        if constexpr (NV == 2) sum2 = sum2 + up[u] * w[kWalkWin];
+      }
+    } else {  // absent entries skipped by a select, as every kernel here
+      auto add = [&](int k, double v) {
+        const bool ok = ((m >> k) & 1) != 0;
+        const double* w = wl + moff(k);
+        const double t1 = sum1 + v * w[0];
+        sum1 = ok ? t1 : sum1;
+        if constexpr (NV == 2) {
+          const double t2 = sum2 + v * w[kWalkWin];
+          sum2 = ok ? t2 : sum2;
+        }
+      };
+#pragma unroll
+      for (int k = 0; k < NH; ++k) add(k, ll[k * kBlock]);
+#pragma unroll
+      for (int u = 0; u <= NH; ++u) add(NH + u, up[u]);
+    }
+    if (active) epi_row_in<EPI>(a, row, sum1, sum2, a.x1, a.x2, pin, acc);
+    __syncthreads();
+  }
+  __syncthreads();
+  block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
+}
+
+// LDS of the walk kernel (dia_walk_grid on the host): the mirror buffers, the
+// junk slots and the x windows of the epilogue's vectors
+template <int E, int NH>
+void spmv_diawalk_launch_t(const SpmvArgs& a, int nblocks, hipStream_t s) {
+  constexpr int nv = EpiTraits<E>::NV;
+  const size_t lds = sizeof(double) * ((size_t)(NH + 1) * kBlock + (size_t)nv * kWalkWin);
+  static size_t opted = 64 * 1024;  // dynamic LDS beyond 64 KiB is opted into per kernel
+  if (lds > opted) {
+    KR_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(spmv_diawalk_kernel<E, NH>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    opted = lds;
+  }
+  spmv_diawalk_kernel<E, NH><<<nblocks, kBlock, lds, s>>>(a);
+}
+
+template <int E>
+void spmv_diawalk_launch(const SpmvArgs& a, int nblocks, hipStream_t s) {
+  KR_REQUIRE(a.dia_sym && a.nm % 2 == 1 && dia_walk_h_supported(a.nm / 2),
+             "walk SpMV: symmetric offsets with a compiled upper-slot count");
+  switch (a.nm / 2) {
+    case 7: return spmv_diawalk_launch_t<E, 7>(a, nblocks, s);
+    case 13: return spmv_diawalk_launch_t<E, 13>(a, nblocks, s);
+    case 15: return spmv_diawalk_launch_t<E, 15>(a, nblocks, s);
+    default: return spmv_diawalk_launch_t<E, 31>(a, nblocks, s);
+  }
 }
 
 // Which kernel serves a shard that has diagonal-offset values (long rows by

@@ -131,7 +131,28 @@ def gpu_ids_range():
     ids = [int(t) for t in env.split(",") if t.strip() != ""]
     if not ids or ids[-1] < ids[0]:
         raise ValueError(f"GPU_IDS={env!r}: expected 'first,...,last' with last >= first")
+    _warn_gpu_ids_over_local_rank(env)
     return list(range(ids[0], ids[-1] + 1))
+
+
+_warned_gpu_ids = False
+
+
+def _warn_gpu_ids_over_local_rank(env):
+    """GPU_IDS takes precedence over LOCAL_RANK (the reference's launcher
+    sets GPU_IDS per process). Under torchrun with several ranks a GPU_IDS
+    exported for the whole job would put every rank on the same GPU(s):
+    say so once, loudly, instead of silently stacking the ranks."""
+    global _warned_gpu_ids
+    if _warned_gpu_ids or int(os.environ.get("WORLD_SIZE", "1")) <= 1 \
+            or "LOCAL_RANK" not in os.environ:
+        return
+    _warned_gpu_ids = True
+    import warnings
+    warnings.warn(f"GPU_IDS={env!r} overrides LOCAL_RANK={os.environ['LOCAL_RANK']} with "
+                  f"WORLD_SIZE={os.environ['WORLD_SIZE']}: every rank whose environment holds "
+                  "this GPU_IDS runs on these GPUs (set it per rank, or unset it to place "
+                  "ranks by LOCAL_RANK)", RuntimeWarning, stacklevel=3)
 
 
 def local_device(rank: int) -> int:
@@ -301,11 +322,13 @@ class KrylovSystem:
         lay = self.shard_layout(s)
         return dict(n=self.row_begin[s + 1] - self.row_begin[s], grid=g.value,
                     spmv_grid=sg.value, int_lo=lay["interior_lo"], int_hi=lay["interior_hi"],
-                    stencil_walk=sw.value)
+                    stencil_walk=sw.value,
+                    dia_walk=1 if _lib.KR_FORMAT[fm.value] == "dia_walk" else 0)
 
     def shard_format(self, s: int) -> str:
         """The SpMV kernel family serving shard s: "csr" (row walk), "stencil",
-        "dia" (diagonal-offset values) or "dense" (GEMV)."""
+        "dia" (diagonal-offset values), "dia_walk" (symmetric diagonal-offset
+        values, row-block walk with the mirrors in LDS) or "dense" (GEMV)."""
         fm = ctypes.c_int()
         call("kr_system_shard_sched", self.handle, s, None, None, None, ctypes.byref(fm))
         return _lib.KR_FORMAT[fm.value]

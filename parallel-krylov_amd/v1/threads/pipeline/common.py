@@ -35,8 +35,8 @@ class Jacobi:
                 raise ValueError("Jacobi needs A or d")
             d = A.diagonal() if hasattr(A, "diagonal") else np.diag(np.asarray(A))
         self.d = np.ascontiguousarray(np.asarray(d, dtype=np.float64))
-        if not np.all(self.d != 0.0):
-            raise ValueError("Jacobi: zero on the diagonal")
+        if not np.all(np.isfinite(self.d) & (self.d != 0.0)):
+            raise ValueError("Jacobi: zero or non-finite entry on the diagonal")
 
     def solve(self, v):
         return v / self.d
@@ -54,9 +54,14 @@ def _diagonal(ilu, N):
         pass
     if isinstance(d, (np.ndarray, list, tuple)):
         d = np.ascontiguousarray(np.asarray(d, dtype=np.float64))
-        if d.ndim == 1 and d.size == N:
-            return d
-        raise ValueError(f"ilu: a diagonal of {N} values is required, got shape {d.shape}")
+        if d.ndim != 1 or d.size != N:
+            raise ValueError(f"ilu: a diagonal of {N} values is required, got shape {d.shape}")
+        # the same check as Jacobi(): u = r / d must stay finite on the device
+        bad = ~np.isfinite(d) | (d == 0.0)
+        if bad.any():
+            raise ValueError(f"ilu: the diagonal has {int(bad.sum())} zero or non-finite "
+                             f"entries (first at row {int(np.argmax(bad))})")
+        return d
     raise TypeError(
         f"ilu={type(ilu).__name__}: the device path takes a diagonal (Jacobi) preconditioner "
         "-- None, Jacobi(A) or the diagonal as a 1-D array; triangular ILU solves "

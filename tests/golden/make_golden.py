@@ -81,6 +81,11 @@ case("band3000w256_kskipmrr_k4", BAND5, "kskipmrr", k=4)
 case("band3000w256_mrr", BAND5, "mrr")
 case("band3000w256_adaptivekskipmrr_k12", BAND5, "adaptivekskipmrr", k=12)
 case("p2d16_adaptivekskipmrr_k12", P2D16, "adaptivekskipmrr", k=12)
+# Round 3. C1 itself (BASELINE.json configs[0]: CG on 2-D 5-point Poisson
+# 256^2 to tol 1e-10, ~880 iterations), so the GPU's C1 run is pinned against
+# the reference's own history and x (tests/test_gpu_solvers.py picks every
+# manifest case up).
+case("p2d256_cg", ["poisson", 256, 2], "cg")
 
 
 def build_matrix(spec):

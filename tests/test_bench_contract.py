@@ -22,8 +22,11 @@ def test_headline_metric_is_baselines():
 def test_cpu_baseline_object_small_sample():
     import bench
     rec = bench.cpu_baseline(12, 4, "kskipmrr")
-    assert set(rec) == {"value", "unit", "cores", "kind", "sample"}
+    assert set(rec) >= {"value", "unit", "cores", "kind", "sample", "cpu_model",
+                        "affinity_cores", "blas_threads"}
     assert rec["kind"] == "port" and rec["unit"] == "iterations/s"
+    assert rec["cpu_model"] and rec["affinity_cores"] >= 1
+    assert "2 outer" in rec["sample"]  # initial step + 2 outer iterations
     assert rec["value"] > 0 and rec["cores"] >= 1
     assert "scaled" in rec["sample"]  # a 12^3 sample is scaled to 512^3 by rows
 
@@ -55,6 +58,10 @@ def test_history_parity_contract():
     gpu["residual"][2] = 0.25
     gpu["nosl"][2] = 5
     assert not bench.history_parity(gpu, ref)["ok"]
+    # a GPU history shorter than the oracle's: ok false with both lengths, no raise
+    short = {"nosl": np.array([0, 1]), "residual": np.array([1.0, 0.5])}
+    p = bench.history_parity(short, ref)
+    assert not p["ok"] and p["entries"] == 2 and p["oracle_entries"] == 3
 
 
 def test_stored_format_bytes():

@@ -221,3 +221,21 @@ def test_local_device_gpu_ids_wins_over_local_rank(monkeypatch):
     assert system.local_device(0) == 1
     monkeypatch.delenv("LOCAL_RANK")
     assert system.local_device(10) == 2
+
+
+def test_job_wide_gpu_ids_warns_under_torchrun(monkeypatch):
+    """A GPU_IDS next to LOCAL_RANK with WORLD_SIZE > 1 (a job-wide export
+    under torchrun would stack every rank on the same GPUs) warns once."""
+    from parallel_krylov_amd import system
+    monkeypatch.setattr(system, "_warned_gpu_ids", False)
+    monkeypatch.setenv("LOCAL_RANK", "1")
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("GPU_IDS", "0,1")
+    with pytest.warns(RuntimeWarning, match="overrides LOCAL_RANK"):
+        assert system.gpu_ids_range() == [0, 1]
+    monkeypatch.setattr(system, "_warned_gpu_ids", False)
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        assert system.gpu_ids_range() == [0, 1]  # one rank: nothing to warn about

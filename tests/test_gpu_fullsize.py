@@ -75,3 +75,52 @@ def test_c5_fullsize_true_residual():
     assert rep < out.info["residual"][0]
     assert abs(true_rel - rep) <= 1e-9 * rep
     sysm.close()
+
+
+def _c4_history(parts, maxiter, k=4):
+    """k-skip MrR k=4 on the 512^3 headline system as `parts` in-process
+    shards of one device (parts = 8: C4's own row partition, one 64-plane
+    slab per shard, one 512^2 halo plane per neighbour, shard partials summed
+    in shard order -- the layout of the 8-GPU run)."""
+    import torch
+    from parallel_krylov_amd.system import KrylovSystem, balanced_partition
+    n = 512 ** 3
+    sysm = KrylovSystem(n, balanced_partition(n, parts), [0] * parts)
+    try:
+        sysm.gen_poisson(512, 3)
+        sysm.finalize()
+        b = sysm.rhs(1)
+        out = sysm.solve("kskipmrr", b, tol=0.0, maxiter=maxiter, k=k)
+        del b
+    finally:
+        sysm.close()
+        torch.cuda.empty_cache()
+    return out.info
+
+
+@pytest.mark.timeout(900)
+def test_c4_fullsize_partitions_match_oracle():
+    """C4 at full size in its own 8-way partition (BASELINE.json configs[3]).
+
+    * 1 shard and 8 shards: nosl identical, every entry of 3 outer iterations
+      (res >= 1e-8 throughout) within 1e-12 relative of each other -- the
+      only difference is the dot summation order (shard partials);
+    * both against the oracle (oracle.v3cpu = the reference's v3/cpu on the
+      SAME b, x0 = 0) over its 2 outer iterations (4 history entries): nosl
+      identical, entries within 1e-12 relative (k-skip MrR
+      entries with res >= 1e-8)."""
+    import bench
+    k, outer = 4, 3
+    maxiter = 1 + outer * (k + 1)
+    h1 = _c4_history(1, maxiter)
+    h8 = _c4_history(8, maxiter)
+    assert list(h1["nosl"]) == [0, 1, 6, 11, 16] and list(h8["nosl"]) == list(h1["nosl"])
+    r1, r8 = np.asarray(h1["residual"]), np.asarray(h8["residual"])
+    assert np.all(r1 >= 1e-8)
+    rel = np.abs(r8 - r1) / r1
+    assert rel.max() <= 1e-12, rel
+    _, ref = bench.cpu_baseline(512, k, "kskipmrr", return_info=True, outer=2)
+    assert list(ref["nosl"]) == [0, 1, 6, 11]
+    for h in (h1, h8):
+        p = bench.history_parity(h, ref)
+        assert p["ok"] and p["entries"] == 4, p

@@ -536,14 +536,24 @@ def test_value_dictionary_spmv_bitwise(torch_dev, monkeypatch, name, shards):
         sysm.close()
 
 
+@pytest.mark.parametrize("grid", ["auto", "1", "2", "5"])
 @pytest.mark.parametrize("shards", [1, 3])
-@pytest.mark.parametrize("spec", [["banded", 3001, 13, 64, 0], ["banded", 2000, 31, 256, 0]])
-def test_dia_symmetric_values_read_mirrored(torch_dev, monkeypatch, spec, shards):
+@pytest.mark.parametrize("spec", [["banded", 3001, 13, 64, 0], ["banded", 2000, 31, 256, 0],
+                                  ["banded", 4100, 7, 256, 3]])
+def test_dia_symmetric_values_read_mirrored(torch_dev, monkeypatch, spec, shards, grid):
     """Symmetric banded values: the DIA SpMV reads every lower entry as the
     mirrored upper entry of an earlier row (kr_system_shard_dia_sym = 1) and
     stays bitwise scipy's; one perturbed value (pattern still symmetric)
-    turns it off for the shard holding it, and KR_DIA_SYM=0 everywhere."""
+    turns it off for the shard holding it, and KR_DIA_SYM=0 everywhere.
+    With symmetric values and a band <= 256 the shard runs the row-block walk
+    (format "dia_walk": mirrors from the LDS copy of this and the previous
+    row block). KR_DIAW_GRID = 1, 2, 5 force long runs of blocks per
+    workgroup at these sizes (the default grid gives every workgroup one
+    block here), so the previous block's tails, segment starts and uneven
+    runs are all exercised."""
     from parallel_krylov_amd.system import KrylovSystem, balanced_partition
+    if grid != "auto":
+        monkeypatch.setenv("KR_DIAW_GRID", grid)
     A = golden_matrix(spec).tocsr()
     n = A.shape[0]
     B = A.copy()
@@ -559,8 +569,13 @@ def test_dia_symmetric_values_read_mirrored(torch_dev, monkeypatch, spec, shards
         try:
             sysm.set_matrix(M)
             sysm.finalize()
-            assert [sysm.shard_format(s) for s in range(shards)] == ["dia"] * shards
+            assert [sysm.shard_format(s) for s in range(shards)] == \
+                ["dia_walk" if w else "dia" for w in want]
             assert [sysm.shard_layout(s)["dia_sym"] for s in range(shards)] == want
+            if grid != "auto":  # (capped at the shard's row blocks)
+                assert all(sysm.shard_sched(s)["spmv_grid"] ==
+                           min(int(grid), -(-sysm.shard_sched(s)["n"] // 256))
+                           for s in range(shards) if want[s])
             y = sysm.gather(sysm.spmv(sysm.split(x)))
             np.testing.assert_array_equal(y.cpu().numpy(), M.dot(x))
         finally:

@@ -208,6 +208,57 @@ def test_gpu_mpi_family_bitwise_equals_gpu_order_oracle(dist_single, spec):
     assert np.any(np.diff(info["khistory"]) != 0)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("grid", ["2", "5"])
+@pytest.mark.parametrize("method,k", [("kskipmrr", 4), ("adaptivekskipmrr", 12), ("kskipcg", 4)])
+def test_dia_walk_long_runs_bitwise_gpu_order(monkeypatch, grid, method, k):
+    """The symmetric DIA walk (spmv_diawalk_kernel) with long runs of row
+    blocks per workgroup (KR_DIAW_GRID; the default grid gives each workgroup
+    one block of this 3000-row C5-family matrix): every epilogue the k-skip
+    methods use (head, dual + Gram, fused steps, fused first two steps) is
+    bitwise the GPU-order oracle summed over the engine's walk geometry."""
+    monkeypatch.setenv("KR_DIAW_GRID", grid)
+    A = golden_matrix(["banded", 3000, 31, 256, 0])
+    b = _rhs(A.shape[0])
+    sc = _engine_scheds(A, 1)
+    assert sc[0].dia_walk == 1 and sc[0].spmv_grid == int(grid)
+    kw = dict(tol=1e-10, k=k)
+    with contextlib.redirect_stdout(io.StringIO()):
+        x, info = _solver(method)(A, b, **kw)
+    x_ref, info_ref = gpu_order.run(method, A, b, sc, **kw)
+    _assert_bitwise(x, info, x_ref, info_ref)
+
+
+def test_dia_walk_visits_partition_blocks():
+    """Walk geometry: every (virtual) row block visited once, in ascending
+    runs, split evenly; the boundary launch's gap skipped."""
+    for rows, grid, gap_at, gap in [(3000, 12, 0, 0), (3000, 5, 0, 0), (100000, 7, 0, 0),
+                                    (3000, 3, 2, 7), (5000, 20, 1, 17)]:
+        vis = gpu_order._visits_dia_walk(rows, grid, gap_at, gap)
+        nrb = -(-rows // 256)
+        flat = [v for run in vis for v in run]
+        want = [v for v in range(nrb) if v < gap_at or v >= gap_at + gap]
+        assert flat == want
+        lens = [len(r) for r in vis]
+        assert max(lens) - min(lens) <= 1
+
+
+def test_dia_walk_detection():
+    """shard_scheds marks the symmetric banded shards (band <= 256, <= 31
+    upper slots) as walk shards with the resident-workgroup grid, and leaves
+    stencils, short rows and perturbed values alone."""
+    A = golden_matrix(["banded", 3000, 31, 256, 0])
+    assert [s.dia_walk for s in gpu_order.shard_scheds(A, [0, 3000])] == [1]
+    big = gpu_order.dia_walk_grid(10_000_000, 27)  # C3: h = 13 -> 3 per CU
+    assert big == 768 and gpu_order.dia_walk_grid(50_000_000, 63) == 512  # C5: 2 per CU
+    B = A.copy()
+    B.data = B.data.copy()
+    B.data[B.indptr[11] - 1] += 1e-3  # one upper value off its mirror
+    assert [s.dia_walk for s in gpu_order.shard_scheds(B, [0, 1500, 3000])] == [0, 1]
+    P = golden_matrix(["poisson", 16, 3])
+    assert gpu_order.shard_scheds(P, [0, P.shape[0]])[0].dia_walk == 0
+
+
 def test_oracle_default_order_untouched():
     """patched() restores the oracle's numpy dot afterwards."""
     A = golden_matrix(["poisson", 8, 2])

@@ -94,6 +94,31 @@ def test_v3_gpu_matches_reference(c):
     assert ("Status:\t\tconverged" in text) == bool(info["residual"][-1] < c["tol"])
 
 
+WALK = [c["name"] for c in CASES if c["matrix"][0] == "banded" and c["x0"] is None
+        and c["maxiter"] is None]
+
+
+@pytest.mark.parametrize("shards", [1, 2])
+@pytest.mark.parametrize("name", WALK)
+def test_dia_walk_long_runs_match_reference(monkeypatch, name, shards):
+    """Banded (symmetric DIA walk) cases with long runs of row blocks per
+    workgroup (KR_DIAW_GRID=3; the default grid gives every workgroup one
+    block at fixture sizes): every method, so every epilogue incl. CG's
+    virtual p and MrR's fused vector step, against the reference fixtures."""
+    c = next(c for c in CASES if c["name"] == name)
+    g = golden_case(name)
+    A = golden_matrix(c["matrix"])
+    monkeypatch.setenv("KR_DIAW_GRID", "3")
+    if shards > 1:
+        monkeypatch.setenv("KRYLOV_AMD_SHARDS", ",".join(["0"] * shards))
+    kw = dict(tol=c["tol"], maxiter=c["maxiter"])
+    if c["k"] is not None:
+        kw["k"] = c["k"]
+    with contextlib.redirect_stdout(io.StringIO()):
+        x, info = _solver(c["method"])(A, g["b"], **kw)
+    check_parity(c, g, x, info)
+
+
 SHARDED = ["p3d16_cg", "p3d16_mrr", "p3d16_kskipcg_k4", "p3d16_kskipmrr_k4",
            "p3d16_adaptivekskipmrr_k4", "band2000_kskipmrr_k4", "band2000_mrr"]
 

@@ -125,6 +125,14 @@ def test_ilu_argument_forms():
         _diagonal(spla.spilu(A), 200)
     with pytest.raises(ValueError):
         Jacobi(d=np.zeros(3))
+    with pytest.raises(ValueError):
+        Jacobi(d=np.array([1.0, np.nan]))
+    # a raw diagonal gets Jacobi's check: zero / non-finite entries are refused
+    for bad in (0.0, np.inf, np.nan):
+        dd = d.copy()
+        dd[7] = bad
+        with pytest.raises(ValueError, match="row 7"):
+            _diagonal(dd, 200)
 
 
 def test_v1_banner_text():
