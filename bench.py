@@ -60,6 +60,10 @@ def parse():
     p.add_argument("--nz", type=int, default=None,
                    help="Poisson planes (a side^2 x nz box, e.g. --nz 64: one rank's slab of "
                         "512^3 at 8 GPUs, for per-rank studies on one GPU)")
+    p.add_argument("--local-shards", type=int, default=1,
+                   help="split this rank's rows into S in-process shards on its one GPU "
+                        "(the single-process multi-GPU layout, for host-enqueue studies; "
+                        "halos are device copies)")
     p.add_argument("--k", type=int, default=None)
     p.add_argument("--method", default=None)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -243,7 +247,10 @@ def run_system(args, cfg, mat, n, world, rank, local, comm, method, k, env=None)
     os.environ.update(env or {})
     try:
         part = balanced_partition(n, world)
-        sysm = KrylovSystem(n, [part[rank], part[rank + 1]], [local], comm)
+        S = max(1, args.local_shards)
+        lo, hi = part[rank], part[rank + 1]
+        rows = [lo + (hi - lo) * j // S for j in range(S + 1)]
+        sysm = KrylovSystem(n, rows, [local] * S, comm)
         if mat[0] == "poisson":
             sysm.gen_poisson(mat[1], mat[2])
         else:
@@ -349,7 +356,8 @@ def kernel_sampling(kernels, run, args):
     if not kernels:
         return None
     every = args.profile_every or PROFILE_EVERY.get(args.config, 4)
-    per_launch = {n_: v["total_ms"] / v["launches"] for n_, v in kernels.items()}
+    # kr_solve_kernel_stats_reset restarts the sampling at the first timed
+    # step: steps 0, N, 2N, ... of the window are the sampled ones
     sampled_steps = max(1, -(-args.steps // every))
     per_step = sum(v["total_ms"] for v in kernels.values()) / sampled_steps
     step_ms = run["elapsed"] / args.steps * 1e3
@@ -460,7 +468,9 @@ def main():
                                    + f", nnz/shard={info['nnz']}, tol=0 fixed iterations",
                        "method": method, "k": k, "matrix": mat,
                        "step": f"one outer iteration = {per_step} solver iterations",
-                       "parallelism": f"row-partitioned x{world}, RCCL halo + Gram all-gather"},
+                       "parallelism": f"row-partitioned x{world}, RCCL halo + Gram all-gather"
+                       + (f"; {args.local_shards} in-process shards per rank on its GPU"
+                          if args.local_shards > 1 else "")},
             "roofline": roofline,
             "cpu_baseline": base,
             "parity": parity,

@@ -358,7 +358,8 @@ typedef struct {
   double bytes_per_launch; /* algorithmic bytes, see DESIGN.md */
 } kr_kernel_stat;
 int kr_solve_kernel_stats(kr_system* sys, kr_kernel_stat* stats, int cap, int* count);
-/* Zero the per-kernel statistics (e.g. after warm-up). */
+/* Zero the per-kernel statistics (e.g. after warm-up) and restart the
+ * every-N-th sampling (profile = N) with the next outer iteration. */
 int kr_solve_kernel_stats_reset(kr_system* sys);
 
 #ifdef __cplusplus

@@ -860,6 +860,9 @@ int kr_solve_kernel_stats_reset(kr_system* sys) {
     KR_REQUIRE(sys, "NULL system");
     sys->harvest_profile();
     for (auto& s : sys->shards) s.stats.clear();
+    // restart the every-N-th sampling with the next outer iteration, so a
+    // window of K steps after a reset samples exactly ceil(K / N) of them
+    sys->prof_tick = 0;
   });
 }
 

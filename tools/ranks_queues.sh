@@ -17,4 +17,9 @@ run() {  # ranks, queues (default = unset), tag
 import json; d=json.load(open('gpurun_out/ranksq/$tag.json'))
 print('$tag', d['value'], 'it/s', d['ms_per_step'], 'ms/step', {k: v['avg_ms'] for k, v in d['kernels'].items()})"
 }
+# the driver's scheduling parameters (read-only module parameters)
+for f in hws_max_conc_proc sched_policy mes cwsr_enable no_system_mem_limit; do
+  echo "amdgpu.$f=$(cat /sys/module/amdgpu/parameters/$f 2>/dev/null || echo n/a)"
+done > gpurun_out/ranksq/amdgpu_params.txt
+cat gpurun_out/ranksq/amdgpu_params.txt
 run 4 "" r4_default && run 8 2 r8_q2 && run 8 1 r8_q1 && run 8 "" r8_default
