@@ -42,7 +42,8 @@ extern "C" {
 /* Preconditioned and pipelined CG (reference v1/threads/pipeline/{pcg,
  * chronopoulos_gear,gropp,pipeline}.py: `method(A, b, ilu, epsilon, T, pt)`),
  * restated as the textbook algorithms those files name with a Jacobi
- * preconditioner (kr_solve_set_precond). maxiter < 0 means
+ * (kr_solve_set_precond) or ILU (kr_solve_set_precond_ilu) preconditioner
+ * (DESIGN.md §5b). maxiter < 0 means
  * 2N (v1/threads/common.py:47); iterations i = 1 .. maxiter-1. */
 #define KR_METHOD_PCG 5
 #define KR_METHOD_CG_GEAR 6
@@ -54,8 +55,9 @@ extern "C" {
  *   100  round 1
  *   200  kr_solve_params gained nan_guard and kr_solve_result diverged (both
  *        structs changed size); maxiter = 0 is honoured instead of meaning
- *        the default (CG / k-skip CG return r0, the MrR family is refused). */
-#define KR_ABI_VERSION 200
+ *        the default (CG / k-skip CG return r0, the MrR family is refused).
+ *   201  kr_solve_set_precond_ilu added (no struct or behaviour change). */
+#define KR_ABI_VERSION 201
 int kr_version(void);
 const char* kr_last_error(void);
 /* Number of HIP devices visible to this process (0 when none). */
@@ -341,6 +343,21 @@ int kr_solve_begin(kr_system* sys, const kr_solve_params* params,
  * its siblings). The pointers are read at kr_solve_begin (copied into the
  * session); d_dev == NULL restores the identity (d = 1). */
 int kr_solve_set_precond(kr_system* sys, const double* const* d_dev);
+/* ILU preconditioner for the same family: the reference's `ilu` is a scipy
+ * SuperLU (spilu / splu) with A ~ Pr^T L U Pc^T, and `ilu.solve(v)` =
+ * Pc U^-1 L^-1 Pr v (v1/threads/pipeline/pcg.py:26,41, gropp.py:25,33,
+ * chronopoulos_gear.py:26,46, pipeline.py:26,39). HOST arrays: L and U as
+ * CSR rows incl. the diagonal (ascending columns, int64 row pointers, int32
+ * columns), perm_r / perm_c as SuperLU gives them (Pr[perm_r[i], i] = 1,
+ * Pc[i, perm_c[i]] = 1). Validated and copied at the call (the factors'
+ * level schedules are built here); the sweeps run on the device, one
+ * workgroup per sweep, levels separated by barriers. Needs a one-shard
+ * system (KR_ERR_INVALID otherwise). l_rowptr == NULL clears it; either
+ * set_precond call replaces the other's preconditioner. */
+int kr_solve_set_precond_ilu(kr_system* sys, int64_t n, const int64_t* l_rowptr,
+                             const int32_t* l_col, const double* l_val, const int64_t* u_rowptr,
+                             const int32_t* u_col, const double* u_val, const int64_t* perm_r,
+                             const int64_t* perm_c);
 /* Run up to `max_outer` further outer iterations (CG/MrR: iterations).
  * *done = 1 once converged or maxiter reached. */
 int kr_solve_step(kr_system* sys, int64_t max_outer, int* done);

@@ -55,6 +55,53 @@ class Jacobi:
         return v / self.d
 
 
+class IluSweeps:
+    """``solve`` of a scipy SuperLU (``spilu`` / ``splu``: A ~ Pr^T L U Pc^T,
+    ilu.solve(v) = Pc U^-1 L^-1 Pr v) restated as the device's two
+    level-scheduled triangular sweeps (kr_kernels.hip ilu_sweep_kernel): row i
+    of a sweep is s = rhs; s = s - T[i][j] * x[j] over its strictly-triangular
+    entries in ascending column order (each product rounded, then the
+    difference); x[i] = s / T[i][i]. Level order does not change any row's
+    arithmetic, so this restates the device bit for bit; SuperLU's own solve
+    (supernodal, column-oriented) agrees to rounding
+    (tests/test_pipecg.py::test_ilu_sweeps_match_superlu)."""
+
+    def __init__(self, ilu):
+        import scipy.sparse as sp
+        self.L = sp.csr_matrix(ilu.L)
+        self.U = sp.csr_matrix(ilu.U)
+        for T in (self.L, self.U):
+            T.sum_duplicates()
+            T.sort_indices()
+        self.pr = np.asarray(ilu.perm_r)
+        self.pc = np.asarray(ilu.perm_c)
+        self.n = self.L.shape[0]
+
+    def _sweep(self, T, rhs, lower):
+        n = self.n
+        x = np.zeros(n)
+        order = range(n) if lower else range(n - 1, -1, -1)
+        ip, ix, dv = T.indptr, T.indices, T.data
+        for i in order:
+            s = rhs[i]
+            d = None
+            for jj in range(ip[i], ip[i + 1]):
+                j = ix[jj]
+                if j == i:
+                    d = dv[jj]
+                elif (j < i) == lower:
+                    s = s - dv[jj] * x[j]
+            x[i] = s / d
+        return x
+
+    def solve(self, v):
+        w = np.empty(self.n)
+        w[self.pr] = v                      # Pr v
+        y = self._sweep(self.L, w, True)    # L^-1
+        z = self._sweep(self.U, y, False)   # U^-1
+        return z[self.pc]                   # Pc z
+
+
 class _Identity:
     def solve(self, v):
         return v.copy()

@@ -20,7 +20,7 @@ KR_METHOD = {"cg": 0, "mrr": 1, "kskipcg": 2, "kskipmrr": 3, "adaptivekskipmrr":
              "pcg": 5, "chronopoulos_gear": 6, "gropp": 7, "pipeline": 8}
 # include/krylov_amd.h KR_ABI_VERSION: the struct layouts below (SolveParams,
 # SolveResult) are this version's; a library of another version is refused.
-KR_ABI_VERSION = 200
+KR_ABI_VERSION = 201
 KR_FORMAT = {0: "csr", 1: "stencil", 2: "dia", 3: "dense", 4: "dia_walk"}  # kr_system_shard_sched
 
 
@@ -104,6 +104,7 @@ _SIGNATURES = {
     "kr_system_spmv": [_PP, _PP, _PP],
     "kr_solve_begin": [_P, ctypes.POINTER(SolveParams), _PP, _PP],
     "kr_solve_set_precond": [_P, _PP],
+    "kr_solve_set_precond_ilu": [_P, _I64, _P, _P, _P, _P, _P, _P, _P, _P],
     "kr_solve_step": [_P, _I64, _PI],
     "kr_solve_end": [_P, _PP, ctypes.POINTER(SolveResult)],
     "kr_solve_history": [_P, _PD, _PI64, _PI64, _I64],

@@ -757,7 +757,31 @@ int kr_solve_set_precond(kr_system* sys, const double* const* d) {
   return guarded([&] {
     KR_REQUIRE(sys && sys->finalized, "system not finalized");
     sys->precond.clear();
+    sys->ilu.reset();  // the last preconditioner set wins
     if (d) sys->precond.assign(d, d + sys->shards.size());
+  });
+}
+
+int kr_solve_set_precond_ilu(kr_system* sys, int64_t n, const int64_t* l_rowptr,
+                             const int32_t* l_col, const double* l_val, const int64_t* u_rowptr,
+                             const int32_t* u_col, const double* u_val, const int64_t* perm_r,
+                             const int64_t* perm_c) {
+  return guarded([&] {
+    KR_REQUIRE(sys && sys->finalized, "system not finalized");
+    if (!l_rowptr) {  // clear
+      sys->ilu.reset();
+      return;
+    }
+    KR_REQUIRE(l_col && l_val && u_rowptr && u_col && u_val && perm_r && perm_c, "NULL argument");
+    // the sweeps run over the whole vector in one workgroup: one shard, one rank
+    KR_REQUIRE(sys->shards.size() == 1 && sys->nglobal_shards() == 1,
+               "ILU preconditioning needs a one-shard system (the triangular sweeps are "
+               "sequential over the whole vector)");
+    KR_REQUIRE(n == sys->n_global, "ILU: factor size differs from the system size");
+    Shard& s = sys->shards[0];
+    sys->ilu = build_ilu(s.dev, s.stream, n, l_rowptr, l_col, l_val, u_rowptr, u_col, u_val,
+                         perm_r, perm_c);
+    sys->precond.clear();  // the last preconditioner set wins
   });
 }
 

@@ -247,6 +247,147 @@ System::~System() {
   }
 }
 
+IluFactors::~IluFactors() {
+  (void)hipSetDevice(dev);
+  for (void* p : owned) (void)hipFree(p);
+}
+
+namespace {
+// Levels of a triangular sweep: level(i) = 1 + the largest level of the rows
+// row i reads (0 for none), in sweep order (ascending rows for L, descending
+// for U). Returns the rows grouped by level (ascending row index inside a
+// level) and the level offsets.
+void sweep_levels(int64_t n, const int64_t* rp, const int32_t* col, bool lower,
+                  std::vector<int32_t>& rows, std::vector<int64_t>& ptr) {
+  std::vector<int32_t> lev((size_t)n, 0);
+  int32_t top = -1;
+  for (int64_t q = 0; q < n; ++q) {
+    const int64_t i = lower ? q : n - 1 - q;
+    int32_t l = 0;
+    for (int64_t jj = rp[i]; jj < rp[i + 1]; ++jj) l = std::max(l, lev[(size_t)col[jj]] + 1);
+    lev[(size_t)i] = l;
+    top = std::max(top, l);
+  }
+  ptr.assign((size_t)top + 2, 0);
+  for (int64_t i = 0; i < n; ++i) ++ptr[(size_t)lev[(size_t)i] + 1];
+  for (size_t l = 1; l < ptr.size(); ++l) ptr[l] += ptr[l - 1];
+  rows.assign((size_t)n, 0);
+  std::vector<int64_t> fill(ptr.begin(), ptr.end() - 1);
+  for (int64_t i = 0; i < n; ++i) rows[(size_t)fill[(size_t)lev[(size_t)i]]++] = (int32_t)i;
+}
+
+// Split one factor (full rows incl. the diagonal, ascending columns) into its
+// strictly-triangular CSR and its diagonal, checking the triangle.
+void split_factor(int64_t n, const int64_t* rp, const int32_t* col, const double* val, bool lower,
+                  std::vector<int64_t>& srp, std::vector<int32_t>& scol, std::vector<double>& sval,
+                  std::vector<double>& diag) {
+  const char* which = lower ? "L" : "U";
+  srp.assign((size_t)n + 1, 0);
+  scol.clear();
+  sval.clear();
+  diag.assign((size_t)n, 0.0);
+  KR_REQUIRE(rp[0] == 0, std::string("ILU: ") + which + " row pointer must start at 0");
+  for (int64_t i = 0; i < n; ++i) {
+    KR_REQUIRE(rp[i + 1] >= rp[i], std::string("ILU: ") + which + " row pointer decreases");
+    bool have = false;
+    int64_t prev = -1;
+    for (int64_t jj = rp[i]; jj < rp[i + 1]; ++jj) {
+      const int64_t j = col[jj];
+      KR_REQUIRE(j > prev && j < n, std::string("ILU: ") + which +
+                                         " columns must ascend within a row and lie in [0, n)");
+      prev = j;
+      if (j == i) {
+        have = true;
+        diag[(size_t)i] = val[jj];
+      } else {
+        KR_REQUIRE(lower ? j < i : j > i,
+                   std::string("ILU: ") + which + " has an entry on the wrong side of the diagonal");
+        scol.push_back((int32_t)j);
+        sval.push_back(val[jj]);
+      }
+    }
+    KR_REQUIRE(have && diag[(size_t)i] != 0.0 && std::isfinite(diag[(size_t)i]),
+               std::string("ILU: ") + which + " needs a finite nonzero diagonal in every row (row " +
+                   std::to_string(i) + ")");
+    srp[(size_t)i + 1] = (int64_t)scol.size();
+  }
+}
+
+std::vector<int32_t> inverse_perm(int64_t n, const int64_t* p, const char* what) {
+  std::vector<int32_t> inv((size_t)n, -1);
+  for (int64_t i = 0; i < n; ++i) {
+    KR_REQUIRE(p[i] >= 0 && p[i] < n && inv[(size_t)p[i]] < 0,
+               std::string("ILU: ") + what + " is not a permutation of 0..n-1");
+    inv[(size_t)p[i]] = (int32_t)i;
+  }
+  return inv;
+}
+}  // namespace
+
+std::unique_ptr<IluFactors> build_ilu(int dev, hipStream_t stream, int64_t n, const int64_t* lrp,
+                                      const int32_t* lcol, const double* lval, const int64_t* urp,
+                                      const int32_t* ucol, const double* uval,
+                                      const int64_t* perm_r, const int64_t* perm_c) {
+  KR_REQUIRE(n > 0 && n < ((int64_t)1 << 31), "ILU: n must lie in [1, 2^31)");
+  auto f = std::make_unique<IluFactors>();
+  f->dev = dev;
+  f->n = n;
+  KR_HIP_CHECK(hipSetDevice(dev));
+  auto up = [&](const void* h, size_t bytes) {
+    void* d = nullptr;
+    KR_HIP_CHECK(hipMalloc(&d, std::max<size_t>(bytes, 8)));
+    f->owned.push_back(d);
+    if (bytes) KR_HIP_CHECK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream));
+    return d;
+  };
+  for (int side = 0; side < 2; ++side) {
+    const bool lo = side == 0;
+    std::vector<int64_t> srp, ptr;
+    std::vector<int32_t> scol, rows;
+    std::vector<double> sval, diag;
+    split_factor(n, lo ? lrp : urp, lo ? lcol : ucol, lo ? lval : uval, lo, srp, scol, sval, diag);
+    sweep_levels(n, srp.data(), scol.data(), lo, rows, ptr);
+    IluSweepArgs& a = lo ? f->lower : f->upper;
+    a.nlev = (int64_t)ptr.size() - 1;
+    a.lvl_ptr = static_cast<const int64_t*>(up(ptr.data(), 8 * ptr.size()));
+    a.lvl_rows = static_cast<const int32_t*>(up(rows.data(), 4 * rows.size()));
+    a.rp = static_cast<const int64_t*>(up(srp.data(), 8 * srp.size()));
+    a.col = static_cast<const int32_t*>(up(scol.data(), 4 * scol.size()));
+    a.val = static_cast<const double*>(up(sval.data(), 8 * sval.size()));
+    a.diag = static_cast<const double*>(up(diag.data(), 8 * diag.size()));
+    const std::vector<int32_t> inv =
+        inverse_perm(n, lo ? perm_r : perm_c, lo ? "perm_r" : "perm_c");
+    a.perm = static_cast<const int32_t*>(up(inv.data(), 4 * inv.size()));
+    f->nnz += (int64_t)scol.size();
+  }
+  f->y = static_cast<double*>(up(nullptr, 8 * (size_t)n));
+  f->z = static_cast<double*>(up(nullptr, 8 * (size_t)n));
+  KR_HIP_CHECK(hipStreamSynchronize(stream));  // the host vectors go out of scope
+  return f;
+}
+
+// M^-1 v (shard 0): w = Pr v folded into the L sweep's loads, y = L^-1 w,
+// z = U^-1 y, out = Pc z folded into the U sweep's stores.
+void System::ilu_apply(int in, int out) {
+  KR_REQUIRE(ilu && shards.size() == 1, "ILU apply: no factors, or more than one shard");
+  Shard& s = shards[0];
+  KR_HIP_CHECK(hipSetDevice(s.dev));
+  hipEvent_t t0;
+  prof_begin(s, "ilu_sweeps", t0);
+  IluSweepArgs lo = ilu->lower, hi = ilu->upper;
+  lo.in = s.own(in);
+  lo.x = ilu->y;
+  hi.in = ilu->y;
+  hi.x = ilu->z;
+  hi.out = s.own(out);
+  launch_ilu_sweep(true, lo, s.stream);
+  launch_ilu_sweep(false, hi, s.stream);
+  // values + columns + row pointers of both factors, the diagonals, and the
+  // vectors: v, y (written, read), z (written), out
+  prof_end(s, "ilu_sweeps", t0,
+           12.0 * (double)ilu->nnz + 8.0 * 2 * (double)(ilu->n + 1) + 8.0 * 8 * (double)ilu->n);
+}
+
 // x window of the DIA kernel (SpmvArgs::nseg ...): offsets closer than 256
 // rows share a segment; at most 4 segments and 4096 rows (32 KiB per vector),
 // else the kernel gathers from global memory. KR_DIA_XL=0 disables (A/B).
@@ -2423,12 +2564,14 @@ class PipeCgSession : public Base {
 
  public:
   explicit PipeCgSession(int v) : variant(v) {}
+  bool ilu = false;  // M^-1 by the ILU sweeps (System::ilu), d = 1
 
   void begin(const double* const* b, const double* const* x0) override {
     sys->alloc_vectors(NV);
     load_bx(B, X, b, x0);
-    // d: the caller's diagonal, else ones
-    const bool have = !sys->precond.empty();
+    // d: the caller's diagonal, else ones (ILU: ones, and M^-1 by the sweeps)
+    ilu = sys->ilu != nullptr;
+    const bool have = !ilu && !sys->precond.empty();
     for (size_t li = 0; li < sys->shards.size(); ++li) {
       Shard& s = sys->shards[li];
       if (have && sys->precond[li]) {
@@ -2440,10 +2583,14 @@ class PipeCgSession : public Base {
     if (!have) sys->ew_n(EW_ONE, 0, 0, ids({D}), 0);
     sys->spmv(EPI_BMINUS, X, -1, R, -1, -1, B, 0);      // r = b - A x
     sys->ew_n(EW_PRE, 0, 0, ids({R, U, D}), 1);           // u = M^-1 r ; <r,r> <r,u>
-    const auto g = sys->reduce(3);                        // slot 0: <r,r> of the SpMV
+    if (ilu) {                                            // u = ilu.solve(r) ; <r,u>: slot 3
+      sys->ilu_apply(R, U);
+      sys->ew(EW_DOT, 0, 0, {R, U, -1, -1, -1, -1}, 3);
+    }
+    const auto g = sys->reduce(ilu ? 4 : 3);              // slot 0: <r,r> of the SpMV
     set_entry(0, rel(g[0]));
     set_nosl(0, 0);
-    gamma = g[2];                                         // <r,u>
+    gamma = g[ilu ? 3 : 2];                               // <r,u>
     switch (variant) {
       case KR_METHOD_PCG:    // p = u.copy()  (pcg.py:28)
       case KR_METHOD_GROPP:  // p = u.copy(); s = A p  (gropp.py:26-27)
@@ -2477,10 +2624,14 @@ class PipeCgSession : public Base {
         const double sigma = sys->reduce(3)[1];
         alpha = gamma / sigma;
         sys->ew_n(EW_PCG, alpha, 0, ids({X, P, R, S, U, D}), 0);  // x, r, u ; <r,r> <r,u>
-        const auto g = sys->reduce(2);
+        if (ilu) {  // u = ilu.solve(r) ; <r,u>: slot 2 (unused after the exit test)
+          sys->ilu_apply(R, U);
+          sys->ew(EW_DOT, 0, 0, {R, U, -1, -1, -1, -1}, 2);
+        }
+        const auto g = sys->reduce(ilu ? 3 : 2);
         rr = g[0];
         if (!(rel(rr) < prm.tol)) {
-          const double gnew = g[1];
+          const double gnew = g[ilu ? 2 : 1];
           beta = gnew / gamma;
           gamma = gnew;
           sys->ew(EW_CG_P, beta, 0, {P, U, -1, -1, -1, -1}, 0);  // p = u + beta p
@@ -2489,10 +2640,14 @@ class PipeCgSession : public Base {
       }
       case KR_METHOD_CG_GEAR: {  // chronopoulos_gear.py:36-51: one sync per iteration
         sys->ew_n(EW_CGG, alpha, beta, ids({P, U, S, W, X, R, D}), 0);  // <r,r> <r,u>
+        if (ilu) {  // u = ilu.solve(r) ; <r,u>: slot 5
+          sys->ilu_apply(R, U);
+          sys->ew(EW_DOT, 0, 0, {R, U, -1, -1, -1, -1}, 5);
+        }
         sys->spmv(EPI_XY, U, -1, W, -1, -1, -1, 2);              // w = A u ; <u,w>: slot 3
-        const auto g = sys->reduce(5);
+        const auto g = sys->reduce(ilu ? 6 : 5);
         rr = g[0];
-        const double gnew = g[1];
+        const double gnew = g[ilu ? 5 : 1];
         delta = g[3];
         beta = gnew / gamma;
         alpha = gnew / (delta - beta * gnew / alpha);
@@ -2501,7 +2656,14 @@ class PipeCgSession : public Base {
       }
       case KR_METHOD_GROPP: {  // gropp.py:30-45
         alpha = gamma / delta;
-        sys->ew_n(EW_GROPP1, alpha, 0, ids({X, P, R, S, U, D}), 0);  // <r,r> <r,u>
+        if (ilu) {  // q = ilu.solve(s); x += a p; r -= a s ; <r,r>; u -= a q; <r,u>
+          sys->ilu_apply(S, Q);
+          sys->ew(EW_CG, alpha, 0, {X, P, R, S, -1, -1}, 0);
+          sys->ew(EW_AXPY, -alpha, 0, {U, Q, -1, -1, -1, -1}, 0);  // u + (-a) q == u - a q
+          sys->ew(EW_DOT, 0, 0, {R, U, -1, -1, -1, -1}, 1);
+        } else {
+          sys->ew_n(EW_GROPP1, alpha, 0, ids({X, P, R, S, U, D}), 0);  // <r,r> <r,u>
+        }
         sys->spmv(EPI_NONE, U, -1, W, -1, -1, -1, 2);                 // w = A u (overlaps)
         const auto g = sys->reduce(2);
         rr = g[0];
@@ -2515,7 +2677,10 @@ class PipeCgSession : public Base {
         break;
       }
       case KR_METHOD_PIPECG: {  // pipeline.py:31-55: one sync per iteration
-        sys->ew_n(EW_DIV, 0, 0, ids({M, W, D}), 0);                   // m = M^-1 w
+        if (ilu)
+          sys->ilu_apply(W, M);                                       // m = ilu.solve(w)
+        else
+          sys->ew_n(EW_DIV, 0, 0, ids({M, W, D}), 0);                 // m = M^-1 w
         sys->spmv(EPI_NONE, M, -1, NN, -1, -1, -1, 0);                // n = A m
         if (it > 1) {
           beta = gamma / gold;

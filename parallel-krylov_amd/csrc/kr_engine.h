@@ -151,6 +151,19 @@ struct StepOps {
 void plan_halo(int P, const int64_t* part, const int64_t* need_lo, const int64_t* need_hi,
                int me, std::vector<HaloPiece>& recv, std::vector<HaloPiece>& send);
 
+// ILU preconditioner of the pipelined CG family (kr_solve_set_precond_ilu):
+// the factors of the reference's `ilu` (a scipy SuperLU, M = Pr^T L U Pc^T)
+// on shard 0's device, with the level schedules of both triangular sweeps.
+struct IluFactors {
+  int dev = 0;
+  int64_t n = 0, nnz = 0;           // nnz: strictly-triangular entries of L and U
+  IluSweepArgs lower, upper;        // in / out / x pointers set per apply
+  double* y = nullptr;              // L^-1 Pr v
+  double* z = nullptr;              // U^-1 y
+  std::vector<void*> owned;
+  ~IluFactors();
+};
+
 struct System {
   int64_t n_global = 0;
   std::vector<Shard> shards;
@@ -215,6 +228,10 @@ struct System {
   // shard (own rows; kr_solve_set_precond), copied into the session's d
   // vector at begin; empty / null: the identity (d = 1).
   std::vector<const double*> precond;
+  // ILU instead of the diagonal (one shard): M^-1 v by the two sweeps
+  // (ilu_apply; the fused vector kernels then run with d = 1)
+  std::unique_ptr<IluFactors> ilu;
+  void ilu_apply(int in, int out);
   // Device-resident scalars (one shard per rank, or every shard in this
   // process): the vector kernel takes c0, c1 from st[coef], st[coef + 1];
   // scalar() runs one scalar_kernel step over the reductions in slots `need`
@@ -306,6 +323,12 @@ class Session {
 };
 
 std::unique_ptr<Session> make_session(System* sys, const kr_solve_params& p);
+// Validate and upload the ILU factors (host CSR rows of L and U incl. the
+// diagonal, ascending columns; SuperLU's perm_r / perm_c) to `dev`.
+std::unique_ptr<IluFactors> build_ilu(int dev, hipStream_t stream, int64_t n, const int64_t* lrp,
+                                      const int32_t* lcol, const double* lval, const int64_t* urp,
+                                      const int32_t* ucol, const double* uval,
+                                      const int64_t* perm_r, const int64_t* perm_c);
 double now_seconds();
 
 }  // namespace kr

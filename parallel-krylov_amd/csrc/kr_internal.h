@@ -455,6 +455,27 @@ struct CgPersistArgs {
 int cg_persist_grid(int64_t n);
 void launch_cg_persist(const CgPersistArgs& a, int grid, hipStream_t s);
 
+// One triangular sweep of the ILU preconditioner (kr_kernels.hip
+// ilu_sweep_kernel): levels lvl_ptr[0..nlev] of rows lvl_rows (device), the
+// strictly-triangular rows in CSR (rp, col, val; ascending columns) and the
+// diagonal. Lower: x[i] = (in[perm[i]] - sum L[i][j] x[j]) / diag[i] (perm =
+// the inverse row permutation); upper: x[i] = (in[i] - sum U[i][j] x[j]) /
+// diag[i], also stored at out[perm[i]] (perm = the inverse column permutation).
+struct IluSweepArgs {
+  int64_t nlev = 0;
+  const int64_t* lvl_ptr = nullptr;
+  const int32_t* lvl_rows = nullptr;
+  const int64_t* rp = nullptr;
+  const int32_t* col = nullptr;
+  const double* val = nullptr;
+  const double* diag = nullptr;
+  const double* in = nullptr;
+  const int32_t* perm = nullptr;
+  double* x = nullptr;
+  double* out = nullptr;
+};
+void launch_ilu_sweep(bool lower, const IluSweepArgs& a, hipStream_t s);
+
 int default_grid(int64_t n);
 // Workgroups of the SpMV kernels for a block of n rows with column reach `reach` rows.
 int spmv_grid_for(int64_t n, int64_t reach);

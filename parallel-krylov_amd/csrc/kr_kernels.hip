@@ -1558,4 +1558,48 @@ void launch_vdict_encode(const double* val, int64_t nnz, const unsigned long lon
   KR_HIP_CHECK(hipGetLastError());
 }
 
+// ---------------------------------------------------------------------------
+// ILU preconditioner sweeps (the reference's `ilu.solve`, a scipy SuperLU:
+// v1/threads/pipeline/pcg.py:26,41). M = Pr^T L U Pc^T; M^-1 v = Pc U^-1
+// L^-1 Pr v as two level-scheduled triangular sweeps (IluSweepArgs). Rows of
+// one level depend only on rows of earlier levels, so each level is a
+// parallel step; the levels run in ONE workgroup, separated by barriers: a
+// sweep is one launch with no inter-workgroup synchronisation (nothing to
+// time out), and the typical level holds tens of rows (a 256^2 Poisson spilu
+// has ~1000 levels of ~65 rows), which one workgroup covers. Row i: s = rhs,
+// s -= T[i][j] x[j] over the stored strictly-triangular entries in ascending
+// column order, x[i] = s / T[i][i].
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int kIluThreads = 1024;
+
+template <bool LOWER>
+__global__ __launch_bounds__(kIluThreads) void ilu_sweep_kernel(IluSweepArgs a) {
+  const int tid = threadIdx.x;
+  for (int64_t lev = 0; lev < a.nlev; ++lev) {
+    const int64_t beg = a.lvl_ptr[lev];  // uniform: scalar loads
+    const int64_t end = a.lvl_ptr[lev + 1];
+    for (int64_t t = beg + tid; t < end; t += kIluThreads) {
+      const int32_t i = a.lvl_rows[t];
+      double s = LOWER ? a.in[a.perm[i]] : a.in[i];  // lower: (Pr v)[i] = v[prinv[i]]
+      const int64_t j1 = a.rp[i + 1];
+      for (int64_t jj = a.rp[i]; jj < j1; ++jj) s = s - a.val[jj] * a.x[a.col[jj]];
+      const double xi = s / a.diag[i];
+      a.x[i] = xi;
+      if (!LOWER) a.out[a.perm[i]] = xi;  // (Pc z)[j] = z[pc[j]]: out[pcinv[i]] = z[i]
+    }
+    __syncthreads();  // this level's x visible to the next level's rows
+  }
+}
+}  // namespace
+
+void launch_ilu_sweep(bool lower, const IluSweepArgs& a, hipStream_t s) {
+  if (a.nlev <= 0) return;
+  if (lower)
+    ilu_sweep_kernel<true><<<1, kIluThreads, 0, s>>>(a);
+  else
+    ilu_sweep_kernel<false><<<1, kIluThreads, 0, s>>>(a);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace kr

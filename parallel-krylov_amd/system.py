@@ -399,6 +399,40 @@ class KrylovSystem:
                 raise ValueError(f"preconditioner part {s}: need {n_own} float64 device values")
         call("kr_solve_set_precond", self.handle, ptr_array([t.data_ptr() for t in self._precond]))
 
+    def set_precond_ilu(self, factors) -> None:
+        """ILU preconditioner of the preconditioned / pipelined CG sessions
+        begun afterwards (kr_solve_set_precond_ilu; one-shard systems):
+        ``factors`` = (L, U, perm_r, perm_c) with L, U scipy CSR factors incl.
+        the diagonal and SuperLU's permutations (A ~ Pr^T L U Pc^T); None
+        clears it. The library validates and copies the host arrays."""
+        if factors is None:
+            call("kr_solve_set_precond_ilu", self.handle, 0, None, None, None, None, None, None,
+                 None, None)
+            return
+        L, U, perm_r, perm_c = factors
+        n = self.n_global
+
+        def csr(T, name):
+            import scipy.sparse as sp
+            T = sp.csr_matrix(T)
+            if T.shape != (n, n):
+                raise ValueError(f"ILU {name}: shape {T.shape}, the system is {n} x {n}")
+            T.sum_duplicates()
+            T.sort_indices()
+            return (np.ascontiguousarray(T.indptr, np.int64),
+                    np.ascontiguousarray(T.indices, np.int32),
+                    np.ascontiguousarray(T.data, np.float64))
+
+        lr, lc, lv = csr(L, "L")
+        ur, uc, uv = csr(U, "U")
+        pr = np.ascontiguousarray(perm_r, np.int64)
+        pc = np.ascontiguousarray(perm_c, np.int64)
+        if pr.shape != (n,) or pc.shape != (n,):
+            raise ValueError(f"ILU permutations must have {n} entries")
+        ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        call("kr_solve_set_precond_ilu", self.handle, n, ptr(lr), ptr(lc), ptr(lv), ptr(ur),
+             ptr(uc), ptr(uv), ptr(pr), ptr(pc))
+
     def solve(self, method: str, b_parts, x0_parts=None, tol=1e-5, maxiter=None, k=0,
               profile=False, max_outer=None, nan_guard=None) -> SolveOutput:
         """Run one solver to completion (or for ``max_outer`` outer steps).

@@ -8,13 +8,18 @@ kernels EW_PCG / EW_CGG / EW_GROPP* / EW_PIPE). ``pt`` is accepted for
 compatibility; both values run on the GPUs (the package has no CPU path).
 
 ``ilu`` is the preconditioner: the reference passes an object whose
-``solve(v)`` applies M^-1 (pcg.py:26). On the device the preconditioner is
-diagonal (Jacobi, M^-1 v = v / d):
+``solve(v)`` applies M^-1 (pcg.py:26), a scipy SuperLU from ``spilu``. On the
+device:
   * ``None``: the identity (d = 1);
   * ``Jacobi(A)`` (or any object with a 1-D ``d`` attribute) or a 1-D array /
-    tensor of N values: the diagonal d.
-Anything else -- e.g. scipy's ``spilu`` SuperLU object, whose triangular
-solves run on the host -- raises TypeError instead of silently falling back.
+    tensor of N values: the diagonal d (M^-1 v = v / d, fused into the
+    vector kernels);
+  * a SuperLU (``scipy.sparse.linalg.spilu`` / ``splu``: attributes L, U,
+    perm_r, perm_c) or a (L, U, perm_r, perm_c) tuple: M = Pr^T L U Pc^T, and
+    ``ilu.solve(v)`` = Pc U^-1 L^-1 Pr v runs as two level-scheduled
+    triangular sweeps on the device (kr_solve_set_precond_ilu; the system is
+    then kept on ONE GPU, the sweeps being sequential over the vector).
+Anything else raises TypeError instead of silently falling back.
 """
 from __future__ import annotations
 
@@ -42,6 +47,19 @@ class Jacobi:
         return v / self.d
 
 
+def _ilu_factors(ilu, N):
+    """(L, U, perm_r, perm_c) of a SuperLU object or such a tuple, else None."""
+    if isinstance(ilu, tuple) and len(ilu) == 4:
+        L, U, pr, pc = ilu
+    elif all(hasattr(ilu, a) for a in ("L", "U", "perm_r", "perm_c")):
+        L, U, pr, pc = ilu.L, ilu.U, ilu.perm_r, ilu.perm_c
+    else:
+        return None
+    if L.shape != (N, N) or U.shape != (N, N):
+        raise ValueError(f"ilu: factors of shape {L.shape} / {U.shape}, the system is N = {N}")
+    return L, U, np.asarray(pr), np.asarray(pc)
+
+
 def _diagonal(ilu, N):
     if ilu is None:
         return None
@@ -63,9 +81,9 @@ def _diagonal(ilu, N):
                              f"entries (first at row {int(np.argmax(bad))})")
         return d
     raise TypeError(
-        f"ilu={type(ilu).__name__}: the device path takes a diagonal (Jacobi) preconditioner "
-        "-- None, Jacobi(A) or the diagonal as a 1-D array; triangular ILU solves "
-        "(scipy spilu) run on the host and are not offered (DESIGN.md §5b)")
+        f"ilu={type(ilu).__name__}: the device path takes None, a diagonal (Jacobi(A) or a "
+        "1-D array) or ILU factors (a scipy spilu / splu SuperLU, or (L, U, perm_r, perm_c)) "
+        "(DESIGN.md §5b)")
 
 
 def run(method: str, banner: str, A, b, ilu, epsilon, T=np.float64, pt="cpu", maxiter=None,
@@ -80,15 +98,21 @@ def run(method: str, banner: str, A, b, ilu, epsilon, T=np.float64, pt="cpu", ma
         raise ValueError(f"pt must be 'cpu' or 'gpu', got {pt!r}")
     bh = _host_vector(b)
     N = bh.size
-    d = _diagonal(ilu, N)
+    factors = _ilu_factors(ilu, N)
+    d = None if factors is not None else _diagonal(ilu, N)
     devices = visible_devices()
+    if factors is not None:  # the triangular sweeps are sequential: one shard
+        devices = devices[:1]
     sysm = KrylovSystem(N, balanced_partition(N, len(devices)), devices)
     try:
         sysm.set_matrix(A)
         sysm.finalize()
         b_parts = sysm.split(bh)
         x0_parts = sysm.split(_host_vector(x0)) if x0 is not None else None
-        sysm.set_precond(sysm.split(d) if d is not None else None)
+        if factors is not None:
+            sysm.set_precond_ilu(factors)
+        else:
+            sysm.set_precond(sysm.split(d) if d is not None else None)
         _start(banner, None)
         out = sysm.solve(method, b_parts, x0_parts, tol=epsilon,
                          maxiter=2 * N if maxiter is None else maxiter)

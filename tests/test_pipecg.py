@@ -112,7 +112,7 @@ def test_jacobi_reduces_iterations_on_varying_diagonal():
 
 def test_ilu_argument_forms():
     import scipy.sparse.linalg as spla
-    from parallel_krylov_amd.v1.threads.pipeline.common import Jacobi, _diagonal
+    from parallel_krylov_amd.v1.threads.pipeline.common import Jacobi, _diagonal, _ilu_factors
     A = golden_matrix(("banded", 200, 3, 8, 0)).tocsc()
     d = A.diagonal()
     assert _diagonal(None, 200) is None
@@ -121,8 +121,17 @@ def test_ilu_argument_forms():
     assert np.array_equal(_diagonal(list(d), 200), d)
     with pytest.raises(ValueError):
         _diagonal(d[:10], 200)
-    with pytest.raises(TypeError, match="spilu"):
-        _diagonal(spla.spilu(A), 200)
+    # a SuperLU is taken as ILU factors (run() checks _ilu_factors first);
+    # any other object is refused
+    ilu = spla.spilu(A)
+    L, U, pr, pc = _ilu_factors(ilu, 200)
+    assert L.shape == U.shape == (200, 200) and np.array_equal(pr, ilu.perm_r)
+    assert _ilu_factors((L, U, pr, pc), 200)[0] is L
+    assert _ilu_factors(Jacobi(A), 200) is None and _ilu_factors(None, 200) is None
+    with pytest.raises(ValueError):
+        _ilu_factors(ilu, 100)
+    with pytest.raises(TypeError, match="ILU factors"):
+        _diagonal(object(), 200)
     with pytest.raises(ValueError):
         Jacobi(d=np.zeros(3))
     with pytest.raises(ValueError):
@@ -133,6 +142,49 @@ def test_ilu_argument_forms():
         dd[7] = bad
         with pytest.raises(ValueError, match="row 7"):
             _diagonal(dd, 200)
+
+
+ILU_SYSTEMS = [("p2d32", ("poisson", 32, 2)), ("p3d10", ("poisson", 10, 3)),
+               ("band2000", ("banded", 2000, 13, 64, 0))]
+
+
+def _spilu(A, drop_tol):
+    import scipy.sparse.linalg as spla
+    return spla.spilu(A.tocsc(), drop_tol=drop_tol)
+
+
+@pytest.mark.parametrize("drop_tol", [1e-4, 1e-2])
+@pytest.mark.parametrize("sysname,spec", ILU_SYSTEMS, ids=[s[0] for s in ILU_SYSTEMS])
+def test_ilu_sweeps_match_superlu(sysname, spec, drop_tol):
+    """The oracle's restatement of the device sweeps (row-oriented, ascending
+    columns) against scipy SuperLU's own solve -- the reference's `ilu` object
+    (v1/threads/pipeline/pcg.py:26): equal to rounding (SuperLU's supernodal
+    column solve orders the same subtractions differently)."""
+    from oracle import pipecg
+    A = golden_matrix(spec)
+    ilu = _spilu(A, drop_tol)
+    assert not np.array_equal(ilu.perm_c, np.arange(A.shape[0]))  # COLAMD: permutations used
+    sw = pipecg.IluSweeps(ilu)
+    for seed in range(3):
+        v = np.random.default_rng(seed).standard_normal(A.shape[0])
+        ref = ilu.solve(v)
+        got = sw.solve(v)
+        assert np.max(np.abs(got - ref)) / np.max(np.abs(ref)) < 1e-13
+
+
+@pytest.mark.parametrize("method", METHODS)
+def test_oracle_ilu_converges_faster(method):
+    """ILU-preconditioned variants (spilu as the reference passes it) converge
+    in far fewer iterations than M = I, and the four variants agree."""
+    from oracle import pipecg
+    A = golden_matrix(("poisson", 32, 2))
+    b = np.random.default_rng(1).standard_normal(A.shape[0])
+    sw = pipecg.IluSweeps(_spilu(A, 1e-2))
+    _, n_i, r_i = pipecg.METHODS[method](A, b, None, 1e-10)
+    _, n_l, r_l = pipecg.METHODS[method](A, b, sw, 1e-10)
+    assert r_l[-1] < 1e-10 and len(r_l) < len(r_i) // 2
+    _, _, r_p = pipecg.pcg(A, b, sw, 1e-10)
+    assert abs(len(r_l) - len(r_p)) <= 1
 
 
 def test_v1_banner_text():
@@ -217,3 +269,85 @@ def test_gpu_maxiter_truncation(method):
                                                      return_x=True)
     assert not conv and len(res) == 8 and np.array_equal(nosl, n_o)
     assert np.max(np.abs(res - r_o) / r_o) < RTOL[method]
+
+
+# (system, spilu drop_tol, shards requested) of the GPU ILU parity tests; 3-D
+# Poisson at spilu's default 1e-4 is left out: its factors are not SPD there
+# and every variant runs its 2N iterations without converging (oracle too).
+ILU_CASES = [("p2d32", ("poisson", 32, 2), 1e-4, 1), ("p2d32", ("poisson", 32, 2), 1e-2, 1),
+             ("p2d32", ("poisson", 32, 2), 1e-2, 3), ("p3d10", ("poisson", 10, 3), 1e-2, 1),
+             ("band2000", ("banded", 2000, 13, 64, 0), 1e-4, 1),
+             ("band2000", ("banded", 2000, 13, 64, 0), 1e-2, 3)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sysname,spec,drop_tol,shards", ILU_CASES,
+                         ids=[f"{c[0]}-{c[2]:g}-{c[3]}" for c in ILU_CASES])
+@pytest.mark.parametrize("method", METHODS)
+def test_gpu_ilu_matches_oracle(monkeypatch, method, sysname, spec, drop_tol, shards):
+    """ILU preconditioning on the device (kr_solve_set_precond_ilu: the two
+    level-scheduled sweeps) with the reference's `ilu` object, a scipy spilu
+    SuperLU, against the oracle run with the same factors through
+    oracle.pipecg.IluSweeps (the device's sweep arithmetic): same nosl,
+    residuals within each variant's dot-order envelope (RTOL), x within XTOL.
+    A 3-shard request still runs the ILU system on one shard (the sweeps are
+    sequential over the vector)."""
+    import importlib
+    from oracle import pipecg
+    monkeypatch.setenv("KRYLOV_AMD_SHARDS", ",".join(["0"] * shards))
+    mod = importlib.import_module(f"parallel_krylov_amd.v1.threads.pipeline.{method}")
+    A = golden_matrix(spec)
+    b = np.random.default_rng(1).standard_normal(A.shape[0])
+    ilu = _spilu(A, drop_tol)
+    _, n_o, r_o, x_o, c_o = pipecg.METHODS[method](A, b, pipecg.IluSweeps(ilu), 1e-10,
+                                                  return_x=True)
+    out = io.StringIO()
+    with contextlib.redirect_stdout(out):
+        _, nosl, res, x, conv = getattr(mod, method)(A, b, ilu, 1e-10, return_x=True)
+    assert conv and c_o and "status:\t\tconverged" in out.getvalue()
+    assert np.array_equal(nosl, n_o), (len(nosl), len(n_o))
+    keep = r_o >= 1e-8
+    rel = np.abs(res - r_o) / r_o
+    assert rel[keep].max() < RTOL[method], rel[keep].max()
+    xh = x.cpu().numpy()
+    assert np.linalg.norm(xh - x_o) / np.linalg.norm(x_o) < XTOL[method]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method", METHODS)
+def test_gpu_ilu_against_superlu_solve(method):
+    """The same solve against the oracle driven by SuperLU's own `solve` (the
+    reference's call, pcg.py:41): the preconditioner applications differ in
+    rounding only, so the iteration counts agree to one and both converge."""
+    import importlib
+    from oracle import pipecg
+    mod = importlib.import_module(f"parallel_krylov_amd.v1.threads.pipeline.{method}")
+    A = golden_matrix(("poisson", 32, 2))
+    b = np.random.default_rng(1).standard_normal(A.shape[0])
+    ilu = _spilu(A, 1e-2)
+    _, n_o, r_o = pipecg.METHODS[method](A, b, ilu, 1e-10)
+    with contextlib.redirect_stdout(io.StringIO()):
+        _, nosl, res = getattr(mod, method)(A, b, ilu, 1e-10)
+    assert abs(len(res) - len(r_o)) <= 1 and res[-1] < 1e-10
+    m = min(len(res), len(r_o)) - 2
+    assert np.max(np.abs(res[:m] - r_o[:m]) / r_o[:m]) < 1e-6
+
+
+@pytest.mark.gpu
+def test_gpu_ilu_refused_on_several_shards():
+    """kr_solve_set_precond_ilu on a multi-shard system is an error, not a
+    silent per-shard (block) ILU."""
+    import scipy.sparse.linalg as spla
+    from parallel_krylov_amd._lib import KrylovError
+    from parallel_krylov_amd.system import KrylovSystem, balanced_partition
+    A = golden_matrix(("poisson", 16, 2))
+    n = A.shape[0]
+    sysm = KrylovSystem(n, balanced_partition(n, 2), [0, 0])
+    try:
+        sysm.set_matrix(A)
+        sysm.finalize()
+        ilu = spla.spilu(A.tocsc())
+        with pytest.raises(KrylovError, match="one-shard"):
+            sysm.set_precond_ilu((ilu.L, ilu.U, ilu.perm_r, ilu.perm_c))
+    finally:
+        sysm.close()
