@@ -337,7 +337,7 @@ std::unique_ptr<IluFactors> build_ilu(int dev, hipStream_t stream, int64_t n, co
     void* d = nullptr;
     KR_HIP_CHECK(hipMalloc(&d, std::max<size_t>(bytes, 8)));
     f->owned.push_back(d);
-    if (bytes) KR_HIP_CHECK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream));
+    if (h && bytes) KR_HIP_CHECK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream));
     return d;
   };
   for (int side = 0; side < 2; ++side) {
@@ -364,6 +364,70 @@ std::unique_ptr<IluFactors> build_ilu(int dev, hipStream_t stream, int64_t n, co
   f->z = static_cast<double*>(up(nullptr, 8 * (size_t)n));
   KR_HIP_CHECK(hipStreamSynchronize(stream));  // the host vectors go out of scope
   return f;
+}
+
+bool stencil_pm(int P);
+
+bool System::pair_ok() const {
+  if (shards.size() != 1 || comm || nglobal_shards() != 1) return false;
+  // opt-in (KR_ST2=1): measured slower than two dual launches
+  const char* env = getenv("KR_ST2");
+  if (!(env && atoi(env) != 0)) return false;
+  const Shard& s = shards[0];
+  if (!s.scode || !stencil_pm(s.st_P) || s.nm != 7 || s.st_nfar != 2) return false;
+  if (s.st_far[0] != -kStencilBlock || s.st_far[1] != kStencilBlock) return false;
+  if (s.st_cb != 2 && s.st_cb != 4) return false;
+  const int64_t W = (int64_t)s.st_P * kStencilBlock;
+  static const int kPat[7] = {1, 4, 3, 0, 3, 5, 2};  // kPat7: PREV FAR0 NEAR CENTER NEAR FAR1 NEXT
+  for (int k = 0; k < 7; ++k)
+    if (s.st_kind[k] != kPat[k]) return false;
+  return s.n % W == 0 && s.n / W >= 2 && s.spmv_grid2 % s.st_P == 0;
+}
+
+void System::spmv_pair(int in1, int in2, int out1, int out2, int slot0) {
+  KR_REQUIRE(pair_ok(), "fused basis pair: shard not eligible");
+  KR_REQUIRE(slot0 + 14 <= kMaxSlots, "reduction slots exhausted");
+  Shard& s = shards[0];
+  KR_HIP_CHECK(hipSetDevice(s.dev));
+  const bool po = products_only && products_only_on;
+  const char* nm = po ? "spmv2x2_gram_mrr_last" : "spmv2x2_gram_mrr";
+  hipEvent_t t0 = nullptr;
+  prof_begin(s, nm, t0);
+  SpmvArgs a;
+  a.n = s.n;
+  a.x1 = s.vec[in1];
+  a.x2 = s.vec[in2];
+  a.xoff = s.pad;
+  a.y1 = s.own(out1);
+  a.y2 = s.own(out2);
+  a.partials = s.partials + (size_t)slot0 * s.pstride;
+  a.partials2 = s.partials + (size_t)(slot0 + 7) * s.pstride;
+  a.grid = s.pstride;
+  a.vtab = s.vtab;
+  a.ntab = s.ntab;
+  a.scode = s.scode;
+  a.st_cb = s.st_cb;
+  a.st_P = s.st_P;
+  a.st_pm = 1;
+  a.st_nm = s.nm;
+  a.st_nfar = s.st_nfar;
+  for (int k = 0; k < 8; ++k) {
+    a.st_off[k] = k < s.nm ? s.moff_h[k] : 0;
+    a.st_kind[k] = s.st_kind[k];
+  }
+  for (int f = 0; f < 4; ++f) a.st_far[f] = s.st_far[f];
+  a.xlen = s.ld;
+  a.scratch = s.scratch;
+  a.products_only = po ? 1 : 0;
+  a.stop = dev_stop ? s.st + ST_STOP : nullptr;
+  launch_spmv_stencil2(a, s.spmv_grid2, s.stream);
+  for (int p = 0; p < 14; ++p) s.slot_n[slot0 + p] = s.spmv_grid2;
+  // algorithmic bytes in CSR terms, like every SpMV's (bench.py subtracts the
+  // stored format's saving): A once, the two input vectors and the two
+  // level-2 outputs (none products-only) -- one dual SpMV's; level 1 never
+  // leaves the chip
+  const double bytes = 12.0 * s.nnz + 4.0 * (s.n + 1) + 16.0 * s.n + (po ? 0.0 : 16.0 * s.n);
+  prof_end(s, nm, t0, bytes);
 }
 
 // M^-1 v (shard 0): w = Pr v folded into the L sweep's loads, y = L^-1 w,
@@ -879,6 +943,18 @@ void System::finalize() {
       const int zmax = ze ? atoi(ze) : 16;
       s.spmv_grid_po = s.scode && zmax > 0 && stencil_pm(s.st_P)
                            ? stencil_grid(s.n, s.st_P, zmax) : s.spmv_grid;
+    }
+    // The fused basis pair (spmv_stencil2_kernel) walks longer segments on
+    // >= 512-plane shards: every segment start re-walks 3 planes (64-plane
+    // segments: 5 %; the general grid's 16: 19 %). Smaller shards keep the
+    // general grid, so the products' summation order there is the two dual
+    // launches' (the GPU-order oracle stays exact). KR_ST2_Z caps the segments.
+    {
+      const char* ze = getenv("KR_ST2_Z");
+      const int z2 = ze ? atoi(ze) : 8;
+      const int64_t planes = s.scode && s.st_P > 0 ? s.n / ((int64_t)s.st_P * kStencilBlock) : 0;
+      s.spmv_grid2 = s.scode && stencil_pm(s.st_P) && planes >= 512 && z2 > 0
+                         ? stencil_grid(s.n, s.st_P, z2) : s.spmv_grid;
     }
     s.pstride = std::max(s.grid, s.spmv_grid);
     s.slot_n.fill(0);
@@ -2245,12 +2321,23 @@ class KskipMrrSession : public Base {
 
   void head() { sys->spmv(EPI_HEAD_MRR, r0, -1, AR(1), -1, y0, -1, 0); }
   void chain(int kk) {
-    for (int m = 0; m < kk; ++m) {
+    // Two basis duals per launch where the shard allows (System::spmv_pair:
+    // Ar[m+2], Ay[m+1] stay on chip); an odd count ends with a single dual.
+    const bool pairs = sys->pair_ok();
+    for (int m = 0; m < kk;) {
+      if (pairs && m + 1 < kk) {
+        sys->products_only = m + 1 == kk - 1;
+        sys->spmv_pair(AR(m + 1), m == 0 ? y0 : AY(m), AR(m + 3), AY(m + 2), kHead + 7 * m);
+        sys->products_only = false;
+        m += 2;
+        continue;
+      }
       // the last pair (Ar[kk+1], Ay[kk]) feeds only the Gram products
       sys->products_only = m == kk - 1;
       sys->spmv(EPI_DUAL_MRR, AR(m + 1), m == 0 ? y0 : AY(m), AR(m + 2), AY(m + 1), -1, -1,
                 kHead + 7 * m);
       sys->products_only = false;
+      ++m;
     }
   }
   // Initial / restart MrR step (v3/cpu/kskipmrr.py:26-31).

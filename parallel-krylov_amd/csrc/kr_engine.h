@@ -108,6 +108,7 @@ struct Shard {
   int grid = 1;                 // workgroups of the vector kernels
   int spmv_grid = 1;            // workgroups of the SpMV kernels
   int spmv_grid_po = 1;         // ... of a products-only stencil launch (<= spmv_grid)
+  int spmv_grid2 = 1;           // ... of the fused basis pair (System::spmv_pair, <= spmv_grid)
   int pstride = 1;              // partial stride per slot: max(grid, spmv_grid)
   std::array<int, kMaxSlots> slot_n{};  // partials written per slot by its last producer
   // reductions
@@ -221,6 +222,14 @@ struct System {
   void halo_async(int id1, int id2, int id3 = -1);
   void spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int b, int slot0,
             const StepOps* st = nullptr);
+  // Two chained EPI_DUAL_MRR basis SpMVs in one launch (spmv_stencil2_kernel):
+  // (in1, in2) -> level 2 in (out1, out2) (not stored under products_only),
+  // products of the first dual at slot0, of the second at slot0 + 7.
+  // pair_ok(): one shard, no communicator, a 7-point stencil shard with n =
+  // 512 and whole planes, narrow codes, and KR_ST2=1 (opt-in: slower than
+  // the two dual launches on MI355X).
+  bool pair_ok() const;
+  void spmv_pair(int in1, int in2, int out1, int out2, int slot0);
   void ew(EwOp op, double c0, double c1, std::array<int, 6> ids, int slot0);
   // The same for ops with more than 6 operands (-1: unused slot).
   void ew_n(EwOp op, double c0, double c1, const std::array<int, kEwOps>& ids, int slot0);

@@ -156,6 +156,8 @@ struct SpmvArgs {
   // 1: the caller needs only the products (the last basis SpMV of a k-skip
   // outer iteration): a kernel MAY skip storing y1/y2 (the stencil walk does)
   int products_only = 0;
+  // the fused basis pair (launch_spmv_stencil2): products of the second dual
+  double* partials2 = nullptr;
   int64_t nnz_total = -1;  // entries of val/col (-1: unknown; spmv_kernel2 needs >= 4)
   // Dense row block (gemv_kernel): val is n x ncols row-major with leading
   // dimension dld; x1 + xcol0 (x2 + xcol0) is the full input vector.
@@ -223,6 +225,11 @@ constexpr double kLongRow = 12.0;
 void launch_spmv(SpmvEpi epi, const SpmvArgs& a, hipStream_t s);
 // Same with gridDim = nblocks (<= a.grid, the partial stride).
 void launch_spmv_grid(SpmvEpi epi, const SpmvArgs& a, int nblocks, hipStream_t s);
+// Two chained k-skip MrR basis SpMVs in one walk (kr_stencil.h
+// spmv_stencil2_kernel): x1, x2 = (Ar[m+1], Ay[m]) -> y1, y2 = (Ar[m+3],
+// Ay[m+2]) (not stored when products_only), EPI_DUAL_MRR products of dual m
+// at partials, of dual m+1 at partials2. 7-point stencil shards with n = 512.
+void launch_spmv_stencil2(const SpmvArgs& a, int nblocks, hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // Elementwise vector steps with fused reductions (all own-row pointers).

@@ -8,4 +8,10 @@
 
 namespace kr {
 template void spmv_launch_epi<KR_EPI>(const SpmvArgs& a, int nblocks, hipStream_t s);
+#if KR_EPI == 7
+static_assert(EPI_DUAL_MRR == 7, "the fused basis pair is built with EPI_DUAL_MRR's unit");
+void launch_spmv_stencil2(const SpmvArgs& a, int nblocks, hipStream_t s) {
+  spmv_stencil2_launch(a, nblocks, s);
+}
+#endif
 }  // namespace kr

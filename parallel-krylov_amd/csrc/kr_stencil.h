@@ -616,3 +616,335 @@ void spmv_stencil_launch(const SpmvArgs& a, int nblocks, hipStream_t s) {
   else
     spmv_stencil_launch_r<E, false>(a, nblocks, s);
 }
+
+// ---------------------------------------------------------------------------
+// Two chained basis SpMVs in ONE walk (k-skip MrR, SpmvArgs x1 = Ar[m+1],
+// x2 = Ay[m]): level 1 = (Ar[m+2], Ay[m+1]) = A (x1, x2) and level 2 =
+// (Ar[m+3], Ay[m+2]) = A level 1, with both duals' Gram products
+// (EPI_DUAL_MRR for m -> partials, for m+1 -> partials2) and only level 2
+// stored (nothing when PO: the last pair of an outer iteration). Level 1 is
+// never written to HBM: the pair moves the bytes of ONE dual SpMV.
+//
+// 7-point pattern with n = 512 (the +-n offsets are the neighbouring 512-row
+// blocks of a plane; W = P blocks). A workgroup walks one column (position p)
+// of the plane segment [z0, z1): level 2 of block p at plane z needs level 1
+// of blocks p-1 .. p+1 (region R1) at plane z and of block p at z +- 1, and
+// level 1 of R1 needs level 0 of blocks p-2 .. p+2 (R0) at its plane and of
+// R1 at the planes beside it. Rows are linear indices throughout (block p-1
+// of position 0 is the last block of the previous plane), so the regions are
+// contiguous row ranges and every neighbour is the same row arithmetic as in
+// the single SpMV; rows outside the vectors read 0 (buffer range check) and
+// only feed entries the codes mark absent.
+//
+// Lane t owns rows 2t, 2t+1 of every block, so the +-n neighbours of an R1
+// row are the same lane's registers (adjacent blocks); only +-1 crosses
+// lanes and goes through LDS (one ds_read2_b64 per block). Every row is
+// summed in stored (ascending offset) order from 0.0: -W, -n, -1, 0, +1, +n
+// are added when the row's plane arrives (partial sums p1 / p2), +W when the
+// next plane does -- bitwise the single SpMV. Step s (planes z0-1 .. z1+1):
+// L0[s] arrives (loaded one step ahead) -> L1[s-1] = p1 + (+W term), p1 =
+// partial of L1[s]; L1[s-1] -> L2[s-2] = p2 + (+W), p2 = partial of L2[s-1].
+// Products: (L0, L1) of plane s-1 and (L1, L2) of plane s-2, each plane in
+// order, row 2t then 2t+1 -- the accumulation order of the two dual launches
+// on the same grid (oracle/gpu_order.py).
+// ---------------------------------------------------------------------------
+constexpr int kS2B0 = 5;  // level-0 blocks per plane (R0)
+constexpr int kS2B1 = 3;  // level-1 blocks per plane (R1)
+
+// Slots k0 .. k1-1 of rows lo / hi (codes clo / chi) for BOTH chains: the
+// slot's code and table value are decoded once and serve the two chains; a
+// slot present in every row of the wave (everywhere but the grid faces: the
+// ballot) adds without the absent-entry selects.
+template <int CB, int K0, int K1>
+__device__ __forceinline__ void st2_terms(uint32_t clo, uint32_t chi,
+                                          const double* __restrict__ tab,
+                                          const double (&xlo)[2][7], const double (&xhi)[2][7],
+                                          double (&slo)[2], double (&shi)[2]) {
+  constexpr unsigned kNone = (1u << CB) - 1u;
+#pragma unroll
+  for (int k = K0; k < K1; ++k) {
+    const unsigned cl = (clo >> (CB * k)) & kNone, ch = (chi >> (CB * k)) & kNone;
+    const double vl = tab[cl], vh = tab[ch];  // tab[kNone]: a valid unused slot
+    if (__builtin_amdgcn_ballot_w64(cl == kNone || ch == kNone) == 0) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        slo[c] = slo[c] + vl * xlo[c][k];
+        shi[c] = shi[c] + vh * xhi[c][k];
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const double tl = slo[c] + vl * xlo[c][k], th = shi[c] + vh * xhi[c][k];
+        slo[c] = cl != kNone ? tl : slo[c];
+        shi[c] = ch != kNone ? th : shi[c];
+      }
+    }
+  }
+}
+
+template <int CB, bool PO>
+__global__ __launch_bounds__(kBlock, 2) void spmv_stencil2_kernel(SpmvArgs a) {
+  if (a.stop && *a.stop != 0.0) return;
+  static_assert(CB == 2 || CB == 4, "fused basis pair: narrow codes");
+  extern __shared__ __attribute__((aligned(16))) double s2_dyn[];
+  double* s_l0 = s2_dyn;                             // [2][kS2B0 * 512]
+  double* s_l1 = s2_dyn + 2 * kS2B0 * kSBlock;       // [2][kS2B1 * 512]
+  __shared__ double s_tab[kVdMax];
+  __shared__ double s_red1[7 * 4], s_red2[7 * 4];
+  const int tid = threadIdx.x;
+  if (tid < a.ntab) s_tab[tid] = a.vtab[tid];
+
+  double acc1[7], acc2[7];
+#pragma unroll
+  for (int q = 0; q < 7; ++q) acc1[q] = acc2[q] = 0.0;
+
+  // ---- the column: position-major grid (kr_stencil.h), segment [z0, z1)
+  const int64_t P = a.st_P;
+  const int64_t W = P * kSBlock;
+  const int64_t planes = a.n / W;  // whole planes (the host checks)
+  const int64_t q = blockIdx.x & 7, w = blockIdx.x >> 3;
+  const int64_t PP = P >> 3, Zt = gridDim.x / P;
+  const int64_t p = q * PP + w % PP;
+  const int64_t zs = w / PP;
+  const int64_t z0 = planes * zs / Zt, z1 = planes * (zs + 1) / Zt;
+
+  const double* const xs[3] = {a.x1, a.x2, a.x2};
+  const SRes res = st_res<2, CB>(a, xs);
+  const uint32_t lb = (uint32_t)tid * 16u;
+  // first row of R0 / R1 at plane z (linear, may be negative)
+  auto r0_of = [&](int64_t z) { return z * W + (p - 2) * kSBlock; };
+  auto ld = [&](int c, int64_t row) {  // the lane's pair at row + 2 tid of vector c
+    return st_bld2(res.x[c], (uint32_t)((a.xoff + row) * 8) + lb);
+  };
+  auto codes = [&](int64_t row) {  // both rows' codes, packed (CB = 2: 16 bits each)
+    if constexpr (CB == 2)
+      return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(
+          res.code, (uint32_t)(row * 2) + (uint32_t)tid * 4u, 0, 2);
+    else
+      return (uint32_t)0;
+  };
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  auto codes4 = [&](int64_t row) {  // CB = 4: a uint32 per row
+    return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(
+                                         res.code, (uint32_t)(row * 4) + (uint32_t)tid * 8u, 0, 2));
+  };
+  auto lo_code = [&](uint32_t c2, u32x2 c4) { return CB == 2 ? (c2 & 0xFFFFu) : c4.x; };
+  auto hi_code = [&](uint32_t c2, u32x2 c4) { return CB == 2 ? (c2 >> 16) : c4.y; };
+
+  // ---- registers
+  dbl2v nx[2][kS2B0];             // level 0 of the arriving plane (loaded a step ahead)
+  uint32_t ncode2[kS2B1];         // its R1 codes
+  u32x2 ncode4[kS2B1];
+  dbl2v l0p[2][kS2B1];            // level 0 of the previous plane, R1 blocks
+  dbl2v p1[2][kS2B1];             // partial level-1 sums of the previous plane
+  uint32_t c1p2[kS2B1];           // R1 codes of the previous plane
+  u32x2 c1p4[kS2B1];
+  dbl2v l1p[2];                   // level 1 two planes back, block p
+  dbl2v p2[2];                    // partial level-2 sums, plane s-2 ... (see below)
+  uint32_t c2p2 = 0;              // block p's codes two planes back
+  u32x2 c2p4 = {0u, 0u};
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    l1p[c] = dbl2v{0.0, 0.0};
+    p2[c] = dbl2v{0.0, 0.0};
+#pragma unroll
+    for (int j = 0; j < kS2B1; ++j) p1[c][j] = dbl2v{0.0, 0.0};
+  }
+#pragma unroll
+  for (int j = 0; j < kS2B1; ++j) {
+    c1p2[j] = 0u;
+    c1p4[j] = u32x2{0u, 0u};
+  }
+
+  auto issue = [&](int64_t z) {  // plane z's level 0 (R0) and R1 codes
+    const int64_t r0 = r0_of(z);
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int j = 0; j < kS2B0; ++j) nx[c][j] = ld(c, r0 + j * kSBlock);
+#pragma unroll
+    for (int j = 0; j < kS2B1; ++j) {
+      if constexpr (CB == 2)
+        ncode2[j] = codes(r0 + (j + 1) * kSBlock);
+      else
+        ncode4[j] = codes4(r0 + (j + 1) * kSBlock);
+    }
+  };
+
+  if (z0 < z1) {
+    // prologue: level 0 of plane z0-2 (R1 blocks: the -W operand of plane
+    // z0-1's level-1 rows), then plane z0-1 in flight
+    const int64_t r0 = r0_of(z0 - 2);
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int j = 0; j < kS2B1; ++j) l0p[c][j] = ld(c, r0 + (j + 1) * kSBlock);
+    issue(z0 - 1);
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  __syncthreads();                      // s_tab
+
+  for (int64_t s = z0 - 1; s <= z1 + 1 && z0 < z1; ++s) {
+    // (1) the arriving plane s: own copies, then the next plane's loads
+    dbl2v l0[2][kS2B0];
+    uint32_t cc2[kS2B1];
+    u32x2 cc4[kS2B1];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int j = 0; j < kS2B0; ++j) l0[c][j] = nx[c][j];
+#pragma unroll
+    for (int j = 0; j < kS2B1; ++j) {
+      cc2[j] = ncode2[j];
+      cc4[j] = ncode4[j];
+    }
+    issue(s + 1 <= z1 + 1 ? s + 1 : s);  // (the last step re-reads its own plane)
+    // (2) level 0 of plane s into LDS (the +-1 neighbours)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int j = 0; j < kS2B0; ++j)
+        reinterpret_cast<dbl2v*>(s_l0 + c * kS2B0 * kSBlock + j * kSBlock)[tid] = l0[c][j];
+    __syncthreads();
+    // (3) level 1 of plane s-1 (R1) completed by its +W term; the products of
+    // (level 0, level 1) at plane s-1; partial level-1 sums of plane s
+    dbl2v l1[2][kS2B1];
+#pragma unroll
+    for (int j = 0; j < kS2B1; ++j) {
+      // +W (slot 6) of plane s-1: x at plane s, same block
+      {
+        double xl[2][7], xh[2][7], sl[2], sh[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          xl[c][6] = l0[c][j + 1].x;
+          xh[c][6] = l0[c][j + 1].y;
+          sl[c] = p1[c][j].x;
+          sh[c] = p1[c][j].y;
+        }
+        st2_terms<CB, 6, 7>(lo_code(c1p2[j], c1p4[j]), hi_code(c1p2[j], c1p4[j]), s_tab, xl, xh,
+                            sl, sh);
+#pragma unroll
+        for (int c = 0; c < 2; ++c) l1[c][j] = dbl2v{sl[c], sh[c]};
+      }
+      // plane s: -W (l0p), -n (block j), -1 (LDS / own), 0, +1 (own / LDS), +n (block j+2)
+      double xl[2][7], xh[2][7], sl[2] = {0.0, 0.0}, sh[2] = {0.0, 0.0};
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const double* line = s_l0 + c * kS2B0 * kSBlock + (j + 1) * kSBlock + 2 * tid;
+        xl[c][0] = l0p[c][j].x;     xh[c][0] = l0p[c][j].y;
+        xl[c][1] = l0[c][j].x;      xh[c][1] = l0[c][j].y;
+        xl[c][2] = line[-1];        xh[c][2] = l0[c][j + 1].x;
+        xl[c][3] = l0[c][j + 1].x;  xh[c][3] = l0[c][j + 1].y;
+        xl[c][4] = l0[c][j + 1].y;  xh[c][4] = line[2];
+        xl[c][5] = l0[c][j + 2].x;  xh[c][5] = l0[c][j + 2].y;
+      }
+      st2_terms<CB, 0, 6>(lo_code(cc2[j], cc4[j]), hi_code(cc2[j], cc4[j]), s_tab, xl, xh, sl, sh);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) p1[c][j] = dbl2v{sl[c], sh[c]};
+    }
+    const bool l1ok = s - 1 >= z0 - 1;  // level 1 of plane s-1 is real (s > z0-1)
+    if (l1ok && s - 1 >= z0 && s - 1 < z1) {
+      // dual m at plane s-1, block p: x = Ar[m+1] (l0p r), x2 = Ay[m] (l0p y)
+      epi_products<EPI_DUAL_MRR>(l0p[0][1].x, l0p[1][1].x, l1[0][1].x, l1[1][1].x, 0.0, acc1);
+      epi_products<EPI_DUAL_MRR>(l0p[0][1].y, l0p[1][1].y, l1[0][1].y, l1[1][1].y, 0.0, acc1);
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int j = 0; j < kS2B1; ++j) l0p[c][j] = l0[c][j + 1];
+    // (4) level 1 of plane s-1 into LDS
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int j = 0; j < kS2B1; ++j)
+        reinterpret_cast<dbl2v*>(s_l1 + c * kS2B1 * kSBlock + j * kSBlock)[tid] = l1[c][j];
+    __syncthreads();
+    // (5) level 2 of plane s-2 (block p) completed by its +W term (level 1 of
+    // plane s-1); products of (level 1, level 2) at s-2; store; partial sums
+    // of plane s-1
+    {
+      dbl2v l2[2];
+      {
+        double xl[2][7], xh[2][7], sl[2], sh[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          xl[c][6] = l1[c][1].x;
+          xh[c][6] = l1[c][1].y;
+          sl[c] = p2[c].x;
+          sh[c] = p2[c].y;
+        }
+        st2_terms<CB, 6, 7>(lo_code(c2p2, c2p4), hi_code(c2p2, c2p4), s_tab, xl, xh, sl, sh);
+#pragma unroll
+        for (int c = 0; c < 2; ++c) l2[c] = dbl2v{sl[c], sh[c]};
+      }
+      if (s - 2 >= z0 && s - 2 < z1) {
+        epi_products<EPI_DUAL_MRR>(l1p[0].x, l1p[1].x, l2[0].x, l2[1].x, 0.0, acc2);
+        epi_products<EPI_DUAL_MRR>(l1p[0].y, l1p[1].y, l2[0].y, l2[1].y, 0.0, acc2);
+        if constexpr (!PO) {
+          const int64_t row = (s - 2) * W + p * kSBlock + 2 * tid;
+          __builtin_nontemporal_store(l2[0], reinterpret_cast<dbl2v*>(a.y1 + row));
+          __builtin_nontemporal_store(l2[1], reinterpret_cast<dbl2v*>(a.y2 + row));
+        }
+      }
+      {
+        double xl[2][7], xh[2][7], sl[2] = {0.0, 0.0}, sh[2] = {0.0, 0.0};
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const double* line = s_l1 + c * kS2B1 * kSBlock + kSBlock + 2 * tid;
+          xl[c][0] = l1p[c].x;       xh[c][0] = l1p[c].y;
+          xl[c][1] = l1[c][0].x;     xh[c][1] = l1[c][0].y;
+          xl[c][2] = line[-1];       xh[c][2] = l1[c][1].x;
+          xl[c][3] = l1[c][1].x;     xh[c][3] = l1[c][1].y;
+          xl[c][4] = l1[c][1].y;     xh[c][4] = line[2];
+          xl[c][5] = l1[c][2].x;     xh[c][5] = l1[c][2].y;
+        }
+        st2_terms<CB, 0, 6>(lo_code(c1p2[1], c1p4[1]), hi_code(c1p2[1], c1p4[1]), s_tab, xl, xh,
+                            sl, sh);
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          p2[c] = dbl2v{sl[c], sh[c]};
+          l1p[c] = l1[c][1];
+        }
+      }
+      c2p2 = c1p2[1];
+      c2p4 = c1p4[1];
+    }
+#pragma unroll
+    for (int j = 0; j < kS2B1; ++j) {
+      c1p2[j] = cc2[j];
+      c1p4[j] = cc4[j];
+    }
+  }
+  __syncthreads();
+  block_reduce_store<7>(acc1, a.partials, a.grid, s_red1, 0);
+  block_reduce_store<7>(acc2, a.partials2, a.grid, s_red2, 0);
+}
+
+// Dynamic LDS of the fused pair: level 0 (5 blocks) and level 1 (3 blocks) of
+// one plane, two chains.
+constexpr size_t kS2Lds = sizeof(double) * 2 * (kS2B0 + kS2B1) * kSBlock;
+
+template <int CB, bool PO>
+void st2_launch_t(const SpmvArgs& a, int nblocks, hipStream_t s) {
+  static bool opted = false;
+  if (!opted) {
+    KR_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(spmv_stencil2_kernel<CB, PO>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kS2Lds));
+    opted = true;
+  }
+  spmv_stencil2_kernel<CB, PO><<<nblocks, kBlock, kS2Lds, s>>>(a);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
+inline void spmv_stencil2_launch(const SpmvArgs& a, int nblocks, hipStream_t s) {
+  KR_REQUIRE(a.scode && a.st_P % 8 == 0 && a.st_nm == 7 && a.st_nfar == 2 &&
+                 a.st_far[0] == -kSBlock && a.st_far[1] == kSBlock &&
+                 a.n % ((int64_t)a.st_P * kSBlock) == 0 && a.rb_gap == 0 && a.partials2 &&
+                 nblocks % a.st_P == 0 && (a.st_cb == 2 || a.st_cb == 4),
+             "fused basis pair: 7-point stencil with n = 512, whole planes, narrow codes");
+  const bool po = a.products_only != 0;
+  if (a.st_cb == 2)
+    po ? st2_launch_t<2, true>(a, nblocks, s) : st2_launch_t<2, false>(a, nblocks, s);
+  else
+    po ? st2_launch_t<4, true>(a, nblocks, s) : st2_launch_t<4, false>(a, nblocks, s);
+}

@@ -98,15 +98,20 @@ MATRICES = {
     "vals3_32x32x7": lambda: revalued(box(32, 32, 7), 3),      # 3 values: 2-bit, code 2 used
     "vals15_64x64x9": lambda: revalued(box(64, 64, 9), 15),    # 15 values: 4-bit, P = 8
     "vals40_32x32x7": lambda: revalued(box(32, 32, 7), 40),    # 40 values: 8-bit codes
+    # n = 512 (the +-n offsets are whole 512-row blocks): the fused basis pair
+    "box512x8x16": lambda: box(512, 8, 16),                    # W = 4096: P = 8
+    "box512x16x12": lambda: box(512, 16, 12),                  # P = 16, 12 planes
+    "aniso512x8x12": lambda: aniso(512, 8, 12, 1.0, 0.5, 0.25),  # 4-bit codes
 }
 # stencil code width (bits per slot) the engine picks for the 7-point pattern
 EXPECT_CB = {"aniso32x32x7": 4, "vals3_32x32x7": 2, "vals15_64x64x9": 4, "vals40_32x32x7": 8,
-             "p3d32": 2, "p3d64": 2, "box64x64x20": 2}
+             "p3d32": 2, "p3d64": 2, "box64x64x20": 2, "box512x8x16": 2, "aniso512x8x12": 4}
 # expected stencil walk P (0: the row walk serves the matrix)
 EXPECT_P = {"p3d32": 2, "p3d64": 8, "box32x32x7": 2, "box64x16x9": 2, "box48x32x5": 3,
             "box32x32x3": 2, "p2d512x6": 1, "band_far": 1, "band_far2": 2,
             "box64x64x20": 8, "box128x32x9": 8, "aniso32x32x7": 2, "vals3_32x32x7": 2,
-            "vals15_64x64x9": 8, "vals40_32x32x7": 2}
+            "vals15_64x64x9": 8, "vals40_32x32x7": 2, "box512x8x16": 8, "box512x16x12": 16,
+            "aniso512x8x12": 8}
 NOT_STENCIL = {
     "p3d24": lambda: golden_matrix(["poisson", 24, 3]),      # 576 % 512 != 0
     "p3d16": lambda: golden_matrix(["poisson", 16, 3]),
@@ -211,12 +216,24 @@ CASES = [
     ("kskipmrr", "box64x64x20", 4, 1), ("adaptivekskipmrr", "box64x64x20", 6, 2),
     ("kskipcg", "box128x32x9", 3, 3), ("kskipmrr", "aniso32x32x7", 4, 1),
     ("adaptivekskipmrr", "aniso32x32x7", 8, 2),
+    # the fused basis pair (one shard, n = 512): level 1 stays on chip, both
+    # duals' products summed in the dual launches' order
+    ("kskipmrr", "box512x8x16", 4, 1), ("kskipmrr", "box512x16x12", 5, 1),
+    ("adaptivekskipmrr", "box512x16x12", 8, 1), ("kskipmrr", "aniso512x8x12", 2, 1),
+    ("kskipmrr", "box512x8x16", 4, 2),
 ]
+# cases also run with the fused basis pair (opt-in KR_ST2=1)
+PAIR_ORACLE = {("kskipmrr", "box512x8x16", 4, 1), ("kskipmrr", "box512x16x12", 5, 1),
+               ("adaptivekskipmrr", "box512x16x12", 8, 1), ("kskipmrr", "aniso512x8x12", 2, 1)}
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("st2", ["0", "1"])
 @pytest.mark.parametrize("method,name,k,shards", CASES)
-def test_stencil_solvers_bitwise_gpu_order_oracle(monkeypatch, method, name, k, shards):
+def test_stencil_solvers_bitwise_gpu_order_oracle(monkeypatch, method, name, k, shards, st2):
+    if st2 == "1" and (method, name, k, shards) not in PAIR_ORACLE:
+        pytest.skip("the fused basis pair serves one-shard n = 512 stencils only")
+    monkeypatch.setenv("KR_ST2", st2)
     A = MATRICES[name]()
     n = A.shape[0]
     b = np.random.default_rng(1).standard_normal(n)
@@ -277,3 +294,64 @@ def test_stencil_cg_mrr_match_reference_contract(method):
     rel = np.abs(info["residual"] - ref["residual"]) / ref["residual"]
     assert rel.max() <= 1e-12
     assert np.linalg.norm(x.cpu().numpy() - x_ref) <= 1e-11 * np.linalg.norm(x_ref)
+
+
+PAIR_CASES = [("kskipmrr", "box512x8x16", 2), ("kskipmrr", "box512x8x16", 3),
+              ("kskipmrr", "box512x16x12", 4), ("kskipmrr", "aniso512x8x12", 5),
+              ("adaptivekskipmrr", "box512x16x12", 6), ("adaptivekskipmrr", "aniso512x8x12", 8)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method,name,k", PAIR_CASES)
+def test_stencil_pair_bitwise_equal_duals(monkeypatch, method, name, k):
+    """The fused basis pair (spmv_stencil2_kernel: two chained duals in one
+    walk, level 1 kept on chip) against the dual SpMVs (KR_ST2=0): the same
+    rows summed the same way and the same products in the same order, so the
+    histories and x are equal bit for bit -- odd k ends with a single dual,
+    adaptive k shrinks through rollbacks."""
+    A = MATRICES[name]()
+    b = np.random.default_rng(5).standard_normal(A.shape[0])
+    kw = dict(tol=1e-10, maxiter=400, k=k)
+    monkeypatch.setenv("KRYLOV_AMD_SHARDS", "0")
+    out = []
+    for st2 in ("0", "1"):
+        monkeypatch.setenv("KR_ST2", st2)
+        with contextlib.redirect_stdout(io.StringIO()):
+            x, info = _solver(method)(A, b, **kw)
+        out.append((x.cpu().numpy(), info))
+    (x0, i0), (x1, i1) = out
+    np.testing.assert_array_equal(i1["nosl"], i0["nosl"])
+    if "khistory" in i0:
+        np.testing.assert_array_equal(i1["khistory"], i0["khistory"])
+    np.testing.assert_array_equal(i1["residual"], i0["residual"])
+    np.testing.assert_array_equal(x1, x0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,k,pairs,st2", [("box512x8x16", 4, True, "1"),
+                                              ("box512x8x16", 3, True, "1"),
+                                              ("box512x8x16", 4, False, "0"),
+                                              ("p3d64", 4, False, "1")])
+def test_stencil_pair_is_used(monkeypatch, name, k, pairs, st2):
+    """With KR_ST2=1 the k-skip MrR basis runs as fused pairs exactly where the
+    shard qualifies (n = 512, one shard): k // 2 pair launches per outer
+    iteration, the last one products-only for even k, and k % 2 single duals;
+    by default (no KR_ST2) the dual launches."""
+    monkeypatch.setenv("KR_ST2", st2)
+    A = MATRICES[name]()
+    sysm = _system(A, 1)
+    try:
+        b = sysm.split(np.random.default_rng(1).standard_normal(A.shape[0]))
+        sysm.begin("kskipmrr", b, None, tol=0.0, maxiter=8 * (k + 1) + 2, k=k, profile=1)
+        sysm.step(4)
+        st = {r["name"]: r["launches"] for r in sysm.kernel_stats()}
+        sysm.finish("kskipmrr")
+    finally:
+        sysm.close()
+    npair = st.get("spmv2x2_gram_mrr", 0) + st.get("spmv2x2_gram_mrr_last", 0)
+    ndual = st.get("spmv2_gram_mrr", 0) + st.get("spmv2_gram_mrr_last", 0)
+    if pairs:
+        assert npair == 4 * (k // 2) and ndual == 4 * (k % 2), st
+        assert st.get("spmv2x2_gram_mrr_last", 0) == (4 if k % 2 == 0 else 0), st
+    else:
+        assert npair == 0 and ndual == 4 * k, st
