@@ -8,9 +8,14 @@
 #include "kr_engine.h"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstring>
+#include <exception>
+#include <mutex>
+#include <thread>
 
 namespace kr {
 
@@ -215,6 +220,7 @@ void plan_halo(int P, const int64_t* part, const int64_t* need_lo, const int64_t
 
 System::~System() {
   session.reset();
+  pool.reset();
   if (hy_send) (void)hipFree(hy_send);
   if (hy_recv) (void)hipFree(hy_recv);
   if (hy_host) (void)hipHostFree(hy_host);
@@ -245,6 +251,90 @@ System::~System() {
     if (s.ev_b) (void)hipEventDestroy(s.ev_b);
     if (s.stream) (void)hipStreamDestroy(s.stream);
   }
+}
+
+// ------------------------------------------------------------- ShardPool
+struct ShardPool::Impl {
+  std::vector<std::thread> th;
+  std::atomic<uint64_t> gen{0};
+  std::atomic<int> pending{0};
+  std::atomic<bool> stop{false};
+  const std::function<void(int)>* fn = nullptr;
+  int n = 0;
+  std::vector<std::exception_ptr> err;
+  std::mutex mu;
+  std::condition_variable cv;
+
+  void worker(int w) {
+    uint64_t seen = 0;
+    for (;;) {
+      int spins = 0;
+      while (gen.load(std::memory_order_acquire) == seen && !stop.load()) {
+        if (++spins < (1 << 14)) {
+          __builtin_ia32_pause();
+        } else {  // idle: sleep until the next run (no lost wake-up: gen changes under mu)
+          std::unique_lock<std::mutex> lk(mu);
+          cv.wait(lk, [&] { return gen.load() != seen || stop.load(); });
+        }
+      }
+      if (stop.load()) return;
+      seen = gen.load(std::memory_order_acquire);
+      const int li = w + 1;
+      if (li < n) {
+        try {
+          (*fn)(li);
+        } catch (...) {
+          err[li] = std::current_exception();
+        }
+      }
+      pending.fetch_sub(1, std::memory_order_acq_rel);
+    }
+  }
+};
+
+ShardPool::ShardPool(int nworkers) : impl_(new Impl) {
+  for (int w = 0; w < nworkers; ++w) impl_->th.emplace_back([this, w] { impl_->worker(w); });
+}
+
+ShardPool::~ShardPool() {
+  {
+    std::lock_guard<std::mutex> lk(impl_->mu);
+    impl_->stop.store(true);
+  }
+  impl_->cv.notify_all();
+  for (auto& t : impl_->th) t.join();
+}
+
+int ShardPool::workers() const { return (int)impl_->th.size(); }
+
+void ShardPool::run(int n, const std::function<void(int)>& fn) {
+  Impl& I = *impl_;
+  KR_REQUIRE(n <= (int)I.th.size() + 1, "ShardPool: more shards than threads");
+  I.fn = &fn;
+  I.n = n;
+  I.err.assign((size_t)n, nullptr);
+  I.pending.store((int)I.th.size(), std::memory_order_release);
+  {
+    std::lock_guard<std::mutex> lk(I.mu);
+    I.gen.fetch_add(1, std::memory_order_acq_rel);
+  }
+  I.cv.notify_all();
+  try {
+    fn(0);
+  } catch (...) {
+    I.err[0] = std::current_exception();
+  }
+  while (I.pending.load(std::memory_order_acquire) > 0) __builtin_ia32_pause();
+  for (auto& e : I.err)
+    if (e) std::rethrow_exception(e);
+}
+
+void System::for_shards(const std::function<void(Shard&, size_t)>& fn) {
+  if (pool && shards.size() > 1) {
+    pool->run((int)shards.size(), [&](int li) { fn(shards[(size_t)li], (size_t)li); });
+    return;
+  }
+  for (size_t li = 0; li < shards.size(); ++li) fn(shards[li], li);
 }
 
 IluFactors::~IluFactors() {
@@ -993,6 +1083,17 @@ void System::finalize() {
     KR_HIP_CHECK(hipHostMalloc(&hy_host, sizeof(double) * kMaxLocal * kMaxSlots * nranks, 0));
     if (!hy_ev) KR_HIP_CHECK(hipEventCreateWithFlags(&hy_ev, hipEventDisableTiming));
   }
+  // in-process: the shards whose comm streams copy halo rows from each shard
+  // (the boundary launch of a shard waits for their copies before its later
+  // kernels may overwrite those rows)
+  if (!comm) {
+    for (auto& s : shards) s.readers.clear();
+    for (size_t li = 0; li < shards.size(); ++li)
+      for (auto& p : shards[li].recv) {
+        auto& r = shards[(size_t)p.peer].readers;
+        if (std::find(r.begin(), r.end(), (int)li) == r.end()) r.push_back((int)li);
+      }
+  }
   // The split SpMV needs interior rows on every shard; with RCCL ranks the
   // decision is global, so the summation order (interior + boundary partials)
   // is the one of the same partition in one process (oracle/gpu_order.py).
@@ -1012,6 +1113,13 @@ void System::finalize() {
     KR_HIP_CHECK(hipStreamSynchronize(s0.stream));
     KR_HIP_CHECK(hipFree(d));
     for (int64_t f : all) all_interior = all_interior && f != 0;
+  }
+  // one host thread per further in-process shard (KR_HOST_THREADS=0: every
+  // shard's work enqueued by the calling thread, A/B)
+  {
+    const char* ht = getenv("KR_HOST_THREADS");
+    if (!comm && shards.size() > 1 && !(ht && atoi(ht) == 0))
+      pool = std::make_unique<ShardPool>((int)shards.size() - 1);
   }
   {
     const char* env = getenv("KR_OVERLAP");  // 0 disables the split SpMV (A/B)
@@ -1321,29 +1429,34 @@ void System::halo_async(int id1, int id2, int id3) {
     KR_HIP_CHECK(hipEventRecord(s.ev_out, s.comm_stream));
     return;
   }
-  for (auto& s : shards) {
-    KR_HIP_CHECK(hipSetDevice(s.dev));
-    // The copies overwrite s's halo rows: s's own earlier kernels (the
-    // previous SpMV's boundary rows read the same halo when consecutive SpMVs
-    // share an input vector) must be done first, not only the peer's.
-    KR_HIP_CHECK(hipStreamWaitEvent(s.comm_stream, s.ev_in, 0));
-    for (auto& p : s.recv) {
-      Shard& t = shards[p.peer];
-      KR_HIP_CHECK(hipStreamWaitEvent(s.comm_stream, t.ev_in, 0));
-      for (int id : {id1, id2, id3}) {
-        if (id < 0) continue;
-        double* dst = s.vec[id] + s.local_index(p.g0);
-        const double* src = t.vec[id] + t.local_index(p.g0);
-        if (s.dev == t.dev)
-          KR_HIP_CHECK(hipMemcpyAsync(dst, src, 8 * (size_t)p.count, hipMemcpyDeviceToDevice,
-                                      s.comm_stream));
-        else
-          KR_HIP_CHECK(hipMemcpyPeerAsync(dst, s.dev, src, t.dev, 8 * (size_t)p.count,
-                                          s.comm_stream));
-      }
+  for (auto& s : shards) halo_in_process(s, id1, id2, id3);
+}
+
+// One in-process shard's part of halo_async: its comm stream copies its halo
+// rows from the peers after their ev_in, then records ev_out. Touches only
+// this shard's streams (the per-shard host threads run it concurrently).
+void System::halo_in_process(Shard& s, int id1, int id2, int id3) {
+  KR_HIP_CHECK(hipSetDevice(s.dev));
+  // The copies overwrite s's halo rows: s's own earlier kernels (the
+  // previous SpMV's boundary rows read the same halo when consecutive SpMVs
+  // share an input vector) must be done first, not only the peer's.
+  KR_HIP_CHECK(hipStreamWaitEvent(s.comm_stream, s.ev_in, 0));
+  for (auto& p : s.recv) {
+    Shard& t = shards[p.peer];
+    KR_HIP_CHECK(hipStreamWaitEvent(s.comm_stream, t.ev_in, 0));
+    for (int id : {id1, id2, id3}) {
+      if (id < 0) continue;
+      double* dst = s.vec[id] + s.local_index(p.g0);
+      const double* src = t.vec[id] + t.local_index(p.g0);
+      if (s.dev == t.dev)
+        KR_HIP_CHECK(hipMemcpyAsync(dst, src, 8 * (size_t)p.count, hipMemcpyDeviceToDevice,
+                                    s.comm_stream));
+      else
+        KR_HIP_CHECK(hipMemcpyPeerAsync(dst, s.dev, src, t.dev, 8 * (size_t)p.count,
+                                        s.comm_stream));
     }
-    KR_HIP_CHECK(hipEventRecord(s.ev_out, s.comm_stream));
   }
+  KR_HIP_CHECK(hipEventRecord(s.ev_out, s.comm_stream));
 }
 
 void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int b,
@@ -1530,26 +1643,42 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
     return;
   }
   std::vector<hipEvent_t> t0s(shards.size(), nullptr);
-  for (size_t li = 0; li < shards.size(); ++li) {
-    Shard& s = shards[li];
+  // In-process shards: three phases on the per-shard host threads (a phase
+  // waits on events the previous one recorded on OTHER shards' streams, so
+  // the phases are separated by the pool's barrier); otherwise serial.
+  const bool threaded = !comm && pool;
+  auto phase_in = [&](Shard& s, size_t li) {
     KR_HIP_CHECK(hipSetDevice(s.dev));
     prof_begin(s, nm, t0s[li]);
     KR_HIP_CHECK(hipEventRecord(s.ev_in, s.stream));
+  };
+  if (threaded) {
+    for_shards(phase_in);
+    for_shards([&](Shard& s, size_t) {
+      halo_in_process(s, in1, hx2, hx3);
+      launch_full(s, s.int_lo, s.int_hi - s.int_lo);  // interior rows
+    });
+  } else {
+    for (size_t li = 0; li < shards.size(); ++li) phase_in(shards[li], li);
+    halo_async(in1, hx2, hx3);
+    for (auto& s : shards) {  // interior rows: all blocks write their partials
+      KR_HIP_CHECK(hipSetDevice(s.dev));
+      launch_full(s, s.int_lo, s.int_hi - s.int_lo);
+    }
   }
-  halo_async(in1, hx2, hx3);
-  for (auto& s : shards) {  // interior rows: all blocks write their partials
-    KR_HIP_CHECK(hipSetDevice(s.dev));
-    launch_full(s, s.int_lo, s.int_hi - s.int_lo);
-  }
-  for (size_t li = 0; li < shards.size(); ++li) {
-    Shard& s = shards[li];
+  auto phase_boundary = [&](Shard& s, size_t li) {
     KR_HIP_CHECK(hipSetDevice(s.dev));
     if (comm && !hybrid()) {
       KR_HIP_CHECK(hipStreamWaitEvent(s.stream, s.ev_out, 0));
+    } else if (!comm) {
+      // own halo copied, and every shard that copies from this one done
+      // reading its rows (the next kernels may overwrite them)
+      KR_HIP_CHECK(hipStreamWaitEvent(s.stream, s.ev_out, 0));
+      for (int t : s.readers) KR_HIP_CHECK(hipStreamWaitEvent(s.stream, shards[t].ev_out, 0));
     } else {
       // own halo copied, and every reader done with this shard's rows
       for (auto& t : shards) KR_HIP_CHECK(hipStreamWaitEvent(s.stream, t.ev_out, 0));
-      if (comm) KR_HIP_CHECK(hipStreamWaitEvent(s.stream, hy_ev, 0));  // RCCL pieces
+      KR_HIP_CHECK(hipStreamWaitEvent(s.stream, hy_ev, 0));  // RCCL pieces
     }
     // both boundary ranges in one launch: row blocks [0, int_lo/B) and
     // [int_hi/B, end) (interior bounds are whole blocks, see finalize)
@@ -1565,7 +1694,11 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
       launch_spmv_grid(epi, ab, g, s.stream);
     }
     prof_end(s, nm, t0s[li], bytes_of(s));
-  }
+  };
+  if (threaded)
+    for_shards(phase_boundary);
+  else
+    for (size_t li = 0; li < shards.size(); ++li) phase_boundary(shards[li], li);
 }
 
 void System::ew(EwOp op, double c0, double c1, std::array<int, 6> ids, int slot0) {
@@ -1578,7 +1711,7 @@ void System::ew(EwOp op, double c0, double c1, std::array<int, 6> ids, int slot0
 void System::ew_n(EwOp op, double c0, double c1, const std::array<int, kEwOps>& ids,
                   int slot0) {
   KR_REQUIRE(slot0 + ew_products(op) <= kMaxSlots, "reduction slots exhausted");
-  for (auto& s : shards) {
+  for_shards([&](Shard& s, size_t) {
     KR_HIP_CHECK(hipSetDevice(s.dev));
     EwArgs a;
     a.c0 = c0;
@@ -1594,7 +1727,7 @@ void System::ew_n(EwOp op, double c0, double c1, const std::array<int, kEwOps>& 
     prof_begin(s, nm, t0);
     launch_ew(op, a, s.stream);
     prof_end(s, nm, t0, 8.0 * ew_vectors(op) * s.n);
-  }
+  });
 }
 
 bool System::device_scalars() const {
@@ -1828,7 +1961,7 @@ std::vector<double> System::reduce(int nslots) {
   std::vector<double> tot(nslots, 0.0);
   if (nslots <= 0) return tot;
   KR_REQUIRE(nslots <= kMaxSlots, "too many slots");
-  for (auto& s : shards) {
+  auto finalize_shard = [&](Shard& s, size_t) {
     KR_HIP_CHECK(hipSetDevice(s.dev));
     hipEvent_t t0 = nullptr;
     prof_begin(s, "reduce", t0);
@@ -1848,7 +1981,11 @@ std::vector<double> System::reduce(int nslots) {
                                   hipMemcpyDeviceToHost, s.stream));
     }
     prof_end(s, "reduce", t0, 8.0 * nslots * s.pstride);
-  }
+  };
+  if (!comm)
+    for_shards(finalize_shard);  // in-process: per-shard host threads
+  else
+    for (size_t li = 0; li < shards.size(); ++li) finalize_shard(shards[li], li);
   if (hybrid()) {
     // every local shard's slots side by side (kMaxLocal x nslots), one
     // all-gather for the rank; the stride stays fixed so any rank can index

@@ -7,6 +7,7 @@
 #include <rccl/rccl.h>
 
 #include <array>
+#include <functional>
 #include <map>
 #include <memory>
 #include <string>
@@ -108,6 +109,7 @@ struct Shard {
   int grid = 1;                 // workgroups of the vector kernels
   int spmv_grid = 1;            // workgroups of the SpMV kernels
   int spmv_grid_po = 1;         // ... of a products-only stencil launch (<= spmv_grid)
+  std::vector<int> readers;     // in-process: local shards that copy halo rows from this one
   int spmv_grid2 = 1;           // ... of the fused basis pair (System::spmv_pair, <= spmv_grid)
   int pstride = 1;              // partial stride per slot: max(grid, spmv_grid)
   std::array<int, kMaxSlots> slot_n{};  // partials written per slot by its last producer
@@ -165,6 +167,28 @@ struct IluFactors {
   ~IluFactors();
 };
 
+// Host threads that enqueue per-shard work in parallel (single-process
+// multi-shard systems: one host thread issuing every shard's launches, halo
+// copies and event waits serially costs ~4 ms per 512^3 k-skip outer
+// iteration at 8 shards, 3x one shard's GPU time). run(n, fn) calls fn(li)
+// for li = 0 .. n-1 -- li = 0 on the calling thread, the others on workers --
+// and returns when all are done, so a run is a barrier between phases; an
+// exception in any fn is rethrown by run. Workers spin between runs and
+// sleep after ~1 ms idle.
+class ShardPool {
+ public:
+  explicit ShardPool(int nworkers);
+  ~ShardPool();
+  ShardPool(const ShardPool&) = delete;
+  ShardPool& operator=(const ShardPool&) = delete;
+  void run(int n, const std::function<void(int)>& fn);
+  int workers() const;
+
+ private:
+  struct Impl;
+  std::unique_ptr<Impl> impl_;
+};
+
 struct System {
   int64_t n_global = 0;
   std::vector<Shard> shards;
@@ -205,6 +229,11 @@ struct System {
   bool products_only = false;
   bool products_only_on = true;
   std::unique_ptr<Session> session;
+  // per-shard host threads (in-process multi-shard, KR_HOST_THREADS != 0)
+  std::unique_ptr<ShardPool> pool;
+  // fn(shard, li) for every local shard: on the pool when there is one, else
+  // in order on this thread (each fn sets its shard's device)
+  void for_shards(const std::function<void(Shard&, size_t)>& fn);
 
   ~System();
   int nglobal_shards() const { return (int)part.size() - 1; }
@@ -220,6 +249,7 @@ struct System {
   // The same exchange on the shards' comm streams, ordered after ev_in and
   // signalling ev_out (overlapped path).
   void halo_async(int id1, int id2, int id3 = -1);
+  void halo_in_process(Shard& s, int id1, int id2, int id3);
   void spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int b, int slot0,
             const StepOps* st = nullptr);
   // Two chained EPI_DUAL_MRR basis SpMVs in one launch (spmv_stencil2_kernel):

@@ -521,6 +521,17 @@ void spmv_stencil_kernel_w4(SpmvArgs a) {
   if (!spmv_entry<EPI>(a)) return;
   spmv_stencil_body<EPI, NFAR, PAT, RELOAD, NTM, CB>(a);
 }
+// The products-only dual (a read-only stream, no store epilogue) at its own
+// wave target (KR_ST_PO_W, compile time; A/B builds).
+#ifndef KR_ST_PO_W
+#define KR_ST_PO_W 4
+#endif
+template <int EPI, int NFAR, uint32_t PAT, bool RELOAD, int NTM = 3, int CB = 8>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KR_ST_PO_W)))
+void spmv_stencil_kernel_po(SpmvArgs a) {
+  if (!spmv_entry<EPI>(a)) return;
+  spmv_stencil_body<EPI, NFAR, PAT, RELOAD, NTM, CB>(a);
+}
 
 // KR_STENCIL_DEPTH=2 (A/B): the dual SpMVs load two visits ahead.
 inline int st_depth() {
@@ -533,7 +544,9 @@ template <int E, bool RELOAD, int NTM, bool W4>
 void st_launch_pat7(const SpmvArgs& a, int nblocks, size_t lds, hipStream_t s) {
   auto go = [&](auto cbc) {
     constexpr int CB = decltype(cbc)::value;
-    if constexpr (W4)
+    if constexpr (W4 && (NTM & 4))
+      spmv_stencil_kernel_po<E, 2, kPat7, RELOAD, NTM, CB><<<nblocks, kBlock, lds, s>>>(a);
+    else if constexpr (W4)
       spmv_stencil_kernel_w4<E, 2, kPat7, RELOAD, NTM, CB><<<nblocks, kBlock, lds, s>>>(a);
     else
       spmv_stencil_kernel<E, 2, kPat7, RELOAD, NTM, CB><<<nblocks, kBlock, lds, s>>>(a);
