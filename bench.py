@@ -144,7 +144,11 @@ def cpu_baseline(n_side: int, k: int, method: str, return_info: bool = False, ou
                        f"scipy SpMV 1 thread, OpenBLAS dot {blas_threads} threads "
                        f"({', '.join(f'{k_}={v}' for k_, v in env_threads.items()) or 'no thread env'}), "
                        f"{cores} affinity cores, {cpu_model()}; wall {wall:.1f} s; "
-                       f"cores = the BLAS threads (the SpMV, most of the time, uses one)"))
+                       f"cores = the BLAS threads (the SpMV, most of the time, uses one); "
+                       f"the BLAS runs on the thread count the environment sets -- the GPU "
+                       f"box's CPU share is 16 cores of the node and its harness fixes "
+                       f"OMP/OpenBLAS at 16, so the other affinity cores belong to other "
+                       f"jobs; scipy's csr_matvec is single-threaded whatever the count"))
     return (rec, info) if return_info else rec
 
 

@@ -1928,6 +1928,9 @@ void spmv_dia_launch(const SpmvArgs& a, int nblocks, hipStream_t s) {
 // indices cost 3 VALU per entry).
 // ---------------------------------------------------------------------------
 constexpr int kWalkWin = 768;  // x window, rows per vector (band <= 256)
+#ifndef KR_DIAW_MODE
+#define KR_DIAW_MODE 1
+#endif
 
 // NH = h, the number of upper (= lower) offsets, is a template parameter:
 // every loop over the offsets is then straight-line code, so the compiler
@@ -1981,11 +1984,23 @@ __global__ __launch_bounds__(kBlock, NH > 15 ? 2 : 1) void spmv_diawalk_kernel(S
     else
       return r1;
   };
-  // store v at s_low[slot][pos] when ok, else at the lane's junk slot (no branch)
+  // store v at s_low[slot][pos] when ok. KR_DIAW_MODE (compile time, A/B
+  // builds): 0 = the other lanes store to a junk slot, every wave issues the
+  // head and the tail store of every offset; 1 = junk slot, but a wave whose
+  // rows all store the head (or all the tail) of an offset skips the other
+  // store (rows wv0 .. wv0+63, wave-uniform tests); 2 = as 1 with
+  // exec-masked stores instead of the junk slot.
   auto low_put = [&](bool ok, int slot, int pos, double v) {
-    double* d = ok ? s_low + slot * kBlock + pos : s_junk + tid;
-    *d = v;
+    if constexpr (KR_DIAW_MODE == 2) {
+      if (ok) s_low[slot * kBlock + pos] = v;
+    } else {
+      double* d = ok ? s_low + slot * kBlock + pos : s_junk + tid;
+      *d = v;
+    }
   };
+  const int wv0 = __builtin_amdgcn_readfirstlane(tid & ~63);
+  auto any_tail = [&](int o) { return KR_DIAW_MODE == 0 || wv0 + 63 + o >= kBlock; };
+  auto any_head = [&](int o) { return KR_DIAW_MODE == 0 || wv0 + o < kBlock; };
 
   // one block ahead: values (diagonal + upper), mask, epilogue operands, the
   // window's new rows (raw loads; a virtual input is formed when stored)
@@ -2022,7 +2037,7 @@ __global__ __launch_bounds__(kBlock, NH > 15 ? 2 : 1) void spmv_diawalk_kernel(S
 #pragma unroll
       for (int u = 1; u <= NH; ++u) {
         const int o = moff(NH + u);
-        low_put(tid + o >= kBlock, NH - u, tid + o - kBlock, up[u]);
+        if (any_tail(o)) low_put(tid + o >= kBlock, NH - u, tid + o - kBlock, up[u]);
       }
     }
     prev = b;
@@ -2068,7 +2083,7 @@ __global__ __launch_bounds__(kBlock, NH > 15 ? 2 : 1) void spmv_diawalk_kernel(S
 #pragma unroll
     for (int u = 1; u <= NH; ++u) {  // heads: rows p + o < 256 of this block
       const int o = moff(NH + u);
-      low_put(tid + o < kBlock, NH - u, tid + o, up[u]);
+      if (any_head(o)) low_put(tid + o < kBlock, NH - u, tid + o, up[u]);
     }
     const bool lane_full = active && m == kFull;
     const uint64_t all = __ballot(lane_full);
