@@ -29,10 +29,10 @@ def short(name):
     m = re.search(r"spmv_kernel\w*<(\w+), (\d+), (\w+)", name)
     if m:
         return EPI[int(m.group(2))] + ("" if m.group(1) == "int" else "_rp64")
-    m = re.search(r"spmv_stencil_kernel(?:_w4)?<(\d+), \d+, \w+, \w+, (\d+)(?:, \d+)?>", name)
+    m = re.search(r"spmv_stencil_kernel(?:_w4|_po)?<(\d+), \d+, \w+, \w+, (\d+)(?:, \d+)?>", name)
     if m:  # NTM bit 2: the products-only dual (engine name ..._last)
         return EPI[int(m.group(1))] + ("_last" if int(m.group(2)) & 4 else "") + "_stencil"
-    m = re.search(r"spmv_stencil_kernel(?:_w4)?<(\d+)\b", name)
+    m = re.search(r"spmv_stencil_kernel(?:_w4|_po)?<(\d+)\b", name)
     if m:
         return EPI[int(m.group(1))] + "_stencil"
     m = re.search(r"spmv_diawalk_kernel<(\d+), \d+>", name)
