@@ -187,6 +187,35 @@ __device__ __forceinline__ void st_issue_edges(SStage<NX, NFAR, CB>& st, const S
   }
 }
 
+// The +-1 neighbours without LDS (NTM bit 5, the 7-point pattern): inside a
+// wave a lane's row 2t-1 is lane t-1's second row and its row 2t+2 lane
+// t+1's first, moved by DPP wave shifts; the wave's two edge rows (128 w - 1
+// and 128 w + 128 of the block) come through the scalar cache. No LDS line
+// and no workgroup barrier per visit.
+__device__ __forceinline__ double st_dpp_shr1(double v, double old) {  // lane t <- lane t-1
+  const long long b = __builtin_bit_cast(long long, v), o = __builtin_bit_cast(long long, old);
+  const int lo = __builtin_amdgcn_update_dpp((int)o, (int)b, 0x138, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(b >> 32), 0x138, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, (long long)(unsigned)lo | ((long long)hi << 32));
+}
+__device__ __forceinline__ double st_dpp_shl1(double v, double old) {  // lane t <- lane t+1
+  const long long b = __builtin_bit_cast(long long, v), o = __builtin_bit_cast(long long, old);
+  const int lo = __builtin_amdgcn_update_dpp((int)o, (int)b, 0x130, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(b >> 32), 0x130, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, (long long)(unsigned)lo | ((long long)hi << 32));
+}
+template <int NX, int NFAR, int CB>
+__device__ __forceinline__ void st_issue_wave_edges(SStage<NX, NFAR, CB>& st, const SpmvArgs& a,
+                                                    const double* const (&xs)[3], int64_t row0,
+                                                    int wave) {
+  const int64_t r = row0 + 128 * (int64_t)wave;
+#pragma unroll
+  for (int v = 0; v < NX; ++v) {
+    st.el[v] = st_ld2_uniform(xs[v], a.xoff + r - 2, a.xlen);    // rows r-2, r-1
+    st.er[v] = st_ld2_uniform(xs[v], a.xoff + r + 128, a.xlen);  // rows r+128, r+129
+  }
+}
+
 // Own-row epilogue of one row from the carried centers (x, x2 / r0, y0, Ar1)
 // and the staged operands: the values epi_row_in stores, without the loads.
 template <int EPI>
@@ -285,6 +314,10 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
   dbl2v cen[NX], prv[NX];  // carried: x at the rows, x at the rows - W
   // NTM bit 3: loads two visits ahead (three stage register sets) instead of one
   constexpr int DEPTH = (!RELOAD && (NTM & 8)) ? 2 : 1;
+  // NTM bit 5: +-1 neighbours by DPP within the wave (7-point pattern whose
+  // NEAR slots are -1 and +1; the host checks), no LDS line, no barrier
+  constexpr bool DPP = (NTM & 32) && PAT == kPat7;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   SStage<NX, NFAR, CB> sA, sB, sC;
   const SRes res = st_res<NX, CB>(a, xs);
   int buf = 0;
@@ -294,7 +327,10 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
     st_issue<EPI, RELOAD, NTM>(st, a, res, row0, tid, rl < a.n ? rl : a.n - 2);
   };
   auto issue_edges = [&](SStage<NX, NFAR, CB>& st, int64_t z) {
-    st_issue_edges(st, a, xs, phys(blk(z)) * kSBlock);
+    if constexpr (DPP)
+      st_issue_wave_edges(st, a, xs, phys(blk(z)) * kSBlock, wave);
+    else
+      st_issue_edges(st, a, xs, phys(blk(z)) * kSBlock);
   };
 
   // One visit: `cur` holds its loads (issued one visit earlier); the next
@@ -339,24 +375,46 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
         opp[v] = prv[v];
       }
     }
-    // (3) the LDS line: this block's centers and the edge pairs
-#pragma unroll
-    for (int v = 0; v < NV; ++v)
-      reinterpret_cast<dbl2v*>(&s_line[buf][v][kSNear])[tid] = opc[v];
-    if (tid < 2) {
-      double* dst = &s_line[buf][0][tid == 0 ? 0 : kSNear + kSBlock];
-      const dbl2v* e = tid == 0 ? cur.el : cur.er;
+    // (3) the +-1 neighbours: DPP within the wave (+ the wave's edge rows),
+    // or the LDS line of this block's centers and its edge pairs
+    double xm1[NV], xp2[NV];  // DPP: x at rows 2t-1 and 2t+2
+    if constexpr (DPP) {
+      double el[NV], er[NV];
       if constexpr (VIRT) {
-        *reinterpret_cast<dbl2v*>(dst) =
-            dbl2v{virt_in<EPI>(a, e[0].x, e[1].x, e[NX - 1].x),
-                  virt_in<EPI>(a, e[0].y, e[1].y, e[NX - 1].y)};
+        el[0] = virt_in<EPI>(a, cur.el[0].y, cur.el[1].y, cur.el[NX - 1].y);
+        er[0] = virt_in<EPI>(a, cur.er[0].x, cur.er[1].x, cur.er[NX - 1].x);
       } else {
 #pragma unroll
-        for (int v = 0; v < NV; ++v) *reinterpret_cast<dbl2v*>(dst + v * kSLine) = e[v];
+        for (int v = 0; v < NV; ++v) {
+          el[v] = cur.el[v].y;
+          er[v] = cur.er[v].x;
+        }
       }
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        xm1[v] = st_dpp_shr1(opc[v].y, el[v]);
+        xp2[v] = st_dpp_shl1(opc[v].x, er[v]);
+      }
+      issue_edges(nxs, zn);
+    } else {
+#pragma unroll
+      for (int v = 0; v < NV; ++v)
+        reinterpret_cast<dbl2v*>(&s_line[buf][v][kSNear])[tid] = opc[v];
+      if (tid < 2) {
+        double* dst = &s_line[buf][0][tid == 0 ? 0 : kSNear + kSBlock];
+        const dbl2v* e = tid == 0 ? cur.el : cur.er;
+        if constexpr (VIRT) {
+          *reinterpret_cast<dbl2v*>(dst) =
+              dbl2v{virt_in<EPI>(a, e[0].x, e[1].x, e[NX - 1].x),
+                    virt_in<EPI>(a, e[0].y, e[1].y, e[NX - 1].y)};
+        } else {
+#pragma unroll
+          for (int v = 0; v < NV; ++v) *reinterpret_cast<dbl2v*>(dst + v * kSLine) = e[v];
+        }
+      }
+      __syncthreads();
+      issue_edges(nxs, zn);
     }
-    __syncthreads();
-    issue_edges(nxs, zn);
     // (4) the two rows' sums, slot by slot in ascending offset order
     double slo[NV], shi[NV];
 #pragma unroll
@@ -380,11 +438,19 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
 #pragma unroll
         for (int v = 0; v < NV; ++v) { xlo[v] = opp[v].x; xhi[v] = opp[v].y; }
       } else if (kind == SK_NEAR) {
-        const int o = a.st_off[k];
+        if constexpr (DPP) {  // kPat7: slot 2 is -1, slot 4 is +1
 #pragma unroll
-        for (int v = 0; v < NV; ++v) {
-          xlo[v] = s_line[buf][v][kSNear + 2 * lp + o];
-          xhi[v] = s_line[buf][v][kSNear + 2 * lp + 1 + o];
+          for (int v = 0; v < NV; ++v) {
+            xlo[v] = k == 2 ? xm1[v] : opc[v].y;
+            xhi[v] = k == 2 ? opc[v].x : xp2[v];
+          }
+        } else {
+          const int o = a.st_off[k];
+#pragma unroll
+          for (int v = 0; v < NV; ++v) {
+            xlo[v] = s_line[buf][v][kSNear + 2 * lp + o];
+            xhi[v] = s_line[buf][v][kSNear + 2 * lp + 1 + o];
+          }
         }
       } else {
         // NEXT or FAR f: a staged pair
@@ -538,6 +604,17 @@ inline int st_depth() {
   const char* e = getenv("KR_STENCIL_DEPTH");
   return e ? atoi(e) : 1;
 }
+// The DPP neighbour path (NTM bit 5) for 7-point shards whose NEAR slots are
+// -1 and +1. Measured on C4 (one box, A/B): the products-only dual 0.645 ->
+// 0.560 ms (a read-only stream: the per-visit barrier was its stall), every
+// storing launch 1-2 % slower (dual 0.889 -> 0.908 ms, steps alike). So
+// KR_STENCIL_DPP = 1 (default): products-only launches only; 2: every
+// 7-point launch; 0: none (A/B).
+inline bool st_dpp(const SpmvArgs& a, bool products_only) {
+  const char* e = getenv("KR_STENCIL_DPP");  // read per launch: tests switch it
+  const int v = e ? atoi(e) : 1;
+  return (v == 2 || (v == 1 && products_only)) && a.st_off[2] == -1 && a.st_off[4] == 1;
+}
 
 // The 7-point pattern's launch at the shard's code width.
 template <int E, bool RELOAD, int NTM, bool W4>
@@ -581,6 +658,8 @@ void spmv_stencil_launch_r(const SpmvArgs& a, int nblocks, hipStream_t s) {
       if (pat7) {
         if (!RELOAD && st_depth() == 2)
           st_launch_pat7<E, RELOAD, 15, false>(a, nblocks, lds, s);
+        else if (st_dpp(a, true))
+          st_launch_pat7<E, RELOAD, 39, !RELOAD>(a, nblocks, lds, s);
         else
           st_launch_pat7<E, RELOAD, 7, !RELOAD>(a, nblocks, lds, s);
         return;
@@ -607,6 +686,8 @@ void spmv_stencil_launch_r(const SpmvArgs& a, int nblocks, hipStream_t s) {
     constexpr bool w4 = !RELOAD && (E == EPI_DUAL_MRR || E == EPI_DUAL_KCG || E == EPI_DUAL_NONE);
     if (w4 && st_depth() == 2)
       st_launch_pat7<E, RELOAD, 11, false>(a, nblocks, lds, s);
+    else if (st_dpp(a, false))
+      st_launch_pat7<E, RELOAD, 35, w4>(a, nblocks, lds, s);
     else
       st_launch_pat7<E, RELOAD, 3, w4>(a, nblocks, lds, s);
     return;

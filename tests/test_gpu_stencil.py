@@ -355,3 +355,30 @@ def test_stencil_pair_is_used(monkeypatch, name, k, pairs, st2):
         assert st.get("spmv2x2_gram_mrr_last", 0) == (4 if k % 2 == 0 else 0), st
     else:
         assert npair == 0 and ndual == 4 * k, st
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method,name,k,shards", [("kskipmrr", "p3d32", 4, "0"),
+                                                  ("kskipmrr", "box64x64x20", 4, "0,0"),
+                                                  ("adaptivekskipmrr", "box512x8x16", 6, "0"),
+                                                  ("kskipcg", "box128x32x9", 3, "0"),
+                                                  ("kskipmrr", "aniso32x32x7", 4, "0,0,0")])
+def test_stencil_dpp_neighbours_bitwise(monkeypatch, method, name, k, shards):
+    """The +-1 neighbours moved by DPP wave shifts (+ the waves' edge rows
+    through the scalar cache; KR_STENCIL_DPP=2: every 7-point launch, 1: the
+    products-only dual, 0: the LDS line) give the same histories and x bit
+    for bit -- cubes, boxes, sharded (boundary launches), VIRT epilogues."""
+    A = MATRICES[name]()
+    b = np.random.default_rng(7).standard_normal(A.shape[0])
+    kw = dict(tol=1e-10, maxiter=300, k=k)
+    monkeypatch.setenv("KRYLOV_AMD_SHARDS", shards)
+    out = []
+    for dpp in ("0", "1", "2"):
+        monkeypatch.setenv("KR_STENCIL_DPP", dpp)
+        with contextlib.redirect_stdout(io.StringIO()):
+            x, info = _solver(method)(A, b, **kw)
+        out.append((x.cpu().numpy(), info))
+    for x1, i1 in out[1:]:
+        np.testing.assert_array_equal(i1["nosl"], out[0][1]["nosl"])
+        np.testing.assert_array_equal(i1["residual"], out[0][1]["residual"])
+        np.testing.assert_array_equal(x1, out[0][0])
