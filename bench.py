@@ -373,6 +373,29 @@ def kernel_sampling(kernels, run, args):
                      "event pairs' launch gaps (not counted in value)")
 
 
+def step_roofline(kernels, stored, run, args, per_step, n, nnz_total, method, k):
+    """The whole outer iteration against HBM (report the
+    whole-iteration fraction beside the SpMV kernel's): the stored-format
+    bytes of every kernel of a sampled step, divided by ms_per_step, and
+    SURVEY 8(d)'s fused-minimal CSR bytes per solver iteration with the
+    it/s they would allow at the 8 TB/s peak (k-skip MrR: (3k+1) B_spmv +
+    (2k+3) 8N + 9(k+1) 8N per outer iteration; one-GPU runs). Per GPU."""
+    if not kernels:
+        return None
+    every = args.profile_every or PROFILE_EVERY.get(args.config, 4)
+    sampled = max(1, -(-args.steps // every))
+    byts = sum(stored[n_][0] * v["launches"] for n_, v in kernels.items()) / sampled
+    step_s = run["elapsed"] / args.steps
+    out = dict(stored_bytes_per_step=round(byts), achieved=round(byts / step_s / 1e9, 1),
+               peak=HBM_PEAK_GBS, unit="GB/s", frac=round(byts / step_s / 1e9 / HBM_PEAK_GBS, 4))
+    if method in ("kskipmrr", "adaptivekskipmrr") and k > 0 and nnz_total > 0:
+        b_spmv = 12.0 * nnz_total + 4.0 * (n + 1) + 16.0 * n
+        per_iter = ((3 * k + 1) * b_spmv + (2 * k + 3) * 8.0 * n + 9 * (k + 1) * 8.0 * n) / (k + 1)
+        out.update(survey_csr_bytes_per_iteration=round(per_iter),
+                   survey_csr_ideal_its=round(HBM_PEAK_GBS * 1e9 / per_iter, 1))
+    return out
+
+
 def dominant(kernels):
     spmv = {n_: v for n_, v in kernels.items() if n_.startswith("spmv")}
     return max(spmv or kernels, key=lambda n_: kernels[n_]["total_ms"])
@@ -481,6 +504,9 @@ def main():
             "csr": csr_rec,
             "kernels": kernels,
             "kernel_sampling": kernel_sampling(kernels, run, args),
+            "step_roofline": step_roofline(kernels, stored, run, args, run["per_step"], n,
+                                           run["info"].get("nnz", 0) if world == 1 else 0,
+                                           method, k),
             "host": host_table(run["stats"]),
             "residual_tail": [float(v) for v in run["history"]["residual"][-3:-1]],
         }

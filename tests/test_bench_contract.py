@@ -87,3 +87,23 @@ def test_stored_format_bytes():
     st2 = dict(st, code_bits=2)
     assert bench.stored_format_delta(nnz, n, st2) == 12.0 * nnz + 4.0 * (n + 1) - 2.0 * n
     assert "2-bit" in bench.format_name(st2)
+
+
+def test_step_roofline_survey_figures():
+    """bench.step_roofline: the whole outer iteration's stored bytes per
+    ms_per_step, and SURVEY.md 8(d)'s fused-minimal CSR bytes of k-skip MrR
+    (C4: 48.27 GB per solver iteration, ideal 166 it/s at 8 TB/s)."""
+    import argparse
+    import bench
+    n = 512 ** 3
+    nnz = 937951232
+    kernels = {"spmv2_gram_mrr": {"launches": 6}, "spmv_step_mrr_nox": {"launches": 4}}
+    stored = {"spmv2_gram_mrr": (4.56e9, 16.09e9), "spmv_step_mrr_nox": (6.7e9, 18e9)}
+    args = argparse.Namespace(profile_every=4, config="C4", steps=8)
+    run = {"elapsed": 8 * 9.5e-3}
+    out = bench.step_roofline(kernels, stored, run, args, 5, n, nnz, "kskipmrr", 4)
+    assert out["stored_bytes_per_step"] == round((6 * 4.56e9 + 4 * 6.7e9) / 2)
+    assert abs(out["survey_csr_bytes_per_iteration"] / 1e9 - 48.27) < 0.01
+    assert abs(out["survey_csr_ideal_its"] - 165.7) < 0.2
+    assert 0 < out["frac"] == round(out["achieved"] / 8000.0, 4) or abs(
+        out["frac"] - out["achieved"] / 8000.0) < 1e-3
