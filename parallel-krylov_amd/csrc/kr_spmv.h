@@ -30,10 +30,12 @@ template <int NP>
 __device__ __forceinline__ void block_reduce_store(double (&acc)[NP > 0 ? NP : 1],
                                                    double* partials, int grid,
                                                    double* s_red /* NP*4 */,
-                                                   int accumulate = 0) {
+                                                   int accumulate = 0,
+                                                   int tid = threadIdx.x,
+                                                   int64_t bid = blockIdx.x) {
   if constexpr (NP > 0) {
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
       double v = acc[p];
@@ -42,13 +44,13 @@ __device__ __forceinline__ void block_reduce_store(double (&acc)[NP > 0 ? NP : 1
       if (lane == 0) s_red[p * 4 + wave] = v;
     }
     __syncthreads();
-    if (threadIdx.x < NP) {
-      const double* r = s_red + threadIdx.x * 4;
+    if (tid < NP) {
+      const double* r = s_red + tid * 4;
       double t = r[0];
       t = t + r[1];
       t = t + r[2];
       t = t + r[3];
-      double* dst = partials + (int64_t)threadIdx.x * grid + blockIdx.x;
+      double* dst = partials + (int64_t)tid * grid + bid;
       *dst = accumulate ? *dst + t : t;  // accumulate: a later launch of the same SpMV
     }
   }

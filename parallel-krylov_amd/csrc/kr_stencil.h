@@ -261,11 +261,25 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
   constexpr int NV = T::NV;                    // sums (input vectors of the SpMV)
   constexpr bool VIRT = is_virtual<EPI>();     // operand r1 formed from x1, x2, x3
   constexpr int NX = VIRT ? (EPI == EPI_XY_VP ? 2 : 3) : NV;  // physical input vectors
-  __shared__ double s_red[(NP > 0 ? NP : 1) * 4];
+  // NTM bit 6: two adjacent positions per workgroup (2 x kBlock threads).
+  // Half h of workgroup B runs virtual workgroup 16 (B >> 3) + 8 h + (B & 7):
+  // the same XCD, positions p and p + 1 of one plane segment, so the +-n FAR
+  // lines one half reads are the rows the other half loads on the same CU in
+  // the same visit. Every virtual workgroup visits the same blocks in the
+  // same order and writes the same partials as an unpaired launch with twice
+  // the grid (the host launches it only where both halves' walks agree).
+  constexpr bool PAIRW = (NTM & 64) && !RELOAD;
+  const int half = PAIRW ? __builtin_amdgcn_readfirstlane(threadIdx.x / kBlock) : 0;
+  const int tid = PAIRW ? (int)(threadIdx.x % kBlock) : (int)threadIdx.x;
+  const int64_t vb =
+      PAIRW ? 16 * (int64_t)(blockIdx.x >> 3) + 8 * half + (blockIdx.x & 7) : (int64_t)blockIdx.x;
+  const int64_t vgrid = PAIRW ? 2 * (int64_t)gridDim.x : (int64_t)gridDim.x;
+  __shared__ double s_redx[PAIRW ? 2 : 1][(NP > 0 ? NP : 1) * 4];
   __shared__ double s_tab[kVdMax];
-  __shared__ __attribute__((aligned(16))) double s_line[2][NV][kSLine];
-  const int tid = threadIdx.x;
-  if (tid < a.ntab) s_tab[tid] = a.vtab[tid];
+  __shared__ __attribute__((aligned(16))) double s_linex[PAIRW ? 2 : 1][2][NV][kSLine];
+  double* const s_red = s_redx[half];
+  auto& s_line = s_linex[half];
+  if (threadIdx.x < (unsigned)a.ntab) s_tab[threadIdx.x] = a.vtab[threadIdx.x];
 
   double acc[NP > 0 ? NP : 1];
 #pragma unroll
@@ -276,21 +290,21 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
   const int64_t W = P * kSBlock;
   const int64_t nrb = (a.n + kSBlock - 1) / kSBlock - a.rb_gap;
   const int64_t planes = (nrb + P - 1) / P;
-  const int64_t q = blockIdx.x & 7;
-  const int64_t w = blockIdx.x >> 3;
+  const int64_t q = vb & 7;
+  const int64_t w = vb >> 3;
   int64_t p, z0, z1;
   if (a.st_pm) {
     // position-major: XCD q walks positions [q P/8, (q+1) P/8) (neighbouring
     // positions, whose x rows are each other's +-512 offsets, share an L2)
     // over plane segment zs of Zt = grid / P; fewer, longer walks than
     // plane-major when the shard has few planes (an 8-GPU slab: 64)
-    const int64_t PP = P >> 3, Zt = gridDim.x / P;
+    const int64_t PP = P >> 3, Zt = vgrid / P;
     p = q * PP + w % PP;
     const int64_t zs = w / PP;
     z0 = planes * zs / Zt;
     z1 = planes * (zs + 1) / Zt;
   } else {
-    const int64_t Z = gridDim.x / (8 * P);
+    const int64_t Z = vgrid / (8 * P);
     p = w % P;
     const int64_t zs = w / P;
     const int64_t pl0 = planes * q / 8, npl = planes * (q + 1) / 8 - pl0;
@@ -304,8 +318,11 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
   // The plane-per-XCD split would leave all but two XCDs idle there.
   const int64_t G = gridDim.x;
   auto blk = [&](int64_t z) { return RELOAD ? (int64_t)blockIdx.x + z * G : z * P + p; };
+  // pairs: the odd position's test for both halves (equal wherever the host
+  // pairs; never one half at a barrier the other skips)
+  const int64_t pt = PAIRW ? (p | 1) : p;
   auto visit_ok = [&](int64_t z) {
-    return RELOAD ? blk(z) < nrb : (z < z1 && z * P + p < nrb);
+    return RELOAD ? blk(z) < nrb : (z < z1 && z * P + pt < nrb);
   };
   constexpr int NM_C = PAT ? (int)(PAT >> 28) : 8;
   const int nm = PAT ? NM_C : a.st_nm;
@@ -317,7 +334,7 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
   // NTM bit 5: +-1 neighbours by DPP within the wave (7-point pattern whose
   // NEAR slots are -1 and +1; the host checks), no LDS line, no barrier
   constexpr bool DPP = (NTM & 32) && PAT == kPat7;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   SStage<NX, NFAR, CB> sA, sB, sC;
   const SRes res = st_res<NX, CB>(a, xs);
   int buf = 0;
@@ -570,11 +587,14 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
     }
   }
   __syncthreads();
-  block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
+  block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate, tid, vb);
 }
 
+// Threads per workgroup of a stencil launch: NTM bit 6 pairs two positions.
+constexpr int st_threads(int ntm) { return (ntm & 64) ? 2 * kBlock : kBlock; }
+
 template <int EPI, int NFAR, uint32_t PAT, bool RELOAD, int NTM = 3, int CB = 8>
-__global__ __launch_bounds__(kBlock) void spmv_stencil_kernel(SpmvArgs a) {
+__global__ __launch_bounds__(st_threads(NTM)) void spmv_stencil_kernel(SpmvArgs a) {
   if (!spmv_entry<EPI>(a)) return;  // converged / the fused scalar step's test fired
   spmv_stencil_body<EPI, NFAR, PAT, RELOAD, NTM, CB>(a);
 }
@@ -582,7 +602,7 @@ __global__ __launch_bounds__(kBlock) void spmv_stencil_kernel(SpmvArgs a) {
 // instead of 3 (512^3 dual -1-4 %, products-only -4 %, 64-plane slab -6/-12 %).
 // The three-vector first-steps kernel and the RELOAD walk would spill there.
 template <int EPI, int NFAR, uint32_t PAT, bool RELOAD, int NTM = 3, int CB = 8>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KR_ST_W4)))
+__global__ __launch_bounds__(st_threads(NTM)) __attribute__((amdgpu_waves_per_eu(KR_ST_W4)))
 void spmv_stencil_kernel_w4(SpmvArgs a) {
   if (!spmv_entry<EPI>(a)) return;
   spmv_stencil_body<EPI, NFAR, PAT, RELOAD, NTM, CB>(a);
@@ -593,7 +613,7 @@ void spmv_stencil_kernel_w4(SpmvArgs a) {
 #define KR_ST_PO_W 4
 #endif
 template <int EPI, int NFAR, uint32_t PAT, bool RELOAD, int NTM = 3, int CB = 8>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KR_ST_PO_W)))
+__global__ __launch_bounds__(st_threads(NTM)) __attribute__((amdgpu_waves_per_eu(KR_ST_PO_W)))
 void spmv_stencil_kernel_po(SpmvArgs a) {
   if (!spmv_entry<EPI>(a)) return;
   spmv_stencil_body<EPI, NFAR, PAT, RELOAD, NTM, CB>(a);
@@ -616,17 +636,51 @@ inline bool st_dpp(const SpmvArgs& a, bool products_only) {
   return (v == 2 || (v == 1 && products_only)) && a.st_off[2] == -1 && a.st_off[4] == 1;
 }
 
+// Position pairs (NTM bit 6) where both halves of every workgroup walk the
+// same planes: position-major, P % 16 == 0 (adjacent positions share an XCD
+// eighth), whole planes, a grid of whole (XCD, position) columns; not for the
+// EPIs whose kernel entry runs a block-wide prologue sized for kBlock.
+// KR_STENCIL_PAIR (bit mask, A/B): 1 products-only duals, 2 storing duals,
+// 4 the single-vector fused steps (is_step), 8 the fused first two steps,
+// 16 every other 7-point launch.
+template <int E>
+inline bool st_pair(const SpmvArgs& a, int nblocks) {
+  if constexpr (E == EPI_XY_VP || E == EPI_MRR_V) {
+    return false;
+  } else {
+    const char* e = getenv("KR_STENCIL_PAIR");  // read per launch: tests switch it
+    const int m = e ? atoi(e) : 0;
+    constexpr bool dual = E == EPI_DUAL_MRR || E == EPI_DUAL_KCG || E == EPI_DUAL_NONE;
+    const int bit = (dual && a.products_only) ? 1
+                    : dual                        ? 2
+                    : E == EPI_STEP_MRR_FIRST2    ? 8
+                    : is_step<E>()                ? 4
+                                                  : 16;
+    if (!(m & bit) || !a.st_pm || a.rb_gap != 0 || a.st_P <= 0 || a.st_P % 16 != 0) return false;
+    const int64_t nrb = (a.n + kSBlock - 1) / kSBlock;
+    return nrb % a.st_P == 0 && nblocks % a.st_P == 0 && nblocks % 16 == 0;
+  }
+}
+
 // The 7-point pattern's launch at the shard's code width.
 template <int E, bool RELOAD, int NTM, bool W4>
 void st_launch_pat7(const SpmvArgs& a, int nblocks, size_t lds, hipStream_t s) {
+  if constexpr (!RELOAD && !(NTM & 64)) {
+    if (st_pair<E>(a, nblocks)) {
+      st_launch_pat7<E, RELOAD, NTM | 64, W4>(a, nblocks, lds, s);
+      return;
+    }
+  }
+  constexpr int TH = st_threads(NTM);
+  const int nb = (NTM & 64) ? nblocks / 2 : nblocks;
   auto go = [&](auto cbc) {
     constexpr int CB = decltype(cbc)::value;
     if constexpr (W4 && (NTM & 4))
-      spmv_stencil_kernel_po<E, 2, kPat7, RELOAD, NTM, CB><<<nblocks, kBlock, lds, s>>>(a);
+      spmv_stencil_kernel_po<E, 2, kPat7, RELOAD, NTM, CB><<<nb, TH, lds, s>>>(a);
     else if constexpr (W4)
-      spmv_stencil_kernel_w4<E, 2, kPat7, RELOAD, NTM, CB><<<nblocks, kBlock, lds, s>>>(a);
+      spmv_stencil_kernel_w4<E, 2, kPat7, RELOAD, NTM, CB><<<nb, TH, lds, s>>>(a);
     else
-      spmv_stencil_kernel<E, 2, kPat7, RELOAD, NTM, CB><<<nblocks, kBlock, lds, s>>>(a);
+      spmv_stencil_kernel<E, 2, kPat7, RELOAD, NTM, CB><<<nb, TH, lds, s>>>(a);
   };
   switch (a.st_cb) {
     case 2: go(std::integral_constant<int, 2>{}); return;

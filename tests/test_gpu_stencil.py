@@ -102,6 +102,11 @@ MATRICES = {
     "box512x8x16": lambda: box(512, 8, 16),                    # W = 4096: P = 8
     "box512x16x12": lambda: box(512, 16, 12),                  # P = 16, 12 planes
     "aniso512x8x12": lambda: aniso(512, 8, 12, 1.0, 0.5, 0.25),  # 4-bit codes
+    # P % 16 == 0: position pairs (KR_STENCIL_PAIR)
+    "box128x64x20": lambda: box(128, 64, 20),                  # W = 8192: P = 16
+    "aniso64x128x18": lambda: aniso(64, 128, 18, 1.0, 0.5, 0.25),  # P = 16, 4-bit codes
+    "vals40_128x64x10": lambda: revalued(box(128, 64, 10), 40),    # P = 16, 8-bit codes
+    "box128x128x16": lambda: box(128, 128, 16),                # P = 32
 }
 # stencil code width (bits per slot) the engine picks for the 7-point pattern
 EXPECT_CB = {"aniso32x32x7": 4, "vals3_32x32x7": 2, "vals15_64x64x9": 4, "vals40_32x32x7": 8,
@@ -215,7 +220,8 @@ CASES = [
     ("kskipmrr", "band_far2", 5, 1), ("adaptivekskipmrr", "p2d512x6", 6, 1),
     ("kskipmrr", "box64x64x20", 4, 1), ("adaptivekskipmrr", "box64x64x20", 6, 2),
     ("kskipcg", "box128x32x9", 3, 3), ("kskipmrr", "aniso32x32x7", 4, 1),
-    ("adaptivekskipmrr", "aniso32x32x7", 8, 2),
+    ("adaptivekskipmrr", "aniso32x32x7", 8, 2), ("kskipmrr", "box128x64x20", 4, 1),
+    ("adaptivekskipmrr", "box128x128x16", 6, 2),
     # the fused basis pair (one shard, n = 512): level 1 stays on chip, both
     # duals' products summed in the dual launches' order
     ("kskipmrr", "box512x8x16", 4, 1), ("kskipmrr", "box512x16x12", 5, 1),
@@ -375,6 +381,41 @@ def test_stencil_dpp_neighbours_bitwise(monkeypatch, method, name, k, shards):
     out = []
     for dpp in ("0", "1", "2"):
         monkeypatch.setenv("KR_STENCIL_DPP", dpp)
+        with contextlib.redirect_stdout(io.StringIO()):
+            x, info = _solver(method)(A, b, **kw)
+        out.append((x.cpu().numpy(), info))
+    for x1, i1 in out[1:]:
+        np.testing.assert_array_equal(i1["nosl"], out[0][1]["nosl"])
+        np.testing.assert_array_equal(i1["residual"], out[0][1]["residual"])
+        np.testing.assert_array_equal(x1, out[0][0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method,name,k,shards", [
+    ("kskipmrr", "box128x64x20", 4, "0"),
+    ("kskipmrr", "box512x16x12", 4, "0"),
+    ("kskipmrr", "box128x64x20", 4, "0,0"),
+    ("adaptivekskipmrr", "aniso64x128x18", 6, "0"),
+    ("kskipcg", "vals40_128x64x10", 3, "0"),
+    ("kskipmrr", "box128x128x16", 5, "0,0,0,0"),
+    ("cg", "box128x128x16", 0, "0"),
+    ("mrr", "box128x64x20", 0, "0,0"),
+    ("kskipmrr", "box64x64x20", 4, "0"),     # P = 8: never paired
+])
+def test_stencil_position_pairs_bitwise(monkeypatch, method, name, k, shards):
+    """Two adjacent positions per workgroup (KR_STENCIL_PAIR bit mask: 1
+    products-only duals, 2 storing duals, 4/8 the fused steps, 16 the rest) run
+    the same virtual workgroups as the unpaired walk: the same histories and
+    x bit for bit, sharded (boundary launches stay unpaired) or not."""
+    A = MATRICES[name]()
+    b = np.random.default_rng(11).standard_normal(A.shape[0])
+    kw = dict(tol=1e-10, maxiter=200)
+    if k:
+        kw["k"] = k
+    monkeypatch.setenv("KRYLOV_AMD_SHARDS", shards)
+    out = []
+    for mask in ("0", "3", "31"):
+        monkeypatch.setenv("KR_STENCIL_PAIR", mask)
         with contextlib.redirect_stdout(io.StringIO()):
             x, info = _solver(method)(A, b, **kw)
         out.append((x.cpu().numpy(), info))
