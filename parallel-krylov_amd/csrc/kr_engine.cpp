@@ -2008,6 +2008,19 @@ std::vector<double> System::reduce(int nslots) {
     KR_HIP_CHECK(hipStreamSynchronize(s.stream));
   }
   host_wait_s += now_seconds() - w0;
+  // KR_POISON=1 (debug): the consumed slots' partials become NaN, so a later
+  // reduction that reads a partial no launch rewrote shows up as NaN (the GPU
+  // suites pass with it: every reduced partial is rewritten before reuse)
+  static const bool poison = [] {
+    const char* e = getenv("KR_POISON");
+    return e && atoi(e) != 0;
+  }();
+  if (poison)
+    for (auto& s : shards) {
+      KR_HIP_CHECK(hipSetDevice(s.dev));
+      KR_HIP_CHECK(hipMemsetAsync(s.partials, 0xFF, sizeof(double) * (size_t)nslots * s.pstride,
+                                  s.stream));
+    }
   // Fixed order: global shard 0, 1, ... (identical for in-process and RCCL).
   if (hybrid()) {
     const size_t per = (size_t)kMaxLocal * nslots;

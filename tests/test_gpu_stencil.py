@@ -110,13 +110,15 @@ MATRICES = {
 }
 # stencil code width (bits per slot) the engine picks for the 7-point pattern
 EXPECT_CB = {"aniso32x32x7": 4, "vals3_32x32x7": 2, "vals15_64x64x9": 4, "vals40_32x32x7": 8,
-             "p3d32": 2, "p3d64": 2, "box64x64x20": 2, "box512x8x16": 2, "aniso512x8x12": 4}
+             "p3d32": 2, "p3d64": 2, "box64x64x20": 2, "box512x8x16": 2, "aniso512x8x12": 4,
+             "aniso64x128x18": 4, "vals40_128x64x10": 8, "box128x64x20": 2}
 # expected stencil walk P (0: the row walk serves the matrix)
 EXPECT_P = {"p3d32": 2, "p3d64": 8, "box32x32x7": 2, "box64x16x9": 2, "box48x32x5": 3,
             "box32x32x3": 2, "p2d512x6": 1, "band_far": 1, "band_far2": 2,
             "box64x64x20": 8, "box128x32x9": 8, "aniso32x32x7": 2, "vals3_32x32x7": 2,
             "vals15_64x64x9": 8, "vals40_32x32x7": 2, "box512x8x16": 8, "box512x16x12": 16,
-            "aniso512x8x12": 8}
+            "aniso512x8x12": 8, "box128x64x20": 16, "aniso64x128x18": 16,
+            "vals40_128x64x10": 16, "box128x128x16": 32}
 NOT_STENCIL = {
     "p3d24": lambda: golden_matrix(["poisson", 24, 3]),      # 576 % 512 != 0
     "p3d16": lambda: golden_matrix(["poisson", 16, 3]),
