@@ -1626,8 +1626,19 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
   // blocks) adds into the first entries.
   const int np = spmv_products(epi);
   auto grid_of = [&](const Shard& s) { return po_shard(s) ? s.spmv_grid_po : s.spmv_grid; };
+  // KR_ZIGZAG=1 (A/B): stencil walks alternate their dispatch order launch by
+  // launch, so each starts on the plane segments the previous kernel streamed
+  // last. Bitwise neutral; measured neutral on C4 (522.3 vs 522.1 it/s, same
+  // box, three pairs: the first-steps kernel +2.5 %, the others -0.5-1 %).
+  const char* zz = getenv("KR_ZIGZAG");  // read per call: tests switch it
+  const bool zigzag = zz && atoi(zz) != 0;
   auto launch_full = [&](Shard& s, int64_t r_begin, int64_t rows) {
-    launch_spmv_grid(epi, args_for(s, r_begin, rows, s.pstride, 0), grid_of(s), s.stream);
+    SpmvArgs a = args_for(s, r_begin, rows, s.pstride, 0);
+    if (s.scode && zigzag) {
+      a.st_rev = s.st_flip;
+      s.st_flip ^= 1;
+    }
+    launch_spmv_grid(epi, a, grid_of(s), s.stream);
     for (int p = 0; p < np; ++p) s.slot_n[slot0 + p] = grid_of(s);
   };
 

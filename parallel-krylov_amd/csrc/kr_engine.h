@@ -122,6 +122,7 @@ struct Shard {
   double* hst = nullptr;        // pinned copy of st
   // vectors, each ld doubles, zero-initialised
   std::vector<double*> vec;
+  int st_flip = 0;  // the next stencil walk launch runs reversed (SpmvArgs::st_rev)
   hipEvent_t ev_a = nullptr, ev_b = nullptr;
   // profiling (event pairs pending until the next sync)
   struct Pending {

@@ -189,6 +189,11 @@ struct SpmvArgs {
   // 0: plane-major: XCD q takes an eighth of the planes at every position;
   // grid = 8 P x segments. See kr_stencil.h.
   int st_pm = 0;
+  // 1: dispatch order reversed -- workgroup b runs the walk of workgroup
+  // grid - 1 - b (same visits, same partials), so the top plane segments go
+  // first. The engine alternates it per launch with KR_ZIGZAG=1 (A/B): the
+  // next kernel starts on the planes the previous one touched last.
+  int st_rev = 0;
   int32_t st_off[8] = {};
   int32_t st_kind[8] = {};
   int32_t st_far[4] = {};

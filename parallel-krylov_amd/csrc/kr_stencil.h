@@ -271,8 +271,8 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
   constexpr bool PAIRW = (NTM & 64) && !RELOAD;
   const int half = PAIRW ? __builtin_amdgcn_readfirstlane(threadIdx.x / kBlock) : 0;
   const int tid = PAIRW ? (int)(threadIdx.x % kBlock) : (int)threadIdx.x;
-  const int64_t vb =
-      PAIRW ? 16 * (int64_t)(blockIdx.x >> 3) + 8 * half + (blockIdx.x & 7) : (int64_t)blockIdx.x;
+  const int64_t pb = (!RELOAD && a.st_rev) ? (int64_t)gridDim.x - 1 - blockIdx.x : blockIdx.x;
+  const int64_t vb = PAIRW ? 16 * (pb >> 3) + 8 * half + (pb & 7) : pb;
   const int64_t vgrid = PAIRW ? 2 * (int64_t)gridDim.x : (int64_t)gridDim.x;
   __shared__ double s_redx[PAIRW ? 2 : 1][(NP > 0 ? NP : 1) * 4];
   __shared__ double s_tab[kVdMax];

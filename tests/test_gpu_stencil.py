@@ -407,7 +407,8 @@ def test_stencil_dpp_neighbours_bitwise(monkeypatch, method, name, k, shards):
 def test_stencil_position_pairs_bitwise(monkeypatch, method, name, k, shards):
     """Two adjacent positions per workgroup (KR_STENCIL_PAIR bit mask: 1
     products-only duals, 2 storing duals, 4/8 the fused steps, 16 the rest) run
-    the same virtual workgroups as the unpaired walk: the same histories and
+    the same virtual workgroups as the unpaired walk, and so does the reversed
+    dispatch order of every other launch (KR_ZIGZAG): the same histories and
     x bit for bit, sharded (boundary launches stay unpaired) or not."""
     A = MATRICES[name]()
     b = np.random.default_rng(11).standard_normal(A.shape[0])
@@ -416,8 +417,9 @@ def test_stencil_position_pairs_bitwise(monkeypatch, method, name, k, shards):
         kw["k"] = k
     monkeypatch.setenv("KRYLOV_AMD_SHARDS", shards)
     out = []
-    for mask in ("0", "3", "31"):
+    for mask, zz in (("0", "0"), ("0", "1"), ("3", "1"), ("31", "0")):
         monkeypatch.setenv("KR_STENCIL_PAIR", mask)
+        monkeypatch.setenv("KR_ZIGZAG", zz)
         with contextlib.redirect_stdout(io.StringIO()):
             x, info = _solver(method)(A, b, **kw)
         out.append((x.cpu().numpy(), info))
