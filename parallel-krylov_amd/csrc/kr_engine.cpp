@@ -1441,6 +1441,11 @@ void System::halo_in_process(Shard& s, int id1, int id2, int id3) {
   // previous SpMV's boundary rows read the same halo when consecutive SpMVs
   // share an input vector) must be done first, not only the peer's.
   KR_HIP_CHECK(hipStreamWaitEvent(s.comm_stream, s.ev_in, 0));
+  // Peers on this device: one gather launch for every piece (KR_HALO_KERNEL=0:
+  // a hipMemcpyAsync per piece); peers on other devices: peer copies.
+  const char* hk = getenv("KR_HALO_KERNEL");
+  const bool gather = !hk || atoi(hk) != 0;
+  HaloGatherArgs g;
   for (auto& p : s.recv) {
     Shard& t = shards[p.peer];
     KR_HIP_CHECK(hipStreamWaitEvent(s.comm_stream, t.ev_in, 0));
@@ -1448,14 +1453,21 @@ void System::halo_in_process(Shard& s, int id1, int id2, int id3) {
       if (id < 0) continue;
       double* dst = s.vec[id] + s.local_index(p.g0);
       const double* src = t.vec[id] + t.local_index(p.g0);
-      if (s.dev == t.dev)
+      if (s.dev == t.dev && gather && g.n < kHaloPieces) {
+        g.src[g.n] = src;
+        g.dst[g.n] = dst;
+        g.count[g.n] = p.count;
+        ++g.n;
+      } else if (s.dev == t.dev) {
         KR_HIP_CHECK(hipMemcpyAsync(dst, src, 8 * (size_t)p.count, hipMemcpyDeviceToDevice,
                                     s.comm_stream));
-      else
+      } else {
         KR_HIP_CHECK(hipMemcpyPeerAsync(dst, s.dev, src, t.dev, 8 * (size_t)p.count,
                                         s.comm_stream));
+      }
     }
   }
+  launch_halo_gather(g, s.comm_stream);  // after every wait above
   KR_HIP_CHECK(hipEventRecord(s.ev_out, s.comm_stream));
 }
 

@@ -1188,6 +1188,38 @@ void launch_finalize_counts(const double* partials, int stride, const SlotCounts
   KR_HIP_CHECK(hipGetLastError());
 }
 
+namespace {
+// blockIdx.y = piece; each workgroup copies kHaloChunk doubles of it (a
+// plain copy: the values are moved, never combined, so the halo is bitwise
+// the peer's rows as with hipMemcpyAsync).
+constexpr int kHaloChunk = 8 * kBlock;
+__global__ __launch_bounds__(kBlock) void halo_gather_kernel(HaloGatherArgs a) {
+  const int q = blockIdx.y;
+  const int64_t cnt = a.count[q];
+  const double* __restrict__ src = a.src[q];
+  double* __restrict__ dst = a.dst[q];
+  const int64_t base = (int64_t)blockIdx.x * kHaloChunk;
+  if (base >= cnt) return;
+#pragma unroll
+  for (int j = 0; j < kHaloChunk / kBlock; ++j) {
+    const int64_t i = base + j * kBlock + threadIdx.x;
+    if (i < cnt) dst[i] = src[i];
+  }
+}
+}  // namespace
+
+void launch_halo_gather(const HaloGatherArgs& a, hipStream_t s) {
+  KR_REQUIRE(a.n >= 0 && a.n <= kHaloPieces, "halo gather: bad piece count");
+  if (a.n == 0) return;
+  int64_t most = 0;
+  for (int q = 0; q < a.n; ++q) most = std::max(most, a.count[q]);
+  if (most == 0) return;
+  const int64_t gx = (most + kHaloChunk - 1) / kHaloChunk;
+  KR_REQUIRE(gx < ((int64_t)1 << 31), "halo gather: piece too long");
+  halo_gather_kernel<<<dim3((unsigned)gx, (unsigned)a.n), kBlock, 0, s>>>(a);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
 void launch_multidot(const MultiDotArgs& a, hipStream_t s) {
   KR_REQUIRE(a.count >= 0 && a.count <= 64, "multidot: count must be in [0, 64]");
   for (int base = 0; base < a.count; base += 16) {
