@@ -77,6 +77,18 @@ struct SStage {
   dbl2v el[NX], er[NX];       // the line's edges x[r0-2..r0-1], x[r0+512..r0+513] (uniform)
 };
 
+// Any of the first nm slots of a row's code word absent (field all ones)?
+template <int CB, typename Code>
+__device__ __forceinline__ bool st_any_absent(Code c, int nm) {
+  Code m = c;
+#pragma unroll
+  for (int b = 1; b < CB; ++b) m &= c >> b;  // bit CB k: field k all ones
+  Code low = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) low |= (k < nm) ? ((Code)1 << (CB * k)) : (Code)0;
+  return (m & low) != 0;
+}
+
 // Uniform 16-byte load through the scalar cache (s_load_dwordx4: counted by
 // lgkmcnt, so it never lengthens a vector-memory wait). x is read-only while
 // the kernel runs. i even, clamped like st_ld2.
@@ -432,10 +444,18 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
       __syncthreads();
       issue_edges(nxs, zn);
     }
-    // (4) the two rows' sums, slot by slot in ascending offset order
+    // (4) the two rows' sums, slot by slot in ascending offset order. A
+    // visit whose rows (every lane of the wave) have all nm slots present --
+    // all but the grid's faces -- runs the straight-line sums (one uniform
+    // branch per visit, not per slot: per-slot branches cost phi copies).
     double slo[NV], shi[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) slo[v] = shi[v] = 0.0;
+    const bool all_present =
+        __builtin_amdgcn_ballot_w64(st_any_absent<CB>(cur.clo, nm) ||
+                                    st_any_absent<CB>(cur.chi, nm)) == 0;
+    auto sums = [&](auto fast_c) {
+    constexpr bool FAST = decltype(fast_c)::value;
 #pragma unroll
     for (int k = 0; k < NM_C; ++k) {
       if (k >= nm) break;
@@ -493,25 +513,27 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
           for (int v = 0; v < NV; ++v) { xlo[v] = g[v].x; xhi[v] = g[v].y; }
         }
       }
-      // Slot k present in both rows of every lane of the wave (the common
-      // case: absent entries sit at the grid's faces): no selects.
-      if (__builtin_amdgcn_ballot_w64(clo == kNone || chi == kNone) == 0) {
+      if constexpr (FAST) {
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
           slo[v] = slo[v] + vlo * xlo[v];
           shi[v] = shi[v] + vhi * xhi[v];
         }
       } else {
-        if (clo != kNone) {
 #pragma unroll
-          for (int v = 0; v < NV; ++v) slo[v] = slo[v] + vlo * xlo[v];
-        }
-        if (chi != kNone) {
-#pragma unroll
-          for (int v = 0; v < NV; ++v) shi[v] = shi[v] + vhi * xhi[v];
+        for (int v = 0; v < NV; ++v) {
+          const double plo = slo[v] + vlo * xlo[v];
+          const double phi = shi[v] + vhi * xhi[v];
+          slo[v] = clo != kNone ? plo : slo[v];
+          shi[v] = chi != kNone ? phi : shi[v];
         }
       }
     }
+    };
+    if (all_present)
+      sums(std::true_type{});
+    else
+      sums(std::false_type{});
     // (5) epilogue: row 2t, then row 2t+1 (products in that order)
     {
       const EpiIn ilo = st_epi_in<EPI>(cen[0].x, NX > 1 ? cen[NX > 1 ? 1 : 0].x : 0.0,
