@@ -77,16 +77,17 @@ struct SStage {
   dbl2v el[NX], er[NX];       // the line's edges x[r0-2..r0-1], x[r0+512..r0+513] (uniform)
 };
 
-// Any of the first nm slots of a row's code word absent (field all ones)?
+// Absent slots among the first nm of a row's code word (field all ones):
+// bit CB k set for an absent slot k.
 template <int CB, typename Code>
-__device__ __forceinline__ bool st_any_absent(Code c, int nm) {
+__device__ __forceinline__ Code st_absent_bits(Code c, int nm) {
   Code m = c;
 #pragma unroll
-  for (int b = 1; b < CB; ++b) m &= c >> b;  // bit CB k: field k all ones
+  for (int b = 1; b < CB; ++b) m &= c >> b;
   Code low = 0;
 #pragma unroll
   for (int k = 0; k < 8; ++k) low |= (k < nm) ? ((Code)1 << (CB * k)) : (Code)0;
-  return (m & low) != 0;
+  return m & low;
 }
 
 // Uniform 16-byte load through the scalar cache (s_load_dwordx4: counted by
@@ -451,11 +452,29 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
     double slo[NV], shi[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) slo[v] = shi[v] = 0.0;
-    const bool all_present =
-        __builtin_amdgcn_ballot_w64(st_any_absent<CB>(cur.clo, nm) ||
-                                    st_any_absent<CB>(cur.chi, nm)) == 0;
-    auto sums = [&](auto fast_c) {
-    constexpr bool FAST = decltype(fast_c)::value;
+    // Faces: when every lane's absent entries sit in ONE slot (the usual
+    // face: the x faces' -1 / +1, the y faces' -n / +n, ...), only that
+    // slot takes the per-row selects (7-point pattern; else every slot).
+    using AM = typename SStage<NX, NFAR, CB>::Code;
+    const AM am = st_absent_bits<CB>(cur.clo, nm) | st_absent_bits<CB>(cur.chi, nm);
+    const uint64_t amb = __builtin_amdgcn_ballot_w64(am != 0);
+    int sel = -1;  // -1: every slot present; 0..7: only that slot has absents; 8: several
+    if (amb != 0) {
+      const int l0 = (int)__builtin_ctzll(amb);
+      AM m0;
+      if constexpr (sizeof(AM) == 8) {
+        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)am, l0);
+        const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(am >> 32), l0);
+        m0 = ((AM)hi << 32) | lo;
+      } else {
+        m0 = (AM)__builtin_amdgcn_readlane((uint32_t)am, l0);
+      }
+      const bool same = __builtin_amdgcn_ballot_w64(am != 0 && am != m0) == 0;
+      const bool one = (m0 & (m0 - 1)) == 0;
+      sel = (same && one) ? (int)(__builtin_ctzll((uint64_t)m0) / CB) : 8;
+    }
+    auto sums = [&](auto sel_c) {
+    constexpr int SEL = decltype(sel_c)::value;
 #pragma unroll
     for (int k = 0; k < NM_C; ++k) {
       if (k >= nm) break;
@@ -513,7 +532,7 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
           for (int v = 0; v < NV; ++v) { xlo[v] = g[v].x; xhi[v] = g[v].y; }
         }
       }
-      if constexpr (FAST) {
+      if (SEL < 0 || (SEL < 8 && k != SEL)) {
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
           slo[v] = slo[v] + vlo * xlo[v];
@@ -530,10 +549,22 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
       }
     }
     };
-    if (all_present)
-      sums(std::true_type{});
-    else
-      sums(std::false_type{});
+    if (sel < 0) {
+      sums(std::integral_constant<int, -1>{});
+    } else if constexpr (PAT == kPat7) {
+      switch (sel) {
+        case 0: sums(std::integral_constant<int, 0>{}); break;
+        case 1: sums(std::integral_constant<int, 1>{}); break;
+        case 2: sums(std::integral_constant<int, 2>{}); break;
+        case 3: sums(std::integral_constant<int, 3>{}); break;
+        case 4: sums(std::integral_constant<int, 4>{}); break;
+        case 5: sums(std::integral_constant<int, 5>{}); break;
+        case 6: sums(std::integral_constant<int, 6>{}); break;
+        default: sums(std::integral_constant<int, 8>{}); break;
+      }
+    } else {
+      sums(std::integral_constant<int, 8>{});
+    }
     // (5) epilogue: row 2t, then row 2t+1 (products in that order)
     {
       const EpiIn ilo = st_epi_in<EPI>(cen[0].x, NX > 1 ? cen[NX > 1 ? 1 : 0].x : 0.0,
