@@ -47,6 +47,8 @@ double* primitive_scratch(size_t doubles) {
     if (hipMalloc(&slot.first, doubles * sizeof(double)) != hipSuccess)
       throw Failure(KR_ERR_NOMEM, "scratch allocation failed");
     slot.second = doubles;
+    fresh_fill(slot.first, doubles * sizeof(double), nullptr);
+    if (poison_alloc()) KR_HIP_CHECK(hipDeviceSynchronize());
   }
   return slot.first;
 }
@@ -522,6 +524,7 @@ void* dmalloc(Shard& s, size_t bytes) {
   if (hipMalloc(&p, bytes ? bytes : 8) != hipSuccess)
     throw Failure(KR_ERR_NOMEM, "matrix allocation failed");
   s.owned.push_back(p);
+  fresh_fill(p, bytes, s.stream);  // KR_POISON_ALLOC: the generators must write every entry
   return p;
 }
 

@@ -24,6 +24,19 @@ double now_seconds() {
   return std::chrono::duration<double>(clk::now().time_since_epoch()).count();
 }
 
+bool poison_alloc() {
+  const char* e = getenv("KR_POISON_ALLOC");  // read per allocation: tests switch it
+  return e && atoi(e) != 0;
+}
+
+void fresh_fill(void* p, size_t bytes, hipStream_t s, int dflt) {
+  if (!p || bytes == 0) return;
+  if (poison_alloc())
+    KR_HIP_CHECK(hipMemsetAsync(p, 0xFF, bytes, s));
+  else if (dflt >= 0)
+    KR_HIP_CHECK(hipMemsetAsync(p, dflt, bytes, s));
+}
+
 namespace {
 
 int g_grid_cap = 0;
@@ -621,6 +634,7 @@ void System::build_masks(Shard& s) {
   KR_HIP_CHECK(hipMalloc(&mask, (size_t)s.n * (mw / 8)));
   s.owned.push_back(dM);
   s.owned.push_back(mask);
+  fresh_fill(mask, (size_t)s.n * (mw / 8), s.stream);
   KR_HIP_CHECK(hipMemcpyAsync(dM, M.data(), nm * sizeof(int32_t), hipMemcpyHostToDevice, s.stream));
   launch_masks(s.rowptr, s.rowptr64, s.n, s.col, s.pad, dM, nm, mw, mask, s.stream);
   if (dia_on) {
@@ -724,6 +738,8 @@ void System::build_stencil(Shard& s) {
   s.owned.push_back(code);
   s.owned.push_back(scratch);
   s.scratch = scratch;
+  fresh_fill(code, sizeof(uint64_t) * (size_t)s.n, s.stream);
+  fresh_fill(scratch, 64 * sizeof(double), s.stream);
   launch_stencil_codes(s.rowptr, s.rowptr64, s.n, s.col, s.vcode, s.pad, s.moff, s.nm, code,
                        s.stream);
   // Narrow codes for the 7-point pattern (the kernel's compile-time slot
@@ -744,6 +760,7 @@ void System::build_stencil(Shard& s) {
     cb = 8;
   }
   if (narrow) {
+    fresh_fill(narrow, (size_t)cb * (size_t)s.n, s.stream);
     launch_stencil_pack(code, s.n, cb, narrow, s.stream);
     KR_HIP_CHECK(hipStreamSynchronize(s.stream));
     s.owned.erase(std::find(s.owned.begin(), s.owned.end(), (void*)code));
@@ -1049,12 +1066,13 @@ void System::finalize() {
     s.pstride = std::max(s.grid, s.spmv_grid);
     s.slot_n.fill(0);
     KR_HIP_CHECK(hipMalloc(&s.partials, sizeof(double) * (size_t)kMaxSlots * s.pstride));
-    KR_HIP_CHECK(hipMemsetAsync(s.partials, 0, sizeof(double) * (size_t)kMaxSlots * s.pstride,
-                                s.stream));
+    fresh_fill(s.partials, sizeof(double) * (size_t)kMaxSlots * s.pstride, s.stream, 0);
     KR_HIP_CHECK(hipMalloc(&s.slots, sizeof(double) * kMaxSlots));
+    fresh_fill(s.slots, sizeof(double) * kMaxSlots, s.stream);
     // RCCL ranks' (or, on the first shard, in-process shards') slot totals
-    KR_HIP_CHECK(hipMalloc(&s.gather,
-                           sizeof(double) * kMaxSlots * std::max<size_t>(nranks, shards.size())));
+    const size_t gbytes = sizeof(double) * kMaxSlots * std::max<size_t>(nranks, shards.size());
+    KR_HIP_CHECK(hipMalloc(&s.gather, gbytes));
+    fresh_fill(s.gather, gbytes, s.stream);
     KR_HIP_CHECK(hipHostMalloc(&s.host, sizeof(double) * kMaxSlots * nranks, 0));
     if (!s.ev_a) KR_HIP_CHECK(hipEventCreateWithFlags(&s.ev_a, hipEventDisableTiming));
     if (!s.ev_b) KR_HIP_CHECK(hipEventCreateWithFlags(&s.ev_b, hipEventDisableTiming));
@@ -1073,13 +1091,17 @@ void System::finalize() {
       KR_HIP_CHECK(hipSetDevice(s0.dev));
       for (auto* list : {&t.send, &t.recv})
         for (auto& p : *list)
-          if (owner[p.peer] != comm->rank && p.count > 0)
+          if (owner[p.peer] != comm->rank && p.count > 0) {
             KR_HIP_CHECK(hipMalloc(&p.stage, sizeof(double) * 3 * (size_t)p.count));
+            fresh_fill(p.stage, sizeof(double) * 3 * (size_t)p.count, s0.stream);
+          }
     }
     KR_HIP_CHECK(hipSetDevice(s0.dev));
     KR_HIP_CHECK(hipMalloc(&hy_send, sizeof(double) * kMaxLocal * kMaxSlots));
     KR_HIP_CHECK(hipMemset(hy_send, 0, sizeof(double) * kMaxLocal * kMaxSlots));
     KR_HIP_CHECK(hipMalloc(&hy_recv, sizeof(double) * kMaxLocal * kMaxSlots * nranks));
+    fresh_fill(hy_recv, sizeof(double) * kMaxLocal * kMaxSlots * nranks, s0.stream);
+    KR_HIP_CHECK(hipStreamSynchronize(s0.stream));
     KR_HIP_CHECK(hipHostMalloc(&hy_host, sizeof(double) * kMaxLocal * kMaxSlots * nranks, 0));
     if (!hy_ev) KR_HIP_CHECK(hipEventCreateWithFlags(&hy_ev, hipEventDisableTiming));
   }
@@ -1172,7 +1194,10 @@ void System::alloc_vectors(int count) {
     for (int i = 0; i < count; ++i) {
       if (hipMalloc(&s.vec[i], sizeof(double) * (size_t)s.ld) != hipSuccess)
         throw Failure(KR_ERR_NOMEM, "vector allocation failed");
-      KR_HIP_CHECK(hipMemsetAsync(s.vec[i], 0, sizeof(double) * (size_t)s.ld, s.stream));
+      // zeros (NaN under KR_POISON_ALLOC): pad and halo rows included, so a
+      // halo row read before its exchange, or a pad row read as an operand,
+      // is a NaN in the poison run. x0 = 0 is written explicitly (load_bx).
+      fresh_fill(s.vec[i], sizeof(double) * (size_t)s.ld, s.stream, 0);
     }
     KR_HIP_CHECK(hipStreamSynchronize(s.stream));
   }
@@ -1670,7 +1695,9 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
   // waits on events the previous one recorded on OTHER shards' streams, so
   // the phases are separated by the pool's barrier); otherwise serial.
   const bool threaded = !comm && pool;
-  auto phase_in = [&](Shard& s, size_t li) {
+  const char* wa = getenv("KR_BOUNDARY_WAIT_ALL");
+  const bool wait_all = wa && atoi(wa) != 0;
+  auto phase_in =[&](Shard& s, size_t li) {
     KR_HIP_CHECK(hipSetDevice(s.dev));
     prof_begin(s, nm, t0s[li]);
     KR_HIP_CHECK(hipEventRecord(s.ev_in, s.stream));
@@ -1697,7 +1724,10 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
       // own halo copied, and every shard that copies from this one done
       // reading its rows (the next kernels may overwrite them)
       KR_HIP_CHECK(hipStreamWaitEvent(s.stream, s.ev_out, 0));
-      for (int t : s.readers) KR_HIP_CHECK(hipStreamWaitEvent(s.stream, shards[t].ev_out, 0));
+      if (wait_all)  // KR_BOUNDARY_WAIT_ALL=1 (debug A/B): the round-2 edge set
+        for (auto& t : shards) KR_HIP_CHECK(hipStreamWaitEvent(s.stream, t.ev_out, 0));
+      else
+        for (int t : s.readers) KR_HIP_CHECK(hipStreamWaitEvent(s.stream, shards[t].ev_out, 0));
     } else {
       // own halo copied, and every reader done with this shard's rows
       for (auto& t : shards) KR_HIP_CHECK(hipStreamWaitEvent(s.stream, t.ev_out, 0));
@@ -1764,7 +1794,10 @@ void System::scalar_state_init(double gamma) {
   Shard& s0 = shards[0];
   for (auto& s : shards) {
     KR_HIP_CHECK(hipSetDevice(s.dev));
-    if (!s.st) KR_HIP_CHECK(hipMalloc(&s.st, sizeof(double) * kScalarState));
+    if (!s.st) {
+      KR_HIP_CHECK(hipMalloc(&s.st, sizeof(double) * kScalarState));
+      fresh_fill(s.st, sizeof(double) * kScalarState, s.stream);
+    }
   }
   KR_HIP_CHECK(hipSetDevice(s0.dev));
   if (!s0.hst) KR_HIP_CHECK(hipHostMalloc(&s0.hst, sizeof(double) * kScalarState, 0));
@@ -2086,6 +2119,8 @@ class Base : public Session {
       if (x0 && x0[li])
         KR_HIP_CHECK(hipMemcpyAsync(s.own(X), x0[li], 8 * (size_t)s.n,
                                     hipMemcpyDeviceToDevice, s.stream));
+      else  // x0 = 0 (v3/gpu/cg.py:12): not left to the allocation's fill
+        KR_HIP_CHECK(hipMemsetAsync(s.own(X), 0, 8 * (size_t)s.n, s.stream));
     }
     sys->ew(EW_DOT, 0, 0, {B, B, -1, -1, -1, -1}, 0);
     bnorm = std::sqrt(sys->reduce(1)[0]);

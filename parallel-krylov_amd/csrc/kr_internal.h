@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <stdexcept>
 #include <string>
@@ -38,6 +39,29 @@ struct Failure : std::runtime_error {
   do {                                                               \
     if (!(cond)) throw ::kr::Failure(KR_ERR_INVALID, std::string(msg)); \
   } while (0)
+
+// Dynamic LDS above 64 KiB is opted into per kernel AND per device
+// (hipFuncSetAttribute acts on the calling thread's current device). `done`
+// holds one bit per device; the per-shard host threads may race here, which
+// only repeats an idempotent attribute call.
+inline void opt_in_lds(std::atomic<uint64_t>& done, const void* fn, size_t lds) {
+  int dev = 0;
+  KR_HIP_CHECK(hipGetDevice(&dev));
+  const uint64_t bit = uint64_t(1) << (dev & 63);
+  if (done.load(std::memory_order_acquire) & bit) return;
+  KR_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  done.fetch_or(bit, std::memory_order_acq_rel);
+}
+
+// KR_POISON_ALLOC=1 (debug): every device buffer the engine allocates starts
+// as all-ones bytes (a NaN in every double) instead of zeros or whatever
+// hipMalloc left, so a read of memory nothing wrote shows up as NaN on the
+// first run. Buffers whose zeros are part of their meaning (DIA slots of
+// absent entries, code padding, counters) keep their explicit zero fill.
+bool poison_alloc();
+// The fill a fresh buffer gets: 0xFF bytes under KR_POISON_ALLOC, else
+// `dflt` (0 for buffers the engine zeroes, -1: left as allocated).
+void fresh_fill(void* p, size_t bytes, hipStream_t s, int dflt = -1);
 
 // ---------------------------------------------------------------------------
 // SpMV with fused epilogue reductions.

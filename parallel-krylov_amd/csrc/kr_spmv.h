@@ -2139,12 +2139,9 @@ template <int E, int NH>
 void spmv_diawalk_launch_t(const SpmvArgs& a, int nblocks, hipStream_t s) {
   constexpr int nv = EpiTraits<E>::NV;
   const size_t lds = sizeof(double) * ((size_t)(NH + 1) * kBlock + (size_t)nv * kWalkWin);
-  static size_t opted = 64 * 1024;  // dynamic LDS beyond 64 KiB is opted into per kernel
-  if (lds > opted) {
-    KR_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(spmv_diawalk_kernel<E, NH>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    opted = lds;
-  }
+  static std::atomic<uint64_t> opted{0};  // per device (opt_in_lds)
+  if (lds > 64 * 1024)
+    opt_in_lds(opted, reinterpret_cast<const void*>(spmv_diawalk_kernel<E, NH>), lds);
   spmv_diawalk_kernel<E, NH><<<nblocks, kBlock, lds, s>>>(a);
 }
 

@@ -1127,12 +1127,8 @@ constexpr size_t kS2Lds = sizeof(double) * 2 * (kS2B0 + kS2B1) * kSBlock;
 
 template <int CB, bool PO>
 void st2_launch_t(const SpmvArgs& a, int nblocks, hipStream_t s) {
-  static bool opted = false;
-  if (!opted) {
-    KR_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(spmv_stencil2_kernel<CB, PO>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kS2Lds));
-    opted = true;
-  }
+  static std::atomic<uint64_t> opted{0};  // per device (opt_in_lds)
+  opt_in_lds(opted, reinterpret_cast<const void*>(spmv_stencil2_kernel<CB, PO>), kS2Lds);
   spmv_stencil2_kernel<CB, PO><<<nblocks, kBlock, kS2Lds, s>>>(a);
   KR_HIP_CHECK(hipGetLastError());
 }
