@@ -353,7 +353,10 @@ int kr_solve_set_precond(kr_system* sys, const double* const* d_dev);
  * level schedules are built here); the sweeps run on the device, one
  * workgroup per sweep, levels separated by barriers. Needs a one-shard
  * system (KR_ERR_INVALID otherwise). l_rowptr == NULL clears it; either
- * set_precond call replaces the other's preconditioner. */
+ * set_precond call replaces the other's preconditioner. A solve uses the
+ * preconditioner set when its kr_solve_begin ran (the factors are shared
+ * with the session, the diagonal copied): a later set_precond call, or a
+ * clear, takes effect at the next kr_solve_begin. */
 int kr_solve_set_precond_ilu(kr_system* sys, int64_t n, const int64_t* l_rowptr,
                              const int32_t* l_col, const double* l_val, const int64_t* u_rowptr,
                              const int32_t* u_col, const double* u_val, const int64_t* perm_r,

@@ -535,8 +535,9 @@ void System::spmv_pair(int in1, int in2, int out1, int out2, int slot0) {
 
 // M^-1 v (shard 0): w = Pr v folded into the L sweep's loads, y = L^-1 w,
 // z = U^-1 y, out = Pc z folded into the U sweep's stores.
-void System::ilu_apply(int in, int out) {
-  KR_REQUIRE(ilu && shards.size() == 1, "ILU apply: no factors, or more than one shard");
+void System::ilu_apply(const IluFactors& f, int in, int out) {
+  KR_REQUIRE(shards.size() == 1, "ILU apply: more than one shard");
+  const IluFactors* ilu = &f;
   Shard& s = shards[0];
   KR_HIP_CHECK(hipSetDevice(s.dev));
   hipEvent_t t0;
@@ -2860,12 +2861,14 @@ class PipeCgSession : public Base {
  public:
   explicit PipeCgSession(int v) : variant(v) {}
   bool ilu = false;  // M^-1 by the ILU sweeps (System::ilu), d = 1
+  std::shared_ptr<IluFactors> ilu_f;  // the factors set when the solve began
 
   void begin(const double* const* b, const double* const* x0) override {
     sys->alloc_vectors(NV);
     load_bx(B, X, b, x0);
     // d: the caller's diagonal, else ones (ILU: ones, and M^-1 by the sweeps)
-    ilu = sys->ilu != nullptr;
+    ilu_f = sys->ilu;
+    ilu = ilu_f != nullptr;
     const bool have = !ilu && !sys->precond.empty();
     for (size_t li = 0; li < sys->shards.size(); ++li) {
       Shard& s = sys->shards[li];
@@ -2879,7 +2882,7 @@ class PipeCgSession : public Base {
     sys->spmv(EPI_BMINUS, X, -1, R, -1, -1, B, 0);      // r = b - A x
     sys->ew_n(EW_PRE, 0, 0, ids({R, U, D}), 1);           // u = M^-1 r ; <r,r> <r,u>
     if (ilu) {                                            // u = ilu.solve(r) ; <r,u>: slot 3
-      sys->ilu_apply(R, U);
+      sys->ilu_apply(*ilu_f, R, U);
       sys->ew(EW_DOT, 0, 0, {R, U, -1, -1, -1, -1}, 3);
     }
     const auto g = sys->reduce(ilu ? 4 : 3);              // slot 0: <r,r> of the SpMV
@@ -2920,7 +2923,7 @@ class PipeCgSession : public Base {
         alpha = gamma / sigma;
         sys->ew_n(EW_PCG, alpha, 0, ids({X, P, R, S, U, D}), 0);  // x, r, u ; <r,r> <r,u>
         if (ilu) {  // u = ilu.solve(r) ; <r,u>: slot 2 (unused after the exit test)
-          sys->ilu_apply(R, U);
+          sys->ilu_apply(*ilu_f, R, U);
           sys->ew(EW_DOT, 0, 0, {R, U, -1, -1, -1, -1}, 2);
         }
         const auto g = sys->reduce(ilu ? 3 : 2);
@@ -2936,7 +2939,7 @@ class PipeCgSession : public Base {
       case KR_METHOD_CG_GEAR: {  // chronopoulos_gear.py:36-51: one sync per iteration
         sys->ew_n(EW_CGG, alpha, beta, ids({P, U, S, W, X, R, D}), 0);  // <r,r> <r,u>
         if (ilu) {  // u = ilu.solve(r) ; <r,u>: slot 5
-          sys->ilu_apply(R, U);
+          sys->ilu_apply(*ilu_f, R, U);
           sys->ew(EW_DOT, 0, 0, {R, U, -1, -1, -1, -1}, 5);
         }
         sys->spmv(EPI_XY, U, -1, W, -1, -1, -1, 2);              // w = A u ; <u,w>: slot 3
@@ -2952,7 +2955,7 @@ class PipeCgSession : public Base {
       case KR_METHOD_GROPP: {  // gropp.py:30-45
         alpha = gamma / delta;
         if (ilu) {  // q = ilu.solve(s); x += a p; r -= a s ; <r,r>; u -= a q; <r,u>
-          sys->ilu_apply(S, Q);
+          sys->ilu_apply(*ilu_f, S, Q);
           sys->ew(EW_CG, alpha, 0, {X, P, R, S, -1, -1}, 0);
           sys->ew(EW_AXPY, -alpha, 0, {U, Q, -1, -1, -1, -1}, 0);  // u + (-a) q == u - a q
           sys->ew(EW_DOT, 0, 0, {R, U, -1, -1, -1, -1}, 1);
@@ -2973,7 +2976,7 @@ class PipeCgSession : public Base {
       }
       case KR_METHOD_PIPECG: {  // pipeline.py:31-55: one sync per iteration
         if (ilu)
-          sys->ilu_apply(W, M);                                       // m = ilu.solve(w)
+          sys->ilu_apply(*ilu_f, W, M);                                       // m = ilu.solve(w)
         else
           sys->ew_n(EW_DIV, 0, 0, ids({M, W, D}), 0);                 // m = M^-1 w
         sys->spmv(EPI_NONE, M, -1, NN, -1, -1, -1, 0);                // n = A m

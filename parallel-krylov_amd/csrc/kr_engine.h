@@ -270,8 +270,11 @@ struct System {
   std::vector<const double*> precond;
   // ILU instead of the diagonal (one shard): M^-1 v by the two sweeps
   // (ilu_apply; the fused vector kernels then run with d = 1)
-  std::unique_ptr<IluFactors> ilu;
-  void ilu_apply(int in, int out);
+  // shared: a session captures the factors at kr_solve_begin, so a later
+  // kr_solve_set_precond_ilu (or a clear) affects the next solve only, like
+  // the Jacobi diagonal, which the session copies at begin
+  std::shared_ptr<IluFactors> ilu;
+  void ilu_apply(const IluFactors& f, int in, int out);
   // Device-resident scalars (one shard per rank, or every shard in this
   // process): the vector kernel takes c0, c1 from st[coef], st[coef + 1];
   // scalar() runs one scalar_kernel step over the reductions in slots `need`

@@ -49,8 +49,10 @@ class Jacobi:
 
 def _ilu_factors(ilu, N):
     """(L, U, perm_r, perm_c) of a SuperLU object or such a tuple, else None."""
-    if isinstance(ilu, tuple) and len(ilu) == 4:
-        L, U, pr, pc = ilu
+    def _square(m):
+        return getattr(m, "shape", None) is not None and len(m.shape) == 2
+    if isinstance(ilu, tuple) and len(ilu) == 4 and _square(ilu[0]) and _square(ilu[1]):
+        L, U, pr, pc = ilu  # (a 4-tuple of numbers is a diagonal: _diagonal)
     elif all(hasattr(ilu, a) for a in ("L", "U", "perm_r", "perm_c")):
         L, U, pr, pc = ilu.L, ilu.U, ilu.perm_r, ilu.perm_c
     else:

@@ -128,6 +128,9 @@ def test_ilu_argument_forms():
     assert L.shape == U.shape == (200, 200) and np.array_equal(pr, ilu.perm_r)
     assert _ilu_factors((L, U, pr, pc), 200)[0] is L
     assert _ilu_factors(Jacobi(A), 200) is None and _ilu_factors(None, 200) is None
+    # N = 4: a 4-tuple of numbers is a diagonal, not (L, U, perm_r, perm_c)
+    assert _ilu_factors((2.0, 3.0, 4.0, 5.0), 4) is None
+    assert np.array_equal(_diagonal((2.0, 3.0, 4.0, 5.0), 4), [2.0, 3.0, 4.0, 5.0])
     with pytest.raises(ValueError):
         _ilu_factors(ilu, 100)
     with pytest.raises(TypeError, match="ILU factors"):
