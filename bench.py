@@ -67,6 +67,9 @@ def parse():
     p.add_argument("--k", type=int, default=None)
     p.add_argument("--method", default=None)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--rhs", default="normal", choices=["normal", "hash"],
+                   help="b = default_rng(1).standard_normal(N) on the host (SURVEY.md 8(d), "
+                        "default) or the device counter hash 2u-1")
     p.add_argument("--no-csr", action="store_true",
                    help="skip the plain-CSR sub-record (KR_MASK=0 KR_VDICT=0 run)")
     p.add_argument("--cpu-n-side", type=int, default=512,
@@ -93,21 +96,38 @@ def cpu_model():
     return platform.processor() or platform.machine()
 
 
-def cpu_baseline(n_side: int, k: int, method: str, return_info: bool = False, outer: int = 2):
+# CPU-baseline sample per config (C1 runs to convergence,
+# C2-C5 are capped; C5 at a stated reduced N of the same banded family, its
+# rate scaled by the row ratio since SpMV and dots are linear in N).
+CPU_SAMPLE = {
+    "C1": dict(tol=1e-10),                 # the config itself: v3/cpu CG to 1e-10
+    "C2": dict(maxiter=16),                # 16 CG iterations of 256^3
+    "C3": dict(maxiter=12),                # 12 MrR iterations of N = 10M
+    "C4": dict(outer=2),                   # initial step + 2 outer iterations of 512^3
+    "C5": dict(outer=1, n=5_000_000),      # initial step + 1 outer iteration at N = 5M
+}
+
+
+def rhs_host(n: int):
+    """b = default_rng(1).standard_normal(N), on the host."""
+    import numpy as np
+    return np.random.default_rng(1).standard_normal(n)
+
+
+def cpu_baseline(config: str, mat, k: int, method: str, n_side=None, return_info=False):
     """The oracle (numpy/scipy restatement of v3/cpu, bitwise the reference) on
-    the host cores, on a bounded sample: the initial MrR step plus `outer`
-    outer k-skip iterations (1 + outer (k+1) solver iterations, 11 at k = 4)
-    of the same system (512^3 by default; a smaller n_side is scaled to 512^3
-    by the row ratio, since SpMV and dots are linear in N). Timed region = the
-    reference's info['time']. With return_info, also the oracle's (x-free)
-    info dict: its residual history is the full-size parity check of the GPU
-    run (bench `parity`, outer + 2 entries).
+    the host cores, on the bounded sample CPU_SAMPLE[config] of the config's
+    system (same generator, same b = default_rng(1).standard_normal(N), x0 = 0).
+    Timed region = the reference's info['time']; it/s of a reduced sample
+    (--cpu-n-side for Poisson, CPU_SAMPLE's n for C5) is scaled to the
+    config's N by the row ratio. With return_info, also the oracle's (x-free)
+    info dict: when the sample is the config's own system, its residual history
+    is the full-size parity check of the GPU run (bench `parity`).
 
     Threads: scipy's csr_matvec is single-threaded; numpy's dots run on
     OpenBLAS with its default pool, which follows OPENBLAS_NUM_THREADS /
     OMP_NUM_THREADS (the GPU box sets 16: the CPU share of one GPU of the
     node, although the process may be scheduled on more affinity cores)."""
-    import numpy as np
     from oracle import matrices, v3cpu
     try:
         from threadpoolctl import threadpool_info
@@ -115,10 +135,32 @@ def cpu_baseline(n_side: int, k: int, method: str, return_info: bool = False, ou
                             if i.get("user_api") == "blas"] or [1])
     except Exception:  # pragma: no cover
         blas_threads = None
-    A = matrices.poisson(n_side, 3)
-    b = matrices.rhs(A.shape[0], 1)
+    samp = CPU_SAMPLE[config]
+    if mat[0] == "poisson":
+        side = n_side or mat[1]
+        dims = mat[2]
+        A = matrices.poisson(side, dims) if len(mat) == 3 else None
+        if A is None:  # --nz boxes: no CPU sample
+            return (None, None) if return_info else None
+        n_full = mat[1] ** dims
+        desc = f"{side}^{dims} Poisson"
+    else:
+        n_s = samp.get("n", mat[1])
+        A = matrices.banded(n_s, mat[2], mat[3], mat[4])
+        n_full = mat[1]
+        desc = f"banded N={n_s}, {2 * mat[2] + 1} nnz/row, band {mat[3]}"
+    n = A.shape[0]
+    b = rhs_host(n)
     fn = v3cpu.METHODS[method]
-    kw = dict(tol=0.0, maxiter=(outer * (k + 1) + 1) if "kskip" in method else 6)
+    if "tol" in samp:
+        kw = dict(tol=samp["tol"])
+        what = f"to tol {samp['tol']:g}"
+    elif "kskip" in method:
+        kw = dict(tol=0.0, maxiter=samp["outer"] * (k + 1) + 1)
+        what = f"initial step + {samp['outer']} outer"
+    else:
+        kw = dict(tol=0.0, maxiter=samp["maxiter"])
+        what = f"{samp['maxiter']} iterations"
     if "kskip" in method:
         kw["k"] = k
     t0 = time.perf_counter()
@@ -128,19 +170,19 @@ def cpu_baseline(n_side: int, k: int, method: str, return_info: bool = False, ou
     its = int(info["nosl"][-1])
     rate = its / info["time"]
     cores = len(os.sched_getaffinity(0))
-    scale = (n_side ** 3) / (512 ** 3)
-    scaled = "" if n_side == 512 else f", scaled x{scale:.4f} to 512^3"
+    scale = n / n_full
+    scaled = "" if n == n_full else f", scaled x{scale:.4f} to N={n_full}"
     env_threads = {v: os.environ[v] for v in ("OPENBLAS_NUM_THREADS", "OMP_NUM_THREADS")
                    if v in os.environ}
     rec = dict(value=rate * scale, unit="iterations/s",
                cores=blas_threads if blas_threads else cores,
                kind="port",
                cpu_model=cpu_model(), affinity_cores=cores, blas_threads=blas_threads,
-               thread_env=env_threads,
+               thread_env=env_threads, sample_n=n, full_n=n_full,
                sample=(f"oracle.v3cpu.{method} (numpy/scipy restatement of v3/cpu, bitwise "
-                       f"the reference) on {n_side}^3 Poisson, {its} iterations "
-                       f"(initial step + {outer} outer) in "
+                       f"the reference) on {desc}, {its} iterations ({what}) in "
                        f"{info['time']:.2f} s ({rate:.3f} it/s){scaled}; "
+                       f"b = default_rng(1).standard_normal(N); "
                        f"scipy SpMV 1 thread, OpenBLAS dot {blas_threads} threads "
                        f"({', '.join(f'{k_}={v}' for k_, v in env_threads.items()) or 'no thread env'}), "
                        f"{cores} affinity cores, {cpu_model()}; wall {wall:.1f} s; "
@@ -149,25 +191,30 @@ def cpu_baseline(n_side: int, k: int, method: str, return_info: bool = False, ou
                        f"box's CPU share is 16 cores of the node and its harness fixes "
                        f"OMP/OpenBLAS at 16, so the other affinity cores belong to other "
                        f"jobs; scipy's csr_matvec is single-threaded whatever the count"))
-    return (rec, info) if return_info else rec
+    full = n == n_full
+    return (rec, info if full else None) if return_info else rec
 
 
-# SURVEY.md 8(c) contract for k-skip MrR (k <= 4): nosl identical, residual
-# entries >= 1e-8 within 1e-12 relative.
+# SURVEY.md 8(c) contract for CG, MrR and k-skip MrR (k <= 4): nosl
+# identical, residual entries >= 1e-8 within 1e-12 relative.
 PARITY_RTOL = 1e-12
 
 
-def history_parity(gpu_info, ref_info, rtol=PARITY_RTOL):
+def history_parity(gpu_info, ref_info, rtol=PARITY_RTOL, overlap=False):
     """Full-size parity: the GPU run's first history entries against the
     oracle's run of the SAME system (same b, x0 = 0) in the cpu_baseline leg.
     The oracle stops at maxiter (its last entry is the exit branch's
     recomputed norm of the same r), so entries are compared by index. A GPU
     history shorter than the oracle's is a parity failure (ok false, both
-    lengths recorded), never an exception."""
+    lengths recorded), never an exception -- unless `overlap` (C1: the oracle
+    runs to convergence, the timed GPU run a fixed count), where the common
+    prefix is compared."""
     import numpy as np
-    m = len(ref_info["residual"])
     g_all = np.asarray(gpu_info["residual"], dtype=np.float64)
-    r_res = np.asarray(ref_info["residual"], dtype=np.float64)
+    r_all = np.asarray(ref_info["residual"], dtype=np.float64)
+    m = min(len(r_all), len(g_all)) if overlap else len(r_all)
+    r_res = r_all[:m]
+    ref_info = dict(ref_info, nosl=np.asarray(ref_info["nosl"])[:m])
     c = min(m, len(g_all))
     g_res = g_all[:c]
     nosl_eq = bool(len(gpu_info["nosl"]) >= m and
@@ -176,10 +223,11 @@ def history_parity(gpu_info, ref_info, rtol=PARITY_RTOL):
     rel = np.abs(g_res - r_res[:c]) / np.abs(r_res[:c])
     max_rel = float(rel[big].max()) if big.any() else 0.0
     ok = nosl_eq and c == m and max_rel <= rtol
-    return dict(ok=bool(ok), entries=int(c), oracle_entries=int(m), nosl_equal=nosl_eq,
+    return dict(ok=bool(ok), entries=int(c), oracle_entries=int(len(r_all)), nosl_equal=nosl_eq,
                 max_rel=max_rel, rtol=rtol,
                 reference="oracle.v3cpu (bitwise the reference's v3/cpu), same b, x0 = 0",
-                gpu=[float(v) for v in g_res], oracle=[float(v) for v in r_res])
+                shown=min(c, 12), gpu=[float(v) for v in g_res[:12]],
+                oracle=[float(v) for v in r_res[:12]])
 
 
 def stored_format_delta(nnz, n, lay, long_row=12.0):
@@ -269,7 +317,9 @@ def run_system(args, cfg, mat, n, world, rank, local, comm, method, k, env=None)
     info = sysm.shard_info(0)
     lay = sysm.shard_layout(0)
     lay["stencil_walk"] = sysm.shard_sched(0)["stencil_walk"]
-    b = sysm.rhs(1)
+    # b = default_rng(1).standard_normal(N), the global
+    # vector's own rows per shard; --rhs hash: the device counter hash (2u-1)
+    b = sysm.split(rhs_host(n)) if args.rhs == "normal" else sysm.rhs(1)
     per_step = (k + 1) if "kskip" in method else 1
     maxiter = (args.warmup + args.steps + 4) * per_step + 2
     # per-kernel HIP events on every 4th step (each event pair costs ~10 us of
@@ -302,6 +352,18 @@ def run_system(args, cfg, mat, n, world, rank, local, comm, method, k, env=None)
     torch.cuda.empty_cache()
     return dict(info=info, lay=lay, per_step=per_step, elapsed=elapsed, stats=stats,
                 history=out.info)
+
+
+def parallelism(world: int, local_shards: int) -> str:
+    """What the run actually exchanges: one shard on one GPU moves nothing."""
+    if world == 1 and local_shards <= 1:
+        return "1 GPU, one shard (no halo exchange, no collective)"
+    if world == 1:
+        return (f"1 GPU, {local_shards} in-process shards (halo device copies, shard "
+                f"partials summed in shard order)")
+    return (f"row-partitioned x{world} ranks (one GPU each), RCCL halo send/recv + Gram "
+            f"all-gather" + (f"; {local_shards} in-process shards per rank"
+                             if local_shards > 1 else ""))
 
 
 METHOD_NAMES = {"cg": "CG", "mrr": "MrR", "kskipcg": "k-skip CG", "kskipmrr": "k-skip MrR",
@@ -471,10 +533,12 @@ def main():
 
     base = None
     parity = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "C4":
-        base, ref_info = cpu_baseline(args.cpu_n_side, k, method, return_info=True)
-        if args.cpu_n_side == mat[1] and args.nz is None and mat[0] == "poisson":
-            parity = history_parity(run["history"], ref_info)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.local_shards == 1:
+        n_side = args.cpu_n_side if args.config == "C4" else None
+        base, ref_info = cpu_baseline(args.config, mat, k, method, n_side=n_side,
+                                      return_info=True)
+        if ref_info is not None and args.rhs == "normal":
+            parity = history_parity(run["history"], ref_info, overlap=args.config == "C1")
     if rank == 0:
         rec = {
             "metric": (HEADLINE_METRIC if args.config == "C4" and method == cfg["method"]
@@ -490,14 +554,14 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (CSR matrix and b = 2u-1 generated on device)",
+            "data": ("synthetic: CSR matrix generated on device; b = "
+                     + ("default_rng(1).standard_normal(N) (host, SURVEY.md 8(d))"
+                        if args.rhs == "normal" else "2u-1 counter hash (device)")),
             "config": {"workload": workload_label(args.config, method, k, mat, n)
                                    + f", nnz/shard={info['nnz']}, tol=0 fixed iterations",
                        "method": method, "k": k, "matrix": mat,
                        "step": f"one outer iteration = {per_step} solver iterations",
-                       "parallelism": f"row-partitioned x{world}, RCCL halo + Gram all-gather"
-                       + (f"; {args.local_shards} in-process shards per rank on its GPU"
-                          if args.local_shards > 1 else "")},
+                       "parallelism": parallelism(world, args.local_shards)},
             "roofline": roofline,
             "cpu_baseline": base,
             "parity": parity,

@@ -21,7 +21,7 @@ def test_headline_metric_is_baselines():
 
 def test_cpu_baseline_object_small_sample():
     import bench
-    rec = bench.cpu_baseline(12, 4, "kskipmrr")
+    rec = bench.cpu_baseline("C4", ["poisson", 512, 3], 4, "kskipmrr", n_side=12)
     assert set(rec) >= {"value", "unit", "cores", "kind", "sample", "cpu_model",
                         "affinity_cores", "blas_threads"}
     assert rec["kind"] == "port" and rec["unit"] == "iterations/s"
@@ -29,6 +29,35 @@ def test_cpu_baseline_object_small_sample():
     assert "2 outer" in rec["sample"]  # initial step + 2 outer iterations
     assert rec["value"] > 0 and rec["cores"] >= 1
     assert "scaled" in rec["sample"]  # a 12^3 sample is scaled to 512^3 by rows
+    assert "standard_normal" in rec["sample"]
+
+
+def test_cpu_baseline_every_config(monkeypatch):
+    """Every config line carries a cpu_baseline: C1 is the v3/cpu CG run to
+    1e-10 on its own system (the config BASELINE.json defines as v3/cpu) and
+    returns the oracle history for the bench's parity field; banded configs
+    sample the same generator at a stated N, scaled by the row ratio."""
+    import numpy as np
+    import bench
+    from oracle import matrices, v3cpu
+    rec, info = bench.cpu_baseline("C1", ["poisson", 256, 2], 0, "cg", return_info=True)
+    assert rec["sample_n"] == rec["full_n"] == 65536 and "to tol 1e-10" in rec["sample"]
+    assert info["residual"][-1] < 1e-10 and rec["value"] > 0
+    A = matrices.poisson(256, 2)
+    _, ref = v3cpu.cg(A, np.random.default_rng(1).standard_normal(A.shape[0]), tol=1e-10)
+    np.testing.assert_array_equal(info["residual"], ref["residual"])
+    monkeypatch.setitem(bench.CPU_SAMPLE, "C5", dict(outer=1, n=3000))
+    rec, info = bench.cpu_baseline("C5", ["banded", 50_000_000, 31, 256, 0], 4,
+                                   "adaptivekskipmrr", return_info=True)
+    assert info is None  # a reduced sample is no parity reference
+    assert rec["sample_n"] == 3000 and "scaled" in rec["sample"] and "1 outer" in rec["sample"]
+
+
+def test_parallelism_is_truthful():
+    import bench
+    assert "no halo exchange" in bench.parallelism(1, 1)
+    assert "in-process" in bench.parallelism(1, 8) and "RCCL" not in bench.parallelism(1, 8)
+    assert "RCCL" in bench.parallelism(8, 1)
 
 
 def test_pmc_traffic_from_committed_profile():
@@ -62,6 +91,10 @@ def test_history_parity_contract():
     short = {"nosl": np.array([0, 1]), "residual": np.array([1.0, 0.5])}
     p = bench.history_parity(short, ref)
     assert not p["ok"] and p["entries"] == 2 and p["oracle_entries"] == 3
+    # C1: the oracle ran to convergence, the timed GPU run a fixed count --
+    # the common prefix is the comparison
+    p = bench.history_parity(short, ref, overlap=True)
+    assert p["ok"] and p["entries"] == 2 and p["oracle_entries"] == 3
 
 
 def test_stored_format_bytes():

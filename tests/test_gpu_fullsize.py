@@ -89,7 +89,7 @@ def _c4_history(parts, maxiter, k=4):
     try:
         sysm.gen_poisson(512, 3)
         sysm.finalize()
-        b = sysm.rhs(1)
+        b = sysm.split(np.random.default_rng(1).standard_normal(n))  # the bench's b
         out = sysm.solve("kskipmrr", b, tol=0.0, maxiter=maxiter, k=k)
         del b
     finally:
@@ -119,7 +119,7 @@ def test_c4_fullsize_partitions_match_oracle():
     assert np.all(r1 >= 1e-8)
     rel = np.abs(r8 - r1) / r1
     assert rel.max() <= 1e-12, rel
-    _, ref = bench.cpu_baseline(512, k, "kskipmrr", return_info=True, outer=2)
+    _, ref = bench.cpu_baseline("C4", ["poisson", 512, 3], k, "kskipmrr", return_info=True)
     assert list(ref["nosl"]) == [0, 1, 6, 11]
     for h in (h1, h8):
         p = bench.history_parity(h, ref)
