@@ -77,6 +77,43 @@ def test_c5_fullsize_true_residual():
     sysm.close()
 
 
+@pytest.mark.timeout(900)
+def test_c5_fullsize_partition_8_shards_match_1():
+    """C5 in its own 8-way partition (BASELINE.json configs[4]: N = 50M,
+    63 nnz/row, 8 GPUs): adaptive k-skip MrR k=4 for 3 outer iterations as 8
+    in-process shards of one device (6.25M rows each, a 256-row halo per
+    neighbour, the symmetric DIA walk per shard, shard partials summed in
+    shard order -- the 8-GPU layout) and as one shard: nosl and khistory
+    identical, every entry within 1e-12 relative (only the dot summation
+    order differs). Rollbacks at scale are covered by the N = 200k C5-family
+    case on 8 shards in test_gpu_order.py (bitwise the GPU-order oracle)."""
+    import torch
+    from parallel_krylov_amd.system import KrylovSystem, balanced_partition
+    n = 50_000_000
+    bh = np.random.default_rng(1).standard_normal(n)
+    hist = {}
+    for parts in (1, 8):
+        sysm = KrylovSystem(n, balanced_partition(n, parts), [0] * parts)
+        try:
+            sysm.gen_banded(31, 256, 0)
+            sysm.finalize()
+            if parts == 8:
+                assert all(sysm.shard_sched(s)["dia_walk"] for s in range(8))
+            b = sysm.split(bh)
+            hist[parts] = sysm.solve("adaptivekskipmrr", b, tol=0.0, maxiter=12, k=4).info
+            del b
+        finally:
+            sysm.close()
+            torch.cuda.empty_cache()
+    h1, h8 = hist[1], hist[8]
+    assert list(h1["nosl"]) == [0, 1, 6, 11, 16] and list(h8["nosl"]) == list(h1["nosl"])
+    assert list(h8["khistory"]) == list(h1["khistory"])
+    r1, r8 = np.asarray(h1["residual"]), np.asarray(h8["residual"])
+    assert np.all(r1 >= 1e-8) and r1[-1] < r1[0]
+    rel = np.abs(r8 - r1) / r1
+    assert rel.max() <= 1e-12, rel
+
+
 def _c4_history(parts, maxiter, k=4):
     """k-skip MrR k=4 on the 512^3 headline system as `parts` in-process
     shards of one device (parts = 8: C4's own row partition, one 64-plane
