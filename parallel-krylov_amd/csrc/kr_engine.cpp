@@ -15,6 +15,7 @@
 #include <cstring>
 #include <exception>
 #include <mutex>
+#include <numeric>
 #include <thread>
 
 namespace kr {
@@ -471,29 +472,36 @@ std::unique_ptr<IluFactors> build_ilu(int dev, hipStream_t stream, int64_t n, co
 
 bool stencil_pm(int P);
 
-bool System::pair_ok() const {
-  if (shards.size() != 1 || comm || nglobal_shards() != 1) return false;
-  // opt-in (KR_ST2=1): measured slower than two dual launches
-  const char* env = getenv("KR_ST2");
-  if (!(env && atoi(env) != 0)) return false;
+int System::pair_mode() const {
+  if (shards.size() != 1 || comm || nglobal_shards() != 1) return 0;
+  const char* env = getenv("KR_ST2");  // 0 / unset: two dual launches; 1, 2: the pairs (A/B)
+  const int mode = env ? atoi(env) : 0;
+  if (mode != 1 && mode != 2) return 0;
   const Shard& s = shards[0];
-  if (!s.scode || !stencil_pm(s.st_P) || s.nm != 7 || s.st_nfar != 2) return false;
-  if (s.st_far[0] != -kStencilBlock || s.st_far[1] != kStencilBlock) return false;
-  if (s.st_cb != 2 && s.st_cb != 4) return false;
+  if (!s.scode || !stencil_pm(s.st_P) || s.nm != 7 || s.st_nfar != 2) return 0;
+  if (s.st_far[0] != -kStencilBlock || s.st_far[1] != kStencilBlock) return 0;
+  if (s.st_cb != 2 && s.st_cb != 4) return 0;
   const int64_t W = (int64_t)s.st_P * kStencilBlock;
   static const int kPat[7] = {1, 4, 3, 0, 3, 5, 2};  // kPat7: PREV FAR0 NEAR CENTER NEAR FAR1 NEXT
   for (int k = 0; k < 7; ++k)
-    if (s.st_kind[k] != kPat[k]) return false;
-  return s.n % W == 0 && s.n / W >= 2 && s.spmv_grid2 % s.st_P == 0;
+    if (s.st_kind[k] != kPat[k]) return 0;
+  if (s.n % W != 0 || s.n / W < 2) return 0;
+  if (mode == 1) return s.spmv_grid2 % s.st_P == 0 ? 1 : 0;
+  // the tiled pair writes the partials of both dual grids (general and
+  // products-only, position-major: P x segments)
+  return s.st_P % 16 == 0 && s.spmv_grid % s.st_P == 0 && s.spmv_grid_po % s.st_P == 0 ? 2 : 0;
 }
 
-void System::spmv_pair(int in1, int in2, int out1, int out2, int slot0) {
-  KR_REQUIRE(pair_ok(), "fused basis pair: shard not eligible");
+void System::spmv_pair(int in1, int in2, int out1, int out2, int slot0, SpmvEpi epi) {
+  const int mode = pair_mode();
+  KR_REQUIRE(mode != 0, "fused basis pair: shard not eligible");
+  KR_REQUIRE(mode == 2 || epi == EPI_DUAL_MRR, "fused basis pair (KR_ST2=1): k-skip MrR only");
   KR_REQUIRE(slot0 + 14 <= kMaxSlots, "reduction slots exhausted");
   Shard& s = shards[0];
   KR_HIP_CHECK(hipSetDevice(s.dev));
   const bool po = products_only && products_only_on;
-  const char* nm = po ? "spmv2x2_gram_mrr_last" : "spmv2x2_gram_mrr";
+  const char* nm = epi == EPI_DUAL_KCG ? (po ? "spmv2x2_gram_kcg_last" : "spmv2x2_gram_kcg")
+                                       : (po ? "spmv2x2_gram_mrr_last" : "spmv2x2_gram_mrr");
   hipEvent_t t0 = nullptr;
   prof_begin(s, nm, t0);
   SpmvArgs a;
@@ -523,8 +531,29 @@ void System::spmv_pair(int in1, int in2, int out1, int out2, int slot0) {
   a.scratch = s.scratch;
   a.products_only = po ? 1 : 0;
   a.stop = dev_stop ? s.st + ST_STOP : nullptr;
-  launch_spmv_stencil2(a, s.spmv_grid2, s.stream);
-  for (int p = 0; p < 14; ++p) s.slot_n[slot0 + p] = s.spmv_grid2;
+  if (mode == 1) {
+    launch_spmv_stencil2(a, s.spmv_grid2, s.stream);
+    for (int p = 0; p < 14; ++p) s.slot_n[slot0 + p] = s.spmv_grid2;
+  } else {
+    // level 1 = dual m on the general grid, level 2 = dual m+1 on the grid
+    // its launch would use (the products-only one for the last pair); the
+    // walk segments divide both: the largest such count <= KR_ST2T_Z
+    const int g1 = s.spmv_grid, g2 = po ? s.spmv_grid_po : s.spmv_grid;
+    const int z1 = g1 / s.st_P, z2 = g2 / s.st_P;
+    const char* ze = getenv("KR_ST2T_Z");
+    const int zcap = ze && atoi(ze) > 0 ? atoi(ze) : 16;
+    const int zg = std::gcd(z1, z2);
+    int zw = 1;
+    for (int d = 1; d <= zg; ++d)
+      if (zg % d == 0 && d <= zcap) zw = d;
+    a.st2_z1 = z1;
+    a.st2_z2 = z2;
+    launch_spmv_stencil2t(epi, a, (s.st_P / 2) * zw, s.stream);
+    for (int p = 0; p < 7; ++p) {
+      s.slot_n[slot0 + p] = g1;
+      s.slot_n[slot0 + 7 + p] = g2;
+    }
+  }
   // algorithmic bytes in CSR terms, like every SpMV's (bench.py subtracts the
   // stored format's saving): A once, the two input vectors and the two
   // level-2 outputs (none products-only) -- one dual SpMV's; level 1 never
@@ -2776,10 +2805,21 @@ class KskipCgSession : public Base {
       set_entry(index, rel(sys->reduce(kHead)[0]));
       return done = true;
     }
-    for (int j = 1; j <= k; ++j) {
+    // the tiled fused pair (KR_ST2=2) chains two duals per launch where the
+    // shard allows; an odd count ends with a single dual
+    const bool pairs = sys->pair_mode() == 2;
+    for (int j = 1; j <= k;) {
+      if (pairs && j + 1 <= k) {
+        sys->products_only = j + 1 == k;  // Ar[k], Ap[k+1] feed only the Gram products
+        sys->spmv_pair(AR(j - 1), AP(j), AR(j + 1), AP(j + 2), kHead + 7 * (j - 1), EPI_DUAL_KCG);
+        sys->products_only = false;
+        j += 2;
+        continue;
+      }
       sys->products_only = j == k;  // Ar[k], Ap[k+1] feed only the Gram products
       sys->spmv(EPI_DUAL_KCG, AR(j - 1), AP(j), AR(j), AP(j + 1), -1, -1, kHead + 7 * (j - 1));
       sys->products_only = false;
+      ++j;
     }
     const std::vector<double> g = sys->reduce(gram_slots());
     set_entry(index, rel(g[0]));

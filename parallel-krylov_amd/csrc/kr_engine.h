@@ -256,11 +256,15 @@ struct System {
   // Two chained EPI_DUAL_MRR basis SpMVs in one launch (spmv_stencil2_kernel):
   // (in1, in2) -> level 2 in (out1, out2) (not stored under products_only),
   // products of the first dual at slot0, of the second at slot0 + 7.
-  // pair_ok(): one shard, no communicator, a 7-point stencil shard with n =
-  // 512 and whole planes, narrow codes, and KR_ST2=1 (opt-in: slower than
-  // the two dual launches on MI355X).
-  bool pair_ok() const;
-  void spmv_pair(int in1, int in2, int out1, int out2, int slot0);
+  // pair_mode(): which fused basis pair serves the shard (0: none, two dual
+  // launches). One shard, no communicator, a 7-point stencil shard with n =
+  // 512 and whole planes, narrow codes; KR_ST2=1: one position per workgroup
+  // (spmv_stencil2_kernel, measured slower than two duals),
+  // KR_ST2=2: two positions per workgroup (spmv_stencil2t_kernel, P % 16 == 0;
+  // bitwise the dual launches, products included).
+  int pair_mode() const;
+  bool pair_ok() const { return pair_mode() != 0; }
+  void spmv_pair(int in1, int in2, int out1, int out2, int slot0, SpmvEpi epi = EPI_DUAL_MRR);
   void ew(EwOp op, double c0, double c1, std::array<int, 6> ids, int slot0);
   // The same for ops with more than 6 operands (-1: unused slot).
   void ew_n(EwOp op, double c0, double c1, const std::array<int, kEwOps>& ids, int slot0);

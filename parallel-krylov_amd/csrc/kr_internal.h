@@ -218,6 +218,10 @@ struct SpmvArgs {
   // first. The engine alternates it per launch with KR_ZIGZAG=1 (A/B): the
   // next kernel starts on the planes the previous one touched last.
   int st_rev = 0;
+  // The tiled fused basis pair (spmv_stencil2t_kernel): plane segments of the
+  // two dual grids whose partials it writes (level 1 = dual m, level 2 = dual
+  // m+1: general grid, or the products-only grid), the walk runs on their gcd
+  int st2_z1 = 0, st2_z2 = 0;
   int32_t st_off[8] = {};
   int32_t st_kind[8] = {};
   int32_t st_far[4] = {};
@@ -259,6 +263,12 @@ void launch_spmv_grid(SpmvEpi epi, const SpmvArgs& a, int nblocks, hipStream_t s
 // Ay[m+2]) (not stored when products_only), EPI_DUAL_MRR products of dual m
 // at partials, of dual m+1 at partials2. 7-point stencil shards with n = 512.
 void launch_spmv_stencil2(const SpmvArgs& a, int nblocks, hipStream_t s);
+// The tiled pair (spmv_stencil2t_kernel): two adjacent positions per
+// 512-thread workgroup, bitwise the two dual launches (products included);
+// EPI_DUAL_MRR or EPI_DUAL_KCG products; nblocks = P/2 x gcd(st2_z1, st2_z2).
+void launch_spmv_stencil2t(SpmvEpi epi, const SpmvArgs& a, int nblocks, hipStream_t s);
+void launch_spmv_stencil2t_mrr(const SpmvArgs& a, int nblocks, hipStream_t s);
+void launch_spmv_stencil2t_kcg(const SpmvArgs& a, int nblocks, hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // Elementwise vector steps with fused reductions (all own-row pointers).

@@ -916,6 +916,14 @@ int spmv_products(SpmvEpi epi) {
   return 0;
 }
 
+void launch_spmv_stencil2t(SpmvEpi epi, const SpmvArgs& a, int nblocks, hipStream_t s) {
+  KR_REQUIRE(epi == EPI_DUAL_MRR || epi == EPI_DUAL_KCG, "tiled pair: dual epilogues only");
+  if (epi == EPI_DUAL_MRR)
+    launch_spmv_stencil2t_mrr(a, nblocks, s);
+  else
+    launch_spmv_stencil2t_kcg(a, nblocks, s);
+}
+
 void launch_spmv(SpmvEpi epi, const SpmvArgs& a, hipStream_t s) {
   launch_spmv_grid(epi, a, a.grid, s);
 }

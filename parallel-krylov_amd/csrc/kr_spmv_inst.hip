@@ -14,4 +14,15 @@ void launch_spmv_stencil2(const SpmvArgs& a, int nblocks, hipStream_t s) {
   spmv_stencil2_launch(a, nblocks, s);
 }
 #endif
+#if KR_EPI == 7
+void launch_spmv_stencil2t_mrr(const SpmvArgs& a, int nblocks, hipStream_t s) {
+  spmv_stencil2t_launch<EPI_DUAL_MRR>(a, nblocks, s);
+}
+#endif
+#if KR_EPI == 8
+static_assert(EPI_DUAL_KCG == 8, "the tiled pair's k-skip CG products are built in EPI_DUAL_KCG's unit");
+void launch_spmv_stencil2t_kcg(const SpmvArgs& a, int nblocks, hipStream_t s) {
+  spmv_stencil2t_launch<EPI_DUAL_KCG>(a, nblocks, s);
+}
+#endif
 }  // namespace kr

@@ -1145,3 +1145,317 @@ inline void spmv_stencil2_launch(const SpmvArgs& a, int nblocks, hipStream_t s) 
   else
     po ? st2_launch_t<4, true>(a, nblocks, s) : st2_launch_t<4, false>(a, nblocks, s);
 }
+
+// ---------------------------------------------------------------------------
+// Tiled fused basis pair (spmv_stencil2t_kernel; KR_ST2=2). The pair above
+// walks ONE position and must rebuild level 1 on three blocks and load level
+// 0 on five for it (3x the level-1 work, 2 waves per SIMD): slower than the
+// two dual launches it replaces. Here a 512-thread workgroup walks TWO
+// adjacent positions p0, p0 + 1 (p0 even) of a plane segment, one 256-lane
+// group per position (group H owns position p0 + H, lane t its rows 2t and
+// 2t + 1, as in the dual kernel):
+//
+//   level 0 (loaded)  : positions p0-2 .. p0+3, three per group
+//   level 1 (computed): positions p0-1 .. p0+2, two per group (one redundant)
+//   level 2 (stored)  : positions p0, p0+1, one per group
+//
+// so the redundant work is one level-1 line per output line, and each group
+// reads three level-0 lines per plane for two levels (the dual reads three
+// per level). Level 0 goes to LDS as it arrives (all six lines: the +-1 and
+// +-n operands of level 1) and the next plane's loads reuse its registers
+// at once, so a whole plane step hides them; level 1 of p0 and p0 + 1 goes
+// to LDS for level 2 (+-1, and +-n across the groups). Two barriers per plane.
+//
+// Bitwise the two dual launches, products included: every row is summed in
+// stored order from 0.0 (-W ... +n when its plane arrives, +W one plane
+// later), and group H accumulates the products of dual m (level 0 x level 1)
+// and of dual m+1 (level 1 x level 2) of its position plane by plane, row 2t
+// then 2t+1, exactly as the dual launch's workgroup of that (position,
+// segment) does. The walk segment is a union of segments of both dual grids
+// (the level-2 grid is the products-only one for the last pair); at each
+// grid's segment boundary the group's accumulator is reduced into that grid's
+// partial of the virtual workgroup, so the partials are the dual launches'.
+// ---------------------------------------------------------------------------
+struct St2tLds {
+  double x0[2][6 * kSBlock];           // level 0 of positions p0-2 .. p0+3 [chain][line*512 + row]
+  double x1[2][2 * kSBlock + 4];       // level 1 of p0, p0+1 [chain][2 + line*512 + row], margins
+};
+
+template <int CB>
+struct St2tStage {
+  dbl2v x[2][3];            // level 0 of the group's three lines [chain][line]
+  uint32_t clo[2], chi[2];  // codes of the two level-1 lines (rows 2t, 2t+1)
+};
+
+template <int EPI, int CB, bool PO, int H>
+__device__ __forceinline__ void st2t_walk(const SpmvArgs& a, St2tLds& L, const double* s_tab,
+                                          double* s_red1, double* s_red2, int tid, int64_t p0,
+                                          int64_t q, int64_t zs, int64_t Zw) {
+  constexpr int NP = 7;
+  constexpr int IO = H == 0 ? 1 : 0;  // owned line among the group's level-1 lines
+  const int64_t P = a.st_P, W = P * kSBlock, PP = P >> 3;
+  const int64_t planes = a.n / W;
+  const int64_t z0 = planes * zs / Zw, z1 = planes * (zs + 1) / Zw;
+  const int64_t pown = p0 + H;
+  const double* const xs[3] = {a.x1, a.x2, a.x2};
+  const SRes res = st_res<2, CB>(a, xs);
+  const uint32_t lb = (uint32_t)tid * 16u;
+  // first row of level-0 line l (0..5: positions p0-2 .. p0+3) at plane z
+  auto row_of = [&](int64_t z, int l) { return z * W + (p0 - 2 + l) * kSBlock; };
+  auto ld = [&](int c, int64_t row) {
+    return st_bld2(res.x[c], (uint32_t)((a.xoff + row) * 8) + lb);
+  };
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  auto issue = [&](St2tStage<CB>& st, int64_t z) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) st.x[c][j] = ld(c, row_of(z, 3 * H + j));
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t r = row_of(z, 1 + 2 * H + i);
+      if constexpr (CB == 2) {
+        const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(
+            res.code, (uint32_t)(r * 2) + (uint32_t)tid * 4u, 0, 2);
+        st.clo[i] = v & 0xFFFFu;
+        st.chi[i] = v >> 16;
+      } else {
+        const u32x2 v = __builtin_bit_cast(
+            u32x2, __builtin_amdgcn_raw_buffer_load_b64(res.code, (uint32_t)(r * 4) + (uint32_t)tid * 8u,
+                                                        0, 2));
+        st.clo[i] = v.x;
+        st.chi[i] = v.y;
+      }
+    }
+  };
+  // products: virtual workgroup of (position, segment) in a dual grid, and
+  // the segment boundaries (walk segment zs of Zw starts segment zs Z / Zw)
+  auto vblock = [&](int64_t seg) { return 8 * (seg * PP + (pown - q * PP)) + q; };
+  const int64_t Z1 = a.st2_z1, Z2 = a.st2_z2;
+  int64_t seg1 = zs * (Z1 / Zw), seg2 = zs * (Z2 / Zw);
+  int64_t nb1 = planes * (seg1 + 1) / Z1, nb2 = planes * (seg2 + 1) / Z2;
+  double acc1[NP], acc2[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) acc1[k] = acc2[k] = 0.0;
+  auto flush = [&](double (&acc)[NP], double* part, double* s_red, int64_t seg) {
+    block_reduce_store<NP>(acc, part, a.grid, s_red, 0, tid, vblock(seg));
+#pragma unroll
+    for (int k = 0; k < NP; ++k) acc[k] = 0.0;
+  };
+
+  // ---- state carried along the walk (step s: level 0 of plane s arrives)
+  dbl2v l0p[2][2];            // level 0 of plane s-1 at the level-1 lines
+  dbl2v p1[2][2];             // partial level-1 sums of plane s-1 (slots -W .. +n)
+  uint32_t c1lo[2] = {0u, 0u}, c1hi[2] = {0u, 0u};  // their codes
+  dbl2v l1p[2];               // level 1 of plane s-2, own line
+  dbl2v p2[2];                // partial level-2 sums of plane s-2
+  uint32_t c2lo = 0u, c2hi = 0u;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    l1p[c] = p2[c] = dbl2v{0.0, 0.0};
+#pragma unroll
+    for (int i = 0; i < 2; ++i) p1[c][i] = dbl2v{0.0, 0.0};
+  }
+  const int64_t zlast = z1 + 1;
+  St2tStage<CB> st;
+  auto step = [&](int64_t s) {
+    // (1) level 0 of plane s to LDS; the next plane's loads take its registers
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        reinterpret_cast<dbl2v*>(L.x0[c] + (3 * H + j) * kSBlock)[tid] = st.x[c][j];
+    uint32_t clo[2], chi[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      clo[i] = st.clo[i];
+      chi[i] = st.chi[i];
+    }
+    issue(st, s + 1 <= zlast ? s + 1 : s);  // (the last step re-reads its own plane)
+    __syncthreads();
+    // (2) level 1: plane s-1 completed by +W, plane s started
+    dbl2v l1[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int li = 1 + 2 * H + i;  // level-0 line of this level-1 line
+      dbl2v cx[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) cx[c] = reinterpret_cast<const dbl2v*>(L.x0[c] + li * kSBlock)[tid];
+      {
+        double xl[2][7], xh[2][7], sl[2], sh[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          xl[c][6] = cx[c].x;
+          xh[c][6] = cx[c].y;
+          sl[c] = p1[c][i].x;
+          sh[c] = p1[c][i].y;
+        }
+        st2_terms<CB, 6, 7>(c1lo[i], c1hi[i], s_tab, xl, xh, sl, sh);
+#pragma unroll
+        for (int c = 0; c < 2; ++c) l1[c][i] = dbl2v{sl[c], sh[c]};
+      }
+      double xl[2][7], xh[2][7], sl[2] = {0.0, 0.0}, sh[2] = {0.0, 0.0};
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const double* line = L.x0[c] + li * kSBlock + 2 * tid;
+        const dbl2v mn = *reinterpret_cast<const dbl2v*>(line - kSBlock);
+        const dbl2v pn = *reinterpret_cast<const dbl2v*>(line + kSBlock);
+        xl[c][0] = l0p[c][i].x;  xh[c][0] = l0p[c][i].y;
+        xl[c][1] = mn.x;         xh[c][1] = mn.y;
+        xl[c][2] = line[-1];     xh[c][2] = cx[c].x;
+        xl[c][3] = cx[c].x;      xh[c][3] = cx[c].y;
+        xl[c][4] = cx[c].y;      xh[c][4] = line[2];
+        xl[c][5] = pn.x;         xh[c][5] = pn.y;
+      }
+      st2_terms<CB, 0, 6>(clo[i], chi[i], s_tab, xl, xh, sl, sh);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) p1[c][i] = dbl2v{sl[c], sh[c]};
+      // (3) dual m's products at plane s-1 (level 0 x level 1, own line)
+      if (i == IO) {
+        const int64_t zp1 = s - 1;
+        if (zp1 >= z0 && zp1 < z1) {
+          if (zp1 >= nb1) {
+            flush(acc1, a.partials, s_red1, seg1);
+            ++seg1;
+            nb1 = planes * (seg1 + 1) / Z1;
+          }
+          epi_products<EPI>(l0p[0][IO].x, l0p[1][IO].x, l1[0][IO].x, l1[1][IO].x, 0.0, acc1);
+          epi_products<EPI>(l0p[0][IO].y, l0p[1][IO].y, l1[0][IO].y, l1[1][IO].y, 0.0, acc1);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 2; ++c) l0p[c][i] = cx[c];
+    }
+    // (4) level 1 of plane s-1, own line (+ the outer margin) for level 2
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      reinterpret_cast<dbl2v*>(L.x1[c] + 2 + H * kSBlock)[tid] = l1[c][IO];
+      if (H == 0 && tid == kBlock - 1) L.x1[c][1] = l1[c][0].y;             // p0-1, row 511
+      if (H == 1 && tid == 0) L.x1[c][2 + 2 * kSBlock] = l1[c][1].x;        // p0+2, row 0
+    }
+    __syncthreads();
+    // (5) level 2: plane s-2 completed by +W (level 1 of plane s-1), plane s-1 started
+    {
+      double xl[2][7], xh[2][7], sl[2], sh[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        xl[c][6] = l1[c][IO].x;
+        xh[c][6] = l1[c][IO].y;
+        sl[c] = p2[c].x;
+        sh[c] = p2[c].y;
+      }
+      st2_terms<CB, 6, 7>(c2lo, c2hi, s_tab, xl, xh, sl, sh);
+      const int64_t zp2 = s - 2;
+      if (zp2 >= z0 && zp2 < z1) {
+        if (zp2 >= nb2) {
+          flush(acc2, a.partials2, s_red2, seg2);
+          ++seg2;
+          nb2 = planes * (seg2 + 1) / Z2;
+        }
+        epi_products<EPI>(l1p[0].x, l1p[1].x, sl[0], sl[1], 0.0, acc2);
+        epi_products<EPI>(l1p[0].y, l1p[1].y, sh[0], sh[1], 0.0, acc2);
+        if constexpr (!PO) {
+          const int64_t row = zp2 * W + pown * kSBlock + 2 * tid;
+          __builtin_nontemporal_store(dbl2v{sl[0], sh[0]}, reinterpret_cast<dbl2v*>(a.y1 + row));
+          __builtin_nontemporal_store(dbl2v{sl[1], sh[1]}, reinterpret_cast<dbl2v*>(a.y2 + row));
+        }
+      }
+    }
+    {
+      double xl[2][7], xh[2][7], sl[2] = {0.0, 0.0}, sh[2] = {0.0, 0.0};
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const double* lx = L.x1[c] + 2 + H * kSBlock + 2 * tid;
+        const dbl2v cx = l1[c][IO];
+        const dbl2v mn = H == 0 ? l1[c][0] : *reinterpret_cast<const dbl2v*>(lx - kSBlock);
+        const dbl2v pn = H == 0 ? *reinterpret_cast<const dbl2v*>(lx + kSBlock) : l1[c][1];
+        xl[c][0] = l1p[c].x;  xh[c][0] = l1p[c].y;
+        xl[c][1] = mn.x;      xh[c][1] = mn.y;
+        xl[c][2] = lx[-1];    xh[c][2] = cx.x;
+        xl[c][3] = cx.x;      xh[c][3] = cx.y;
+        xl[c][4] = cx.y;      xh[c][4] = lx[2];
+        xl[c][5] = pn.x;      xh[c][5] = pn.y;
+      }
+      st2_terms<CB, 0, 6>(c1lo[IO], c1hi[IO], s_tab, xl, xh, sl, sh);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        p2[c] = dbl2v{sl[c], sh[c]};
+        l1p[c] = l1[c][IO];
+      }
+      c2lo = c1lo[IO];
+      c2hi = c1hi[IO];
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      c1lo[i] = clo[i];
+      c1hi[i] = chi[i];
+    }
+  };
+
+  // prologue: level 0 of plane z0-2 (the -W operand of plane z0-1's level 1),
+  // plane z0-1 in flight
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) l0p[c][i] = ld(c, row_of(z0 - 2, 1 + 2 * H + i));
+  issue(st, z0 - 1);
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  __syncthreads();                      // s_tab
+  for (int64_t s = z0 - 1; s <= zlast; ++s) step(s);
+  flush(acc1, a.partials, s_red1, seg1);
+  flush(acc2, a.partials2, s_red2, seg2);
+}
+
+// KR_ST2T_W (compile time, A/B builds): waves-per-SIMD target (0: the
+// compiler's choice).
+#ifndef KR_ST2T_W
+#define KR_ST2T_W 0
+#endif
+template <int EPI, int CB, bool PO>
+__global__ __launch_bounds__(2 * kBlock)
+#if KR_ST2T_W > 0
+__attribute__((amdgpu_waves_per_eu(KR_ST2T_W)))
+#endif
+void spmv_stencil2t_kernel(SpmvArgs a) {
+  if (a.stop && *a.stop != 0.0) return;
+  static_assert(CB == 2 || CB == 4, "tiled fused basis pair: narrow codes");
+  __shared__ __attribute__((aligned(16))) St2tLds s_l;
+  __shared__ double s_tab[kVdMax];
+  __shared__ double s_red[2][2][7 * 4];  // [level][group]
+  if (threadIdx.x < (unsigned)a.ntab) s_tab[threadIdx.x] = a.vtab[threadIdx.x];
+  // position-major pairs: XCD q = B & 7 walks the position pairs of
+  // [q P/8, (q+1) P/8) over the plane segments of the walk grid
+  const int64_t P = a.st_P, PP = P >> 3;
+  const int64_t B = blockIdx.x, q = B & 7, w2 = B >> 3;
+  const int64_t half = PP >> 1, Zw = gridDim.x / (P >> 1);
+  const int64_t p0 = q * PP + 2 * (w2 % half);
+  const int64_t zs = w2 / half;
+  const int h = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kBlock));
+  const int tid = (int)(threadIdx.x % kBlock);
+  if (h == 0)
+    st2t_walk<EPI, CB, PO, 0>(a, s_l, s_tab, s_red[0][0], s_red[1][0], tid, p0, q, zs, Zw);
+  else
+    st2t_walk<EPI, CB, PO, 1>(a, s_l, s_tab, s_red[0][1], s_red[1][1], tid, p0, q, zs, Zw);
+}
+
+template <int EPI>
+inline void spmv_stencil2t_launch(const SpmvArgs& a, int nblocks, hipStream_t s) {
+  const int64_t planes = a.st_P > 0 ? a.n / ((int64_t)a.st_P * kSBlock) : 0;
+  KR_REQUIRE(a.scode && a.st_P % 16 == 0 && a.st_nm == 7 && a.st_nfar == 2 &&
+                 a.st_far[0] == -kSBlock && a.st_far[1] == kSBlock &&
+                 a.n % ((int64_t)a.st_P * kSBlock) == 0 && a.rb_gap == 0 && a.partials2 &&
+                 (a.st_cb == 2 || a.st_cb == 4) && a.st2_z1 > 0 && a.st2_z2 > 0 &&
+                 nblocks % (a.st_P / 2) == 0 && a.st2_z1 % (2 * nblocks / a.st_P) == 0 &&
+                 a.st2_z2 % (2 * nblocks / a.st_P) == 0 && planes >= a.st2_z1 &&
+                 planes >= a.st2_z2,
+             "tiled fused basis pair: 7-point stencil with n = 512, P % 16 == 0, whole planes, "
+             "narrow codes, a walk grid dividing both dual grids");
+  const bool po = a.products_only != 0;
+  if (a.st_cb == 2)
+    po ? spmv_stencil2t_kernel<EPI, 2, true><<<nblocks, 2 * kBlock, 0, s>>>(a)
+       : spmv_stencil2t_kernel<EPI, 2, false><<<nblocks, 2 * kBlock, 0, s>>>(a);
+  else
+    po ? spmv_stencil2t_kernel<EPI, 4, true><<<nblocks, 2 * kBlock, 0, s>>>(a)
+       : spmv_stencil2t_kernel<EPI, 4, false><<<nblocks, 2 * kBlock, 0, s>>>(a);
+  KR_HIP_CHECK(hipGetLastError());
+}

@@ -107,6 +107,10 @@ MATRICES = {
     "aniso64x128x18": lambda: aniso(64, 128, 18, 1.0, 0.5, 0.25),  # P = 16, 4-bit codes
     "vals40_128x64x10": lambda: revalued(box(128, 64, 10), 40),    # P = 16, 8-bit codes
     "box128x128x16": lambda: box(128, 128, 16),                # P = 32
+    # n = 512 and P % 16 == 0: the tiled fused pair (KR_ST2=2)
+    "box512x32x10": lambda: box(512, 32, 10),                  # P = 32
+    "aniso512x16x12": lambda: aniso(512, 16, 12, 1.0, 0.5, 0.25),  # P = 16, 4-bit codes
+    "box512x16x64": lambda: box(512, 16, 64),                  # P = 16, 64 planes: 8 segments
 }
 # stencil code width (bits per slot) the engine picks for the 7-point pattern
 EXPECT_CB = {"aniso32x32x7": 4, "vals3_32x32x7": 2, "vals15_64x64x9": 4, "vals40_32x32x7": 8,
@@ -118,7 +122,8 @@ EXPECT_P = {"p3d32": 2, "p3d64": 8, "box32x32x7": 2, "box64x16x9": 2, "box48x32x
             "box64x64x20": 8, "box128x32x9": 8, "aniso32x32x7": 2, "vals3_32x32x7": 2,
             "vals15_64x64x9": 8, "vals40_32x32x7": 2, "box512x8x16": 8, "box512x16x12": 16,
             "aniso512x8x12": 8, "box128x64x20": 16, "aniso64x128x18": 16,
-            "vals40_128x64x10": 16, "box128x128x16": 32}
+            "vals40_128x64x10": 16, "box128x128x16": 32, "box512x32x10": 32,
+            "aniso512x16x12": 16, "box512x16x64": 16}
 NOT_STENCIL = {
     "p3d24": lambda: golden_matrix(["poisson", 24, 3]),      # 576 % 512 != 0
     "p3d16": lambda: golden_matrix(["poisson", 16, 3]),
@@ -333,6 +338,72 @@ def test_stencil_pair_bitwise_equal_duals(monkeypatch, method, name, k):
         np.testing.assert_array_equal(i1["khistory"], i0["khistory"])
     np.testing.assert_array_equal(i1["residual"], i0["residual"])
     np.testing.assert_array_equal(x1, x0)
+
+
+# the tiled pair (KR_ST2=2, two positions per workgroup, P % 16 == 0); env:
+# KR_PO_ZMAX=1 gives the products-only dual a 1-segment grid against the
+# general grid's 8 (the pair then flushes level 1 every 8 planes inside one
+# 64-plane walk), KR_ST2T_Z=1 makes every pair walk 64 planes (both levels flush)
+TILED_CASES = [("kskipmrr", "box512x16x12", 4, {}), ("kskipmrr", "box512x16x12", 5, {}),
+               ("adaptivekskipmrr", "box512x16x12", 8, {}), ("kskipmrr", "aniso512x16x12", 4, {}),
+               ("kskipmrr", "box512x32x10", 3, {}), ("kskipcg", "box512x16x12", 4, {}),
+               ("kskipcg", "box512x32x10", 5, {}),
+               ("kskipmrr", "box512x16x64", 4, {"KR_PO_ZMAX": "1"}),
+               ("kskipmrr", "box512x16x64", 4, {"KR_PO_ZMAX": "1", "KR_ST2T_Z": "1"}),
+               ("kskipcg", "box512x16x64", 4, {"KR_PO_ZMAX": "2", "KR_ST2T_Z": "1"})]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method,name,k,env", TILED_CASES,
+                         ids=[f"{m}-{n}-k{k}-{len(e)}" for m, n, k, e in TILED_CASES])
+def test_stencil_tiled_pair_bitwise_equal_duals(monkeypatch, method, name, k, env):
+    """The tiled fused basis pair (spmv_stencil2t_kernel: two positions per
+    workgroup, level 1 on chip) against the dual SpMVs (KR_ST2=0): histories
+    and x bit for bit -- every row summed in stored order and every product
+    accumulated in the dual launches' order into their partials, through
+    segment boundaries of either dual grid inside one walk, for k-skip MrR,
+    adaptive k-skip MrR and k-skip CG, odd and even k, 2- and 4-bit codes."""
+    A = MATRICES[name]()
+    b = np.random.default_rng(5).standard_normal(A.shape[0])
+    kw = dict(tol=1e-10, maxiter=400, k=k)
+    monkeypatch.setenv("KRYLOV_AMD_SHARDS", "0")
+    for key, val in env.items():
+        monkeypatch.setenv(key, val)
+    out = []
+    for st2 in ("0", "2"):
+        monkeypatch.setenv("KR_ST2", st2)
+        with contextlib.redirect_stdout(io.StringIO()):
+            x, info = _solver(method)(A, b, **kw)
+        out.append((x.cpu().numpy(), info))
+    (x0, i0), (x1, i1) = out
+    np.testing.assert_array_equal(i1["nosl"], i0["nosl"])
+    if "khistory" in i0:
+        np.testing.assert_array_equal(i1["khistory"], i0["khistory"])
+    np.testing.assert_array_equal(i1["residual"], i0["residual"])
+    np.testing.assert_array_equal(x1, x0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method,k", [("kskipmrr", 4), ("kskipmrr", 3), ("kskipcg", 4)])
+def test_stencil_tiled_pair_is_used(monkeypatch, method, k):
+    """KR_ST2=2 runs k // 2 tiled pair launches per outer iteration (the last
+    products-only for even k) and k % 2 single duals on a qualifying shard."""
+    monkeypatch.setenv("KR_ST2", "2")
+    A = MATRICES["box512x16x12"]()
+    sysm = _system(A, 1)
+    tag = "mrr" if method == "kskipmrr" else "kcg"
+    try:
+        b = sysm.split(np.random.default_rng(1).standard_normal(A.shape[0]))
+        sysm.begin(method, b, None, tol=0.0, maxiter=8 * (k + 1) + 2, k=k, profile=1)
+        sysm.step(4)
+        st = {r["name"]: r["launches"] for r in sysm.kernel_stats()}
+        sysm.finish(method)
+    finally:
+        sysm.close()
+    npair = st.get(f"spmv2x2_gram_{tag}", 0) + st.get(f"spmv2x2_gram_{tag}_last", 0)
+    ndual = st.get(f"spmv2_gram_{tag}", 0) + st.get(f"spmv2_gram_{tag}_last", 0)
+    assert npair == 4 * (k // 2) and ndual == 4 * (k % 2), st
+    assert st.get(f"spmv2x2_gram_{tag}_last", 0) == (4 if k % 2 == 0 else 0), st
 
 
 @pytest.mark.gpu
