@@ -1150,67 +1150,78 @@ inline void spmv_stencil2_launch(const SpmvArgs& a, int nblocks, hipStream_t s) 
 // Tiled fused basis pair (spmv_stencil2t_kernel; KR_ST2=2). The pair above
 // walks ONE position and must rebuild level 1 on three blocks and load level
 // 0 on five for it (3x the level-1 work, 2 waves per SIMD): slower than the
-// two dual launches it replaces. Here a 512-thread workgroup walks TWO
-// adjacent positions p0, p0 + 1 (p0 even) of a plane segment, one 256-lane
-// group per position (group H owns position p0 + H, lane t its rows 2t and
-// 2t + 1, as in the dual kernel):
+// two dual launches it replaces. Here a 1024-thread workgroup walks TWO
+// adjacent positions p0, p0 + 1 (p0 even) of a plane segment; four 256-lane
+// groups g = (line H = g >> 1, chain C = g & 1), lane t owning rows 2t and
+// 2t + 1 of position p0 + H in chain C (the dual kernel's lane mapping):
 //
-//   level 0 (loaded)  : positions p0-2 .. p0+3, three per group
-//   level 1 (computed): positions p0-1 .. p0+2, two per group (one redundant)
-//   level 2 (stored)  : positions p0, p0+1, one per group
+//   level 0 (loaded)  : positions p0-2 .. p0+3, three per line group
+//   level 1 (computed): positions p0-1 .. p0+2, two per line group (one redundant)
+//   level 2 (stored)  : positions p0, p0+1, one per line group
 //
-// so the redundant work is one level-1 line per output line, and each group
-// reads three level-0 lines per plane for two levels (the dual reads three
-// per level). Level 0 goes to LDS as it arrives (all six lines: the +-1 and
-// +-n operands of level 1) and the next plane's loads reuse its registers
-// at once, so a whole plane step hides them; level 1 of p0 and p0 + 1 goes
-// to LDS for level 2 (+-1, and +-n across the groups). Two barriers per plane.
+// so the redundant work is one level-1 line per output line, and a group
+// reads three level-0 lines of its chain per plane for two levels (the dual
+// reads three per level and chain). Level 0 goes to LDS as it arrives (the
+// six lines' +-1 and +-n operands) and the next plane's loads reuse its
+// registers at once, so a whole plane step hides them; level 1 of p0 and
+// p0 + 1 goes to LDS for level 2. A group holds one chain: ~120 VGPRs, so
+// 16 waves (4 per SIMD) share the CU. Two barriers per plane.
 //
 // Bitwise the two dual launches, products included: every row is summed in
 // stored order from 0.0 (-W ... +n when its plane arrives, +W one plane
-// later), and group H accumulates the products of dual m (level 0 x level 1)
-// and of dual m+1 (level 1 x level 2) of its position plane by plane, row 2t
-// then 2t+1, exactly as the dual launch's workgroup of that (position,
-// segment) does. The walk segment is a union of segments of both dual grids
-// (the level-2 grid is the products-only one for the last pair); at each
-// grid's segment boundary the group's accumulator is reduced into that grid's
-// partial of the virtual workgroup, so the partials are the dual launches'.
+// later). Dual m's products (level 0 x level 1) of position p0 + H are
+// accumulated by group (H, 0), dual m+1's (level 1 x level 2) by group
+// (H, 1) -- each lane plane by plane, row 2t then 2t+1, the other chain's
+// operands read from LDS -- exactly as the dual launch's workgroup of that
+// (position, segment) accumulates them. The walk segment is a union of
+// segments of both dual grids (the level-2 grid is the products-only one for
+// the last pair); at each grid's segment boundary the group's accumulator is
+// reduced into that grid's partial of the virtual workgroup.
 // ---------------------------------------------------------------------------
 struct St2tLds {
-  double x0[2][6 * kSBlock];           // level 0 of positions p0-2 .. p0+3 [chain][line*512 + row]
-  double x1[2][2 * kSBlock + 4];       // level 1 of p0, p0+1 [chain][2 + line*512 + row], margins
+  double x0[2][6 * kSBlock];       // level 0 of positions p0-2 .. p0+3 [chain][line*512 + row]
+  double x1[2][2 * kSBlock + 4];   // level 1 of p0, p0+1 [chain][2 + line*512 + row], margins
+  double xa[2][kSBlock];           // chain 1's level 0 of plane s-1, own line [line]
+  double xb[2][2][kSBlock];        // chain 0's level 1 and level 2 of plane s-2 [line][level]
+  double tab[kVdMax];
+  double red[4][7 * 4];            // [group]
 };
+constexpr size_t kSt2tLds = sizeof(St2tLds);
 
 template <int CB>
 struct St2tStage {
-  dbl2v x[2][3];            // level 0 of the group's three lines [chain][line]
+  dbl2v x[3];               // level 0 of the group's three lines
   uint32_t clo[2], chi[2];  // codes of the two level-1 lines (rows 2t, 2t+1)
 };
 
-template <int EPI, int CB, bool PO, int H>
-__device__ __forceinline__ void st2t_walk(const SpmvArgs& a, St2tLds& L, const double* s_tab,
-                                          double* s_red1, double* s_red2, int tid, int64_t p0,
+// One chain of one line: the tiled pair's work of group (H, C).
+template <int EPI, int CB, bool PO, int H, int C>
+__device__ __forceinline__ void st2t_walk(const SpmvArgs& a, St2tLds& L, int tid, int64_t p0,
                                           int64_t q, int64_t zs, int64_t Zw) {
   constexpr int NP = 7;
-  constexpr int IO = H == 0 ? 1 : 0;  // owned line among the group's level-1 lines
+  constexpr int IO = H == 0 ? 1 : 0;  // own line among the group's level-1 lines
+  constexpr int g = 2 * H + C;
   const int64_t P = a.st_P, W = P * kSBlock, PP = P >> 3;
   const int64_t planes = a.n / W;
   const int64_t z0 = planes * zs / Zw, z1 = planes * (zs + 1) / Zw;
   const int64_t pown = p0 + H;
-  const double* const xs[3] = {a.x1, a.x2, a.x2};
-  const SRes res = st_res<2, CB>(a, xs);
+  const double* const xs[3] = {C == 0 ? a.x1 : a.x2, a.x2, a.x2};
+  const SRes res = st_res<1, CB>(a, xs);
   const uint32_t lb = (uint32_t)tid * 16u;
+  const double* __restrict__ tab = L.tab;
   // first row of level-0 line l (0..5: positions p0-2 .. p0+3) at plane z
   auto row_of = [&](int64_t z, int l) { return z * W + (p0 - 2 + l) * kSBlock; };
-  auto ld = [&](int c, int64_t row) {
-    return st_bld2(res.x[c], (uint32_t)((a.xoff + row) * 8) + lb);
+#ifdef KR_ST2T_TIMING  // timing-only A/B build: every level-0 load reads plane 0 (L2 hits)
+  auto ld = [&](int64_t row) {
+    return st_bld2(res.x[0], (uint32_t)((a.xoff + (row % W + W) % W) * 8) + lb);
   };
+#else
+  auto ld = [&](int64_t row) { return st_bld2(res.x[0], (uint32_t)((a.xoff + row) * 8) + lb); };
+#endif
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
   auto issue = [&](St2tStage<CB>& st, int64_t z) {
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) st.x[c][j] = ld(c, row_of(z, 3 * H + j));
+    for (int j = 0; j < 3; ++j) st.x[j] = ld(row_of(z, 3 * H + j));
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int64_t r = row_of(z, 1 + 2 * H + i);
@@ -1228,43 +1239,111 @@ __device__ __forceinline__ void st2t_walk(const SpmvArgs& a, St2tLds& L, const d
       }
     }
   };
-  // products: virtual workgroup of (position, segment) in a dual grid, and
-  // the segment boundaries (walk segment zs of Zw starts segment zs Z / Zw)
-  auto vblock = [&](int64_t seg) { return 8 * (seg * PP + (pown - q * PP)) + q; };
-  const int64_t Z1 = a.st2_z1, Z2 = a.st2_z2;
-  int64_t seg1 = zs * (Z1 / Zw), seg2 = zs * (Z2 / Zw);
-  int64_t nb1 = planes * (seg1 + 1) / Z1, nb2 = planes * (seg2 + 1) / Z2;
-  double acc1[NP], acc2[NP];
+  // One chain's sums over slots K0 .. K1-1 (st2_terms' rules: a slot present
+  // in every row of the wave adds without the absent-entry selects).
+  auto terms = [&](auto k0c, auto k1c, uint32_t clo, uint32_t chi, const double (&xl)[7],
+                   const double (&xh)[7], double& sl, double& sh) {
+    constexpr int K0 = decltype(k0c)::value, K1 = decltype(k1c)::value;
+    constexpr unsigned kNone = (1u << CB) - 1u;
 #pragma unroll
-  for (int k = 0; k < NP; ++k) acc1[k] = acc2[k] = 0.0;
-  auto flush = [&](double (&acc)[NP], double* part, double* s_red, int64_t seg) {
-    block_reduce_store<NP>(acc, part, a.grid, s_red, 0, tid, vblock(seg));
+    for (int k = K0; k < K1; ++k) {
+      const unsigned cl = (clo >> (CB * k)) & kNone, ch = (chi >> (CB * k)) & kNone;
+      const double vl = tab[cl], vh = tab[ch];
+      if (__builtin_amdgcn_ballot_w64(cl == kNone || ch == kNone) == 0) {
+        sl = sl + vl * xl[k];
+        sh = sh + vh * xh[k];
+      } else {
+        const double tl = sl + vl * xl[k], th = sh + vh * xh[k];
+        sl = cl != kNone ? tl : sl;
+        sh = ch != kNone ? th : sh;
+      }
+    }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I6 = std::integral_constant<int, 6>;
+  using I7 = std::integral_constant<int, 7>;
+
+  // products: group (H, 0) accumulates dual m's (grid 1), group (H, 1) dual
+  // m+1's (grid 2) into the partials of the virtual workgroup (position,
+  // segment); walk segment zs of Zw starts segment zs Z / Zw of a grid of Z
+  double* const part = C == 0 ? a.partials : a.partials2;
+  int64_t seg = zs * ((C == 0 ? a.st2_z1 : a.st2_z2) / Zw);  // this group's level's segment
+  double acc[NP];
 #pragma unroll
-    for (int k = 0; k < NP; ++k) acc[k] = 0.0;
+  for (int k = 0; k < NP; ++k) acc[k] = 0.0;
+  // every group joins every flush (it holds a barrier); `mine`: this group's level
+  auto flush = [&](bool mine) {
+    const int lane = tid & 63, wave = tid >> 6;
+    if (mine) {
+#pragma unroll
+      for (int k = 0; k < NP; ++k) {
+        double v = acc[k];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+        if (lane == 0) L.red[g][k * 4 + wave] = v;
+      }
+    }
+    __syncthreads();
+    if (mine) {
+      if (tid < NP) {
+        const double* r = L.red[g] + tid * 4;
+        double t = r[0];
+        t = t + r[1];
+        t = t + r[2];
+        t = t + r[3];
+        part[(int64_t)tid * a.grid + 8 * (seg * PP + (pown - q * PP)) + q] = t;
+      }
+#pragma unroll
+      for (int k = 0; k < NP; ++k) acc[k] = 0.0;
+      ++seg;
+    }
+  };
+  // a level's products at plane z: flush first when z starts the next
+  // segment of that level's grid (the test is uniform: every group joins)
+  int64_t sg1 = zs * (a.st2_z1 / Zw), sg2 = zs * (a.st2_z2 / Zw);
+  int64_t nb1 = planes * (sg1 + 1) / a.st2_z1;  // level 1's next boundary
+  int64_t nb2 = planes * (sg2 + 1) / a.st2_z2;
+  auto cross = [&](int64_t z, int level) {
+    int64_t& b = level == 1 ? nb1 : nb2;
+    int64_t& sgx = level == 1 ? sg1 : sg2;
+    const int64_t Zl = level == 1 ? a.st2_z1 : a.st2_z2;
+    if (z >= b) {
+      flush((level == 1) == (C == 0));
+      ++sgx;
+      b = planes * (sgx + 1) / Zl;
+    }
   };
 
   // ---- state carried along the walk (step s: level 0 of plane s arrives)
-  dbl2v l0p[2][2];            // level 0 of plane s-1 at the level-1 lines
-  dbl2v p1[2][2];             // partial level-1 sums of plane s-1 (slots -W .. +n)
+  dbl2v l0p[2];                 // level 0 of plane s-1 at the two level-1 lines
+  dbl2v p1[2];                  // partial level-1 sums of plane s-1 (slots -W .. +n)
   uint32_t c1lo[2] = {0u, 0u}, c1hi[2] = {0u, 0u};  // their codes
-  dbl2v l1p[2];               // level 1 of plane s-2, own line
-  dbl2v p2[2];                // partial level-2 sums of plane s-2
+  dbl2v l1p = dbl2v{0.0, 0.0};  // level 1 of plane s-2, own line
+  dbl2v p2 = dbl2v{0.0, 0.0};   // partial level-2 sums of plane s-2
   uint32_t c2lo = 0u, c2hi = 0u;
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    l1p[c] = p2[c] = dbl2v{0.0, 0.0};
-#pragma unroll
-    for (int i = 0; i < 2; ++i) p1[c][i] = dbl2v{0.0, 0.0};
-  }
+  dbl2v k1 = dbl2v{0.0, 0.0}, k2 = dbl2v{0.0, 0.0};  // C = 1: own level 1, 2 of plane s-3
+  p1[0] = p1[1] = dbl2v{0.0, 0.0};
   const int64_t zlast = z1 + 1;
   St2tStage<CB> st;
+  // C = 1: dual m+1's products at plane z = s-3 (level 1, 2 of chain 0 from LDS)
+  auto level2_products = [&](int64_t z) {
+    if (z >= z0 && z < z1) {
+      cross(z, 2);
+      if constexpr (C == 1) {
+        const dbl2v o1 = reinterpret_cast<const dbl2v*>(L.xb[H][0])[tid];
+        const dbl2v o2 = reinterpret_cast<const dbl2v*>(L.xb[H][1])[tid];
+        epi_products<EPI>(o1.x, k1.x, o2.x, k2.x, 0.0, acc);
+        epi_products<EPI>(o1.y, k1.y, o2.y, k2.y, 0.0, acc);
+      }
+    }
+  };
   auto step = [&](int64_t s) {
-    // (1) level 0 of plane s to LDS; the next plane's loads take its registers
+    // (1) level 0 of plane s to LDS; chain 1 hands its own line's level 0 of
+    // plane s-1 to chain 0 (dual m's x2); the next plane's loads take the
+    // stage registers
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int j = 0; j < 3; ++j)
-        reinterpret_cast<dbl2v*>(L.x0[c] + (3 * H + j) * kSBlock)[tid] = st.x[c][j];
+    for (int j = 0; j < 3; ++j) reinterpret_cast<dbl2v*>(L.x0[C] + (3 * H + j) * kSBlock)[tid] = st.x[j];
+    if constexpr (C == 1) reinterpret_cast<dbl2v*>(L.xa[H])[tid] = l0p[IO];
     uint32_t clo[2], chi[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -1273,115 +1352,88 @@ __device__ __forceinline__ void st2t_walk(const SpmvArgs& a, St2tLds& L, const d
     }
     issue(st, s + 1 <= zlast ? s + 1 : s);  // (the last step re-reads its own plane)
     __syncthreads();
+    level2_products(s - 3);
+    dbl2v x2p = dbl2v{0.0, 0.0};  // C = 0: chain 1's level 0 of plane s-1, own line
+    if constexpr (C == 0) x2p = reinterpret_cast<const dbl2v*>(L.xa[H])[tid];
+    const dbl2v x1p = l0p[IO];    // own chain's level 0 of plane s-1, own line
     // (2) level 1: plane s-1 completed by +W, plane s started
-    dbl2v l1[2][2];
+    dbl2v l1[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int li = 1 + 2 * H + i;  // level-0 line of this level-1 line
-      dbl2v cx[2];
-#pragma unroll
-      for (int c = 0; c < 2; ++c) cx[c] = reinterpret_cast<const dbl2v*>(L.x0[c] + li * kSBlock)[tid];
+      const double* line = L.x0[C] + (1 + 2 * H + i) * kSBlock + 2 * tid;
+      const dbl2v cx = *reinterpret_cast<const dbl2v*>(line);
       {
-        double xl[2][7], xh[2][7], sl[2], sh[2];
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          xl[c][6] = cx[c].x;
-          xh[c][6] = cx[c].y;
-          sl[c] = p1[c][i].x;
-          sh[c] = p1[c][i].y;
-        }
-        st2_terms<CB, 6, 7>(c1lo[i], c1hi[i], s_tab, xl, xh, sl, sh);
-#pragma unroll
-        for (int c = 0; c < 2; ++c) l1[c][i] = dbl2v{sl[c], sh[c]};
+        double xl[7], xh[7], sl = p1[i].x, sh = p1[i].y;
+        xl[6] = cx.x;
+        xh[6] = cx.y;
+        terms(I6{}, I7{}, c1lo[i], c1hi[i], xl, xh, sl, sh);
+        l1[i] = dbl2v{sl, sh};
       }
-      double xl[2][7], xh[2][7], sl[2] = {0.0, 0.0}, sh[2] = {0.0, 0.0};
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const double* line = L.x0[c] + li * kSBlock + 2 * tid;
-        const dbl2v mn = *reinterpret_cast<const dbl2v*>(line - kSBlock);
-        const dbl2v pn = *reinterpret_cast<const dbl2v*>(line + kSBlock);
-        xl[c][0] = l0p[c][i].x;  xh[c][0] = l0p[c][i].y;
-        xl[c][1] = mn.x;         xh[c][1] = mn.y;
-        xl[c][2] = line[-1];     xh[c][2] = cx[c].x;
-        xl[c][3] = cx[c].x;      xh[c][3] = cx[c].y;
-        xl[c][4] = cx[c].y;      xh[c][4] = line[2];
-        xl[c][5] = pn.x;         xh[c][5] = pn.y;
-      }
-      st2_terms<CB, 0, 6>(clo[i], chi[i], s_tab, xl, xh, sl, sh);
-#pragma unroll
-      for (int c = 0; c < 2; ++c) p1[c][i] = dbl2v{sl[c], sh[c]};
-      // (3) dual m's products at plane s-1 (level 0 x level 1, own line)
-      if (i == IO) {
-        const int64_t zp1 = s - 1;
-        if (zp1 >= z0 && zp1 < z1) {
-          if (zp1 >= nb1) {
-            flush(acc1, a.partials, s_red1, seg1);
-            ++seg1;
-            nb1 = planes * (seg1 + 1) / Z1;
-          }
-          epi_products<EPI>(l0p[0][IO].x, l0p[1][IO].x, l1[0][IO].x, l1[1][IO].x, 0.0, acc1);
-          epi_products<EPI>(l0p[0][IO].y, l0p[1][IO].y, l1[0][IO].y, l1[1][IO].y, 0.0, acc1);
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < 2; ++c) l0p[c][i] = cx[c];
+      const dbl2v mn = *reinterpret_cast<const dbl2v*>(line - kSBlock);
+      const dbl2v pn = *reinterpret_cast<const dbl2v*>(line + kSBlock);
+      double xl[7], xh[7], sl = 0.0, sh = 0.0;
+      xl[0] = l0p[i].x;  xh[0] = l0p[i].y;
+      xl[1] = mn.x;      xh[1] = mn.y;
+      xl[2] = line[-1];  xh[2] = cx.x;
+      xl[3] = cx.x;      xh[3] = cx.y;
+      xl[4] = cx.y;      xh[4] = line[2];
+      xl[5] = pn.x;      xh[5] = pn.y;
+      terms(I0{}, I6{}, clo[i], chi[i], xl, xh, sl, sh);
+      p1[i] = dbl2v{sl, sh};
+      l0p[i] = cx;
     }
-    // (4) level 1 of plane s-1, own line (+ the outer margin) for level 2
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      reinterpret_cast<dbl2v*>(L.x1[c] + 2 + H * kSBlock)[tid] = l1[c][IO];
-      if (H == 0 && tid == kBlock - 1) L.x1[c][1] = l1[c][0].y;             // p0-1, row 511
-      if (H == 1 && tid == 0) L.x1[c][2 + 2 * kSBlock] = l1[c][1].x;        // p0+2, row 0
-    }
+    // (3) level 1 of plane s-1, own line (+ the outer margin) for level 2
+    reinterpret_cast<dbl2v*>(L.x1[C] + 2 + H * kSBlock)[tid] = l1[IO];
+    if (H == 0 && tid == kBlock - 1) L.x1[C][1] = l1[0].y;                 // p0-1, row 511
+    if (H == 1 && tid == 0) L.x1[C][2 + 2 * kSBlock] = l1[1].x;            // p0+2, row 0
     __syncthreads();
+    // (4) dual m's products at plane s-1: level 0 x level 1, both chains
+    const int64_t zp1 = s - 1;
+    if (zp1 >= z0 && zp1 < z1) {
+      cross(zp1, 1);
+      if constexpr (C == 0) {
+        const dbl2v y2 = reinterpret_cast<const dbl2v*>(L.x1[1] + 2 + H * kSBlock)[tid];
+        epi_products<EPI>(x1p.x, x2p.x, l1[IO].x, y2.x, 0.0, acc);
+        epi_products<EPI>(x1p.y, x2p.y, l1[IO].y, y2.y, 0.0, acc);
+      }
+    }
     // (5) level 2: plane s-2 completed by +W (level 1 of plane s-1), plane s-1 started
     {
-      double xl[2][7], xh[2][7], sl[2], sh[2];
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        xl[c][6] = l1[c][IO].x;
-        xh[c][6] = l1[c][IO].y;
-        sl[c] = p2[c].x;
-        sh[c] = p2[c].y;
-      }
-      st2_terms<CB, 6, 7>(c2lo, c2hi, s_tab, xl, xh, sl, sh);
+      double xl[7], xh[7], sl = p2.x, sh = p2.y;
+      xl[6] = l1[IO].x;
+      xh[6] = l1[IO].y;
+      terms(I6{}, I7{}, c2lo, c2hi, xl, xh, sl, sh);
       const int64_t zp2 = s - 2;
       if (zp2 >= z0 && zp2 < z1) {
-        if (zp2 >= nb2) {
-          flush(acc2, a.partials2, s_red2, seg2);
-          ++seg2;
-          nb2 = planes * (seg2 + 1) / Z2;
-        }
-        epi_products<EPI>(l1p[0].x, l1p[1].x, sl[0], sl[1], 0.0, acc2);
-        epi_products<EPI>(l1p[0].y, l1p[1].y, sh[0], sh[1], 0.0, acc2);
         if constexpr (!PO) {
           const int64_t row = zp2 * W + pown * kSBlock + 2 * tid;
-          __builtin_nontemporal_store(dbl2v{sl[0], sh[0]}, reinterpret_cast<dbl2v*>(a.y1 + row));
-          __builtin_nontemporal_store(dbl2v{sl[1], sh[1]}, reinterpret_cast<dbl2v*>(a.y2 + row));
+          __builtin_nontemporal_store(dbl2v{sl, sh},
+                                      reinterpret_cast<dbl2v*>((C == 0 ? a.y1 : a.y2) + row));
         }
+      }
+      if constexpr (C == 0) {  // chain 0's level 1 and 2 of plane s-2 for the level-2 products
+        reinterpret_cast<dbl2v*>(L.xb[H][0])[tid] = l1p;
+        reinterpret_cast<dbl2v*>(L.xb[H][1])[tid] = dbl2v{sl, sh};
+      } else {
+        k1 = l1p;
+        k2 = dbl2v{sl, sh};
       }
     }
     {
-      double xl[2][7], xh[2][7], sl[2] = {0.0, 0.0}, sh[2] = {0.0, 0.0};
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const double* lx = L.x1[c] + 2 + H * kSBlock + 2 * tid;
-        const dbl2v cx = l1[c][IO];
-        const dbl2v mn = H == 0 ? l1[c][0] : *reinterpret_cast<const dbl2v*>(lx - kSBlock);
-        const dbl2v pn = H == 0 ? *reinterpret_cast<const dbl2v*>(lx + kSBlock) : l1[c][1];
-        xl[c][0] = l1p[c].x;  xh[c][0] = l1p[c].y;
-        xl[c][1] = mn.x;      xh[c][1] = mn.y;
-        xl[c][2] = lx[-1];    xh[c][2] = cx.x;
-        xl[c][3] = cx.x;      xh[c][3] = cx.y;
-        xl[c][4] = cx.y;      xh[c][4] = lx[2];
-        xl[c][5] = pn.x;      xh[c][5] = pn.y;
-      }
-      st2_terms<CB, 0, 6>(c1lo[IO], c1hi[IO], s_tab, xl, xh, sl, sh);
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        p2[c] = dbl2v{sl[c], sh[c]};
-        l1p[c] = l1[c][IO];
-      }
+      const double* lx = L.x1[C] + 2 + H * kSBlock + 2 * tid;
+      const dbl2v cx = l1[IO];
+      const dbl2v mn = H == 0 ? l1[0] : *reinterpret_cast<const dbl2v*>(lx - kSBlock);
+      const dbl2v pn = H == 0 ? *reinterpret_cast<const dbl2v*>(lx + kSBlock) : l1[1];
+      double xl[7], xh[7], sl = 0.0, sh = 0.0;
+      xl[0] = l1p.x;   xh[0] = l1p.y;
+      xl[1] = mn.x;    xh[1] = mn.y;
+      xl[2] = lx[-1];  xh[2] = cx.x;
+      xl[3] = cx.x;    xh[3] = cx.y;
+      xl[4] = cx.y;    xh[4] = lx[2];
+      xl[5] = pn.x;    xh[5] = pn.y;
+      terms(I0{}, I6{}, c1lo[IO], c1hi[IO], xl, xh, sl, sh);
+      p2 = dbl2v{sl, sh};
+      l1p = cx;
       c2lo = c1lo[IO];
       c2hi = c1hi[IO];
     }
@@ -1395,15 +1447,15 @@ __device__ __forceinline__ void st2t_walk(const SpmvArgs& a, St2tLds& L, const d
   // prologue: level 0 of plane z0-2 (the -W operand of plane z0-1's level 1),
   // plane z0-1 in flight
 #pragma unroll
-  for (int c = 0; c < 2; ++c)
-#pragma unroll
-    for (int i = 0; i < 2; ++i) l0p[c][i] = ld(c, row_of(z0 - 2, 1 + 2 * H + i));
+  for (int i = 0; i < 2; ++i) l0p[i] = ld(row_of(z0 - 2, 1 + 2 * H + i));
   issue(st, z0 - 1);
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-  __syncthreads();                      // s_tab
+  __syncthreads();                      // tab
   for (int64_t s = z0 - 1; s <= zlast; ++s) step(s);
-  flush(acc1, a.partials, s_red1, seg1);
-  flush(acc2, a.partials2, s_red2, seg2);
+  __syncthreads();
+  level2_products(z1 - 1);  // the last plane's, written by the last step
+  flush(C == 0);            // level 1's last segment (group (H, 0))
+  flush(C == 1);            // level 2's (group (H, 1))
 }
 
 // KR_ST2T_W (compile time, A/B builds): waves-per-SIMD target (0: the
@@ -1412,17 +1464,16 @@ __device__ __forceinline__ void st2t_walk(const SpmvArgs& a, St2tLds& L, const d
 #define KR_ST2T_W 0
 #endif
 template <int EPI, int CB, bool PO>
-__global__ __launch_bounds__(2 * kBlock)
+__global__ __launch_bounds__(4 * kBlock)
 #if KR_ST2T_W > 0
 __attribute__((amdgpu_waves_per_eu(KR_ST2T_W)))
 #endif
 void spmv_stencil2t_kernel(SpmvArgs a) {
   if (a.stop && *a.stop != 0.0) return;
   static_assert(CB == 2 || CB == 4, "tiled fused basis pair: narrow codes");
-  __shared__ __attribute__((aligned(16))) St2tLds s_l;
-  __shared__ double s_tab[kVdMax];
-  __shared__ double s_red[2][2][7 * 4];  // [level][group]
-  if (threadIdx.x < (unsigned)a.ntab) s_tab[threadIdx.x] = a.vtab[threadIdx.x];
+  extern __shared__ __attribute__((aligned(16))) double s2t_dyn[];
+  St2tLds& L = *reinterpret_cast<St2tLds*>(s2t_dyn);
+  if (threadIdx.x < (unsigned)a.ntab) L.tab[threadIdx.x] = a.vtab[threadIdx.x];
   // position-major pairs: XCD q = B & 7 walks the position pairs of
   // [q P/8, (q+1) P/8) over the plane segments of the walk grid
   const int64_t P = a.st_P, PP = P >> 3;
@@ -1430,12 +1481,22 @@ void spmv_stencil2t_kernel(SpmvArgs a) {
   const int64_t half = PP >> 1, Zw = gridDim.x / (P >> 1);
   const int64_t p0 = q * PP + 2 * (w2 % half);
   const int64_t zs = w2 / half;
-  const int h = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kBlock));
+  const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kBlock));
   const int tid = (int)(threadIdx.x % kBlock);
-  if (h == 0)
-    st2t_walk<EPI, CB, PO, 0>(a, s_l, s_tab, s_red[0][0], s_red[1][0], tid, p0, q, zs, Zw);
-  else
-    st2t_walk<EPI, CB, PO, 1>(a, s_l, s_tab, s_red[0][1], s_red[1][1], tid, p0, q, zs, Zw);
+  switch (g) {
+    case 0: st2t_walk<EPI, CB, PO, 0, 0>(a, L, tid, p0, q, zs, Zw); break;
+    case 1: st2t_walk<EPI, CB, PO, 0, 1>(a, L, tid, p0, q, zs, Zw); break;
+    case 2: st2t_walk<EPI, CB, PO, 1, 0>(a, L, tid, p0, q, zs, Zw); break;
+    default: st2t_walk<EPI, CB, PO, 1, 1>(a, L, tid, p0, q, zs, Zw); break;
+  }
+}
+
+template <int EPI, int CB, bool PO>
+void st2t_launch_t(const SpmvArgs& a, int nblocks, hipStream_t s) {
+  static std::atomic<uint64_t> opted{0};  // per device (opt_in_lds)
+  opt_in_lds(opted, reinterpret_cast<const void*>(spmv_stencil2t_kernel<EPI, CB, PO>), kSt2tLds);
+  spmv_stencil2t_kernel<EPI, CB, PO><<<nblocks, 4 * kBlock, kSt2tLds, s>>>(a);
+  KR_HIP_CHECK(hipGetLastError());
 }
 
 template <int EPI>
@@ -1452,10 +1513,7 @@ inline void spmv_stencil2t_launch(const SpmvArgs& a, int nblocks, hipStream_t s)
              "narrow codes, a walk grid dividing both dual grids");
   const bool po = a.products_only != 0;
   if (a.st_cb == 2)
-    po ? spmv_stencil2t_kernel<EPI, 2, true><<<nblocks, 2 * kBlock, 0, s>>>(a)
-       : spmv_stencil2t_kernel<EPI, 2, false><<<nblocks, 2 * kBlock, 0, s>>>(a);
+    po ? st2t_launch_t<EPI, 2, true>(a, nblocks, s) : st2t_launch_t<EPI, 2, false>(a, nblocks, s);
   else
-    po ? spmv_stencil2t_kernel<EPI, 4, true><<<nblocks, 2 * kBlock, 0, s>>>(a)
-       : spmv_stencil2t_kernel<EPI, 4, false><<<nblocks, 2 * kBlock, 0, s>>>(a);
-  KR_HIP_CHECK(hipGetLastError());
+    po ? st2t_launch_t<EPI, 4, true>(a, nblocks, s) : st2t_launch_t<EPI, 4, false>(a, nblocks, s);
 }
