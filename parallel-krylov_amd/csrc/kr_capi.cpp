@@ -11,8 +11,11 @@ namespace {
 
 thread_local std::string g_last_error;
 
-template <class F>
+// BUMP: the call re-reads the cached KR_* knobs (kr_internal.h KR_ENV);
+// kr_solve_step keeps the values of its solve
+template <bool BUMP = true, class F>
 int guarded(F&& f) {
+  if (BUMP) g_env_epoch.fetch_add(1, std::memory_order_relaxed);
   try {
     f();
     return KR_OK;
@@ -427,13 +430,23 @@ int kr_system_create(kr_system** out, int64_t n_global, int nshards, const int* 
     sys->n_global = n_global;
     sys->comm = comm;
     sys->shards.resize(nshards);
+    // In-process shards on one device share that device's stream (System::
+    // groups). KR_SHARED_STREAM: 1 (default) all of a device's shards, 0 a
+    // stream per shard (A/B), g >= 2 runs of g consecutive shards (tests:
+    // several stream groups on one device, as several devices would have).
+    // With a communicator every local shard keeps its own (the hybrid RCCL paths).
+    const int ss = KR_ENV("KR_SHARED_STREAM", 1);
+    const bool share = !comm && ss != 0;
+    const int run = ss >= 2 ? ss : nshards;
     for (int s = 0; s < nshards; ++s) {
       Shard& sh = sys->shards[s];
       sh.dev = devices[s];
       sh.row0 = row_begin[s];
       sh.n = row_begin[s + 1] - row_begin[s];
       KR_HIP_CHECK(hipSetDevice(sh.dev));
-      KR_HIP_CHECK(hipStreamCreateWithFlags(&sh.stream, hipStreamNonBlocking));
+      for (int t = 0; share && t < s && !sh.stream; ++t)
+        if (sys->shards[t].dev == sh.dev && t / run == s / run) sh.stream = sys->shards[t].stream;
+      if (!sh.stream) KR_HIP_CHECK(hipStreamCreateWithFlags(&sh.stream, hipStreamNonBlocking));
     }
     if (comm) {
       // global partition from every rank's local shards: record = [count,
@@ -789,7 +802,7 @@ int kr_solve_set_precond_ilu(kr_system* sys, int64_t n, const int64_t* l_rowptr,
 }
 
 int kr_solve_step(kr_system* sys, int64_t max_outer, int* done) {
-  return guarded([&] {
+  return guarded<false>([&] {
     KR_REQUIRE(sys, "NULL system");
     if (!sys->session) throw Failure(KR_ERR_STATE, "kr_solve_begin was not called");
     Session& ss = *sys->session;

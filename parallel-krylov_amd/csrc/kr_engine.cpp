@@ -20,6 +20,8 @@
 
 namespace kr {
 
+std::atomic<uint64_t> g_env_epoch{0};
+
 double now_seconds() {
   using clk = std::chrono::steady_clock;
   return std::chrono::duration<double>(clk::now().time_since_epoch()).count();
@@ -263,7 +265,16 @@ System::~System() {
     if (s.comm_stream) (void)hipStreamDestroy(s.comm_stream);
     if (s.ev_a) (void)hipEventDestroy(s.ev_a);
     if (s.ev_b) (void)hipEventDestroy(s.ev_b);
-    if (s.stream) (void)hipStreamDestroy(s.stream);
+  }
+  // streams last, each once (shards of one device may share one)
+  for (size_t li = 0; li < shards.size(); ++li) {
+    Shard& s = shards[li];
+    bool first = s.stream != nullptr;
+    for (size_t t = 0; t < li && first; ++t) first = shards[t].stream != s.stream;
+    if (first) {
+      (void)hipSetDevice(s.dev);
+      (void)hipStreamDestroy(s.stream);
+    }
   }
 }
 
@@ -343,12 +354,22 @@ void ShardPool::run(int n, const std::function<void(int)>& fn) {
     if (e) std::rethrow_exception(e);
 }
 
-void System::for_shards(const std::function<void(Shard&, size_t)>& fn) {
-  if (pool && shards.size() > 1) {
-    pool->run((int)shards.size(), [&](int li) { fn(shards[(size_t)li], (size_t)li); });
+void System::for_groups(const std::function<void(const std::vector<int>&)>& fn) {
+  if (pool && groups.size() > 1) {
+    pool->run((int)groups.size(), [&](int g) { fn(groups[(size_t)g]); });
     return;
   }
-  for (size_t li = 0; li < shards.size(); ++li) fn(shards[li], li);
+  for (auto& g : groups) fn(g);
+}
+
+void System::for_shards(const std::function<void(Shard&, size_t)>& fn) {
+  if (groups.empty()) {  // before finalize
+    for (size_t li = 0; li < shards.size(); ++li) fn(shards[li], li);
+    return;
+  }
+  for_groups([&](const std::vector<int>& g) {
+    for (int li : g) fn(shards[(size_t)li], (size_t)li);
+  });
 }
 
 IluFactors::~IluFactors() {
@@ -474,8 +495,7 @@ bool stencil_pm(int P);
 
 int System::pair_mode() const {
   if (shards.size() != 1 || comm || nglobal_shards() != 1) return 0;
-  const char* env = getenv("KR_ST2");  // 0 / unset: two dual launches; 1, 2: the pairs (A/B)
-  const int mode = env ? atoi(env) : 0;
+  const int mode = KR_ENV("KR_ST2", 0);  // 0 / unset: two dual launches; 1, 2: the pairs (A/B)
   if (mode != 1 && mode != 2) return 0;
   const Shard& s = shards[0];
   if (!s.scode || !stencil_pm(s.st_P) || s.nm != 7 || s.st_nfar != 2) return 0;
@@ -1139,12 +1159,33 @@ void System::finalize() {
   // (the boundary launch of a shard waits for their copies before its later
   // kernels may overwrite those rows)
   if (!comm) {
-    for (auto& s : shards) s.readers.clear();
+    for (auto& s : shards) {
+      s.readers.clear();
+      s.ext_readers.clear();
+      s.ext_in = false;
+    }
     for (size_t li = 0; li < shards.size(); ++li)
       for (auto& p : shards[li].recv) {
-        auto& r = shards[(size_t)p.peer].readers;
+        Shard& t = shards[(size_t)p.peer];
+        auto& r = t.readers;
         if (std::find(r.begin(), r.end(), (int)li) == r.end()) r.push_back((int)li);
+        if (t.stream != shards[li].stream) {
+          shards[li].ext_in = true;
+          auto& x = t.ext_readers;
+          if (std::find(x.begin(), x.end(), (int)li) == x.end()) x.push_back((int)li);
+        }
       }
+  }
+  // stream groups (kr_system_create shares a device's stream between its
+  // in-process shards): shards in order within a group, groups in order of
+  // their first shard
+  groups.clear();
+  for (size_t li = 0; li < shards.size(); ++li) {
+    size_t g = 0;
+    while (g < groups.size() && shards[(size_t)groups[g][0]].stream != shards[li].stream) ++g;
+    if (g == groups.size()) groups.emplace_back();
+    shards[li].lead = groups[g].empty();
+    groups[g].push_back((int)li);
   }
   // The split SpMV needs interior rows on every shard; with RCCL ranks the
   // decision is global, so the summation order (interior + boundary partials)
@@ -1166,12 +1207,12 @@ void System::finalize() {
     KR_HIP_CHECK(hipFree(d));
     for (int64_t f : all) all_interior = all_interior && f != 0;
   }
-  // one host thread per further in-process shard (KR_HOST_THREADS=0: every
-  // shard's work enqueued by the calling thread, A/B)
+  // one host thread per further in-process stream group (KR_HOST_THREADS=0:
+  // every shard's work enqueued by the calling thread, A/B)
   {
     const char* ht = getenv("KR_HOST_THREADS");
-    if (!comm && shards.size() > 1 && !(ht && atoi(ht) == 0))
-      pool = std::make_unique<ShardPool>((int)shards.size() - 1);
+    if (!comm && groups.size() > 1 && !(ht && atoi(ht) == 0))
+      pool = std::make_unique<ShardPool>((int)groups.size() - 1);
   }
   {
     const char* env = getenv("KR_OVERLAP");  // 0 disables the split SpMV (A/B)
@@ -1484,6 +1525,7 @@ void System::halo_async(int id1, int id2, int id3) {
     KR_HIP_CHECK(hipEventRecord(s.ev_out, s.comm_stream));
     return;
   }
+  for (auto& g : groups) halo_group(g, id1, id2, id3);
   for (auto& s : shards) halo_in_process(s, id1, id2, id3);
 }
 
@@ -1491,6 +1533,8 @@ void System::halo_async(int id1, int id2, int id3) {
 // rows from the peers after their ev_in, then records ev_out. Touches only
 // this shard's streams (the per-shard host threads run it concurrently).
 void System::halo_in_process(Shard& s, int id1, int id2, int id3) {
+  // pieces from shards on s's own stream: halo_group (the group's gather)
+  if (!s.ext_in) return;
   KR_HIP_CHECK(hipSetDevice(s.dev));
   // The copies overwrite s's halo rows: s's own earlier kernels (the
   // previous SpMV's boundary rows read the same halo when consecutive SpMVs
@@ -1498,11 +1542,11 @@ void System::halo_in_process(Shard& s, int id1, int id2, int id3) {
   KR_HIP_CHECK(hipStreamWaitEvent(s.comm_stream, s.ev_in, 0));
   // Peers on this device: one gather launch for every piece (KR_HALO_KERNEL=0:
   // a hipMemcpyAsync per piece); peers on other devices: peer copies.
-  const char* hk = getenv("KR_HALO_KERNEL");
-  const bool gather = !hk || atoi(hk) != 0;
+  const bool gather = KR_ENV("KR_HALO_KERNEL", 1) != 0;
   HaloGatherArgs g;
   for (auto& p : s.recv) {
     Shard& t = shards[p.peer];
+    if (t.stream == s.stream) continue;
     KR_HIP_CHECK(hipStreamWaitEvent(s.comm_stream, t.ev_in, 0));
     for (int id : {id1, id2, id3}) {
       if (id < 0) continue;
@@ -1524,6 +1568,36 @@ void System::halo_in_process(Shard& s, int id1, int id2, int id3) {
   }
   launch_halo_gather(g, s.comm_stream);  // after every wait above
   KR_HIP_CHECK(hipEventRecord(s.ev_out, s.comm_stream));
+}
+
+// The halo pieces a stream group's shards take from each other, in ONE gather
+// launch on the group's stream (up to kHaloPieces pieces per launch): stream
+// order alone puts it after the producers of the source rows and the readers
+// of the destination rows (every earlier kernel of the group), and before the
+// boundary launches that read it -- no events, no comm stream.
+void System::halo_group(const std::vector<int>& grp, int id1, int id2, int id3) {
+  Shard& s0 = shards[(size_t)grp[0]];
+  KR_HIP_CHECK(hipSetDevice(s0.dev));
+  HaloGatherArgs g;
+  for (int li : grp) {
+    Shard& s = shards[(size_t)li];
+    for (auto& p : s.recv) {
+      Shard& t = shards[p.peer];
+      if (t.stream != s.stream) continue;
+      for (int id : {id1, id2, id3}) {
+        if (id < 0) continue;
+        if (g.n == kHaloPieces) {
+          launch_halo_gather(g, s0.stream);
+          g = HaloGatherArgs{};
+        }
+        g.src[g.n] = t.vec[id] + t.local_index(p.g0);
+        g.dst[g.n] = s.vec[id] + s.local_index(p.g0);
+        g.count[g.n] = p.count;
+        ++g.n;
+      }
+    }
+  }
+  launch_halo_gather(g, s0.stream);
 }
 
 void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int b,
@@ -1697,8 +1771,7 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
   // launch, so each starts on the plane segments the previous kernel streamed
   // last. Bitwise neutral; measured neutral on C4 (522.3 vs 522.1 it/s, same
   // box, three pairs: the first-steps kernel +2.5 %, the others -0.5-1 %).
-  const char* zz = getenv("KR_ZIGZAG");  // read per call: tests switch it
-  const bool zigzag = zz && atoi(zz) != 0;
+  const bool zigzag = KR_ENV("KR_ZIGZAG", 0) != 0;
   auto launch_full = [&](Shard& s, int64_t r_begin, int64_t rows) {
     SpmvArgs a = args_for(s, r_begin, rows, s.pstride, 0);
     if (s.scode && zigzag) {
@@ -1721,50 +1794,16 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
     return;
   }
   std::vector<hipEvent_t> t0s(shards.size(), nullptr);
-  // In-process shards: three phases on the per-shard host threads (a phase
-  // waits on events the previous one recorded on OTHER shards' streams, so
-  // the phases are separated by the pool's barrier); otherwise serial.
-  const bool threaded = !comm && pool;
-  const char* wa = getenv("KR_BOUNDARY_WAIT_ALL");
-  const bool wait_all = wa && atoi(wa) != 0;
+  const bool wait_all = KR_ENV("KR_BOUNDARY_WAIT_ALL", 0) != 0;
   auto phase_in =[&](Shard& s, size_t li) {
     KR_HIP_CHECK(hipSetDevice(s.dev));
     prof_begin(s, nm, t0s[li]);
     KR_HIP_CHECK(hipEventRecord(s.ev_in, s.stream));
   };
-  if (threaded) {
-    for_shards(phase_in);
-    for_shards([&](Shard& s, size_t) {
-      halo_in_process(s, in1, hx2, hx3);
-      launch_full(s, s.int_lo, s.int_hi - s.int_lo);  // interior rows
-    });
-  } else {
-    for (size_t li = 0; li < shards.size(); ++li) phase_in(shards[li], li);
-    halo_async(in1, hx2, hx3);
-    for (auto& s : shards) {  // interior rows: all blocks write their partials
-      KR_HIP_CHECK(hipSetDevice(s.dev));
-      launch_full(s, s.int_lo, s.int_hi - s.int_lo);
-    }
-  }
-  auto phase_boundary = [&](Shard& s, size_t li) {
-    KR_HIP_CHECK(hipSetDevice(s.dev));
-    if (comm && !hybrid()) {
-      KR_HIP_CHECK(hipStreamWaitEvent(s.stream, s.ev_out, 0));
-    } else if (!comm) {
-      // own halo copied, and every shard that copies from this one done
-      // reading its rows (the next kernels may overwrite them)
-      KR_HIP_CHECK(hipStreamWaitEvent(s.stream, s.ev_out, 0));
-      if (wait_all)  // KR_BOUNDARY_WAIT_ALL=1 (debug A/B): the round-2 edge set
-        for (auto& t : shards) KR_HIP_CHECK(hipStreamWaitEvent(s.stream, t.ev_out, 0));
-      else
-        for (int t : s.readers) KR_HIP_CHECK(hipStreamWaitEvent(s.stream, shards[t].ev_out, 0));
-    } else {
-      // own halo copied, and every reader done with this shard's rows
-      for (auto& t : shards) KR_HIP_CHECK(hipStreamWaitEvent(s.stream, t.ev_out, 0));
-      KR_HIP_CHECK(hipStreamWaitEvent(s.stream, hy_ev, 0));  // RCCL pieces
-    }
-    // both boundary ranges in one launch: row blocks [0, int_lo/B) and
-    // [int_hi/B, end) (interior bounds are whole blocks, see finalize)
+  // both boundary ranges in one launch: row blocks [0, int_lo/B) and
+  // [int_hi/B, end) (interior bounds are whole blocks, see finalize); the
+  // boundary launch adds its partials to the interior launch's
+  auto launch_boundary = [&](Shard& s) {
     const int64_t rbs = s.scode ? kStencilBlock : kBlock;  // rows per row block
     const int64_t nb_lo = s.int_lo / rbs, nb_gap = (s.int_hi - s.int_lo) / rbs;
     const int64_t nb_all = (s.n + rbs - 1) / rbs;
@@ -1776,12 +1815,78 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
       const int g = (int)std::min<int64_t>(grid_of(s), nb_all - nb_gap);
       launch_spmv_grid(epi, ab, g, s.stream);
     }
-    prof_end(s, nm, t0s[li], bytes_of(s));
   };
-  if (threaded)
-    for_shards(phase_boundary);
-  else
-    for (size_t li = 0; li < shards.size(); ++li) phase_boundary(shards[li], li);
+  if (!comm) {
+    // In-process shards: three phases, stream group by stream group (on the
+    // host threads when there are several groups: a phase waits on events the
+    // previous one recorded on OTHER groups' streams, so the phases are
+    // separated by the pool's barrier). Within a group (shards sharing a
+    // stream) stream order is the only edge: one gather launch moves the
+    // pieces the group's shards take from each other, then the interior
+    // launches, then (phase 3) the boundary launches. Pieces from other
+    // streams go through the receiving shard's comm stream between ev_in and
+    // ev_out as before. Profiling: one window per group, on its first shard.
+    for_shards([&](Shard& s, size_t li) {
+      KR_HIP_CHECK(hipSetDevice(s.dev));
+      if (s.lead) prof_begin(s, nm, t0s[li]);
+      if (s.ext_in || !s.ext_readers.empty()) KR_HIP_CHECK(hipEventRecord(s.ev_in, s.stream));
+    });
+    for_groups([&](const std::vector<int>& grp) {
+      halo_group(grp, in1, hx2, hx3);
+      for (int li : grp) halo_in_process(shards[(size_t)li], in1, hx2, hx3);
+      for (int li : grp) {
+        Shard& s = shards[(size_t)li];
+        KR_HIP_CHECK(hipSetDevice(s.dev));
+        launch_full(s, s.int_lo, s.int_hi - s.int_lo);  // interior rows
+      }
+    });
+    for_groups([&](const std::vector<int>& grp) {
+      double bytes = 0;
+      for (int li : grp) {
+        Shard& s = shards[(size_t)li];
+        KR_HIP_CHECK(hipSetDevice(s.dev));
+        // own halo copied by the comm stream, and every shard on another
+        // stream that copies from this one done reading its rows (the next
+        // kernels may overwrite them)
+        if (s.ext_in) KR_HIP_CHECK(hipStreamWaitEvent(s.stream, s.ev_out, 0));
+        if (wait_all) {  // KR_BOUNDARY_WAIT_ALL=1 (debug A/B): the round-2 edge set
+          for (auto& t : shards)
+            if (t.ext_in) KR_HIP_CHECK(hipStreamWaitEvent(s.stream, t.ev_out, 0));
+        } else {
+          for (int t : s.ext_readers)
+            KR_HIP_CHECK(hipStreamWaitEvent(s.stream, shards[(size_t)t].ev_out, 0));
+        }
+        launch_boundary(s);
+        bytes += bytes_of(s);
+      }
+      Shard& s0 = shards[(size_t)grp[0]];
+      KR_HIP_CHECK(hipSetDevice(s0.dev));
+      prof_end(s0, nm, t0s[(size_t)grp[0]], bytes);
+    });
+    return;
+  }
+  // With a communicator (one host thread): ev_in, the exchange on the comm
+  // stream(s) (RCCL), interior launches, then each boundary launch after the
+  // exchange.
+  for (size_t li = 0; li < shards.size(); ++li) phase_in(shards[li], li);
+  halo_async(in1, hx2, hx3);
+  for (auto& s : shards) {  // interior rows: all blocks write their partials
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    launch_full(s, s.int_lo, s.int_hi - s.int_lo);
+  }
+  for (size_t li = 0; li < shards.size(); ++li) {
+    Shard& s = shards[li];
+    KR_HIP_CHECK(hipSetDevice(s.dev));
+    if (!hybrid()) {
+      KR_HIP_CHECK(hipStreamWaitEvent(s.stream, s.ev_out, 0));
+    } else {
+      // own halo copied, and every reader done with this shard's rows
+      for (auto& t : shards) KR_HIP_CHECK(hipStreamWaitEvent(s.stream, t.ev_out, 0));
+      KR_HIP_CHECK(hipStreamWaitEvent(s.stream, hy_ev, 0));  // RCCL pieces
+    }
+    launch_boundary(s);
+    prof_end(s, nm, t0s[li], bytes_of(s));
+  }
 }
 
 void System::ew(EwOp op, double c0, double c1, std::array<int, 6> ids, int slot0) {
@@ -1814,8 +1919,7 @@ void System::ew_n(EwOp op, double c0, double c1, const std::array<int, kEwOps>& 
 }
 
 bool System::device_scalars() const {
-  const char* env = getenv("KR_DEVICE_SCALARS");  // 0: one host sync per reduction (A/B)
-  if (env && atoi(env) == 0) return false;
+  if (KR_ENV("KR_DEVICE_SCALARS", 1) == 0) return false;  // one host sync per reduction (A/B)
   // one shard per RCCL rank, or any number of shards in one process
   return comm ? !hybrid() : true;
 }
@@ -1933,14 +2037,12 @@ void System::scalar(ScalarOp op, int need, int64_t it, int h, double thr, int ch
 }
 
 bool System::fused_scalars() const {
-  const char* env = getenv("KR_FUSE_SCALAR");
-  if (env && atoi(env) == 0) return false;
+  if (KR_ENV("KR_FUSE_SCALAR", 1) == 0) return false;
   return !comm && shards.size() == 1;
 }
 
 bool System::vp_ok() const {
-  const char* env = getenv("KR_CG_VP");
-  if (env && atoi(env) == 0) return false;
+  if (KR_ENV("KR_CG_VP", 1) == 0) return false;
   if (!fused_scalars()) return false;
   const Shard& s = shards[0];
   if (s.dense || s.n == 0) return false;

@@ -110,6 +110,12 @@ struct Shard {
   int spmv_grid = 1;            // workgroups of the SpMV kernels
   int spmv_grid_po = 1;         // ... of a products-only stencil launch (<= spmv_grid)
   std::vector<int> readers;     // in-process: local shards that copy halo rows from this one
+  // ... of them, the ones on another stream (their comm streams copy; the
+  // others share this shard's stream, System::groups); ext_in: this shard
+  // receives halo pieces from a shard on another stream
+  std::vector<int> ext_readers;
+  bool ext_in = false;
+  bool lead = true;             // first shard of its stream group
   int spmv_grid2 = 1;           // ... of the fused basis pair (System::spmv_pair, <= spmv_grid)
   int pstride = 1;              // partial stride per slot: max(grid, spmv_grid)
   std::array<int, kMaxSlots> slot_n{};  // partials written per slot by its last producer
@@ -230,10 +236,18 @@ struct System {
   bool products_only = false;
   bool products_only_on = true;
   std::unique_ptr<Session> session;
-  // per-shard host threads (in-process multi-shard, KR_HOST_THREADS != 0)
+  // Stream groups: the local shards sharing one stream (in-process shards of
+  // one device, kr_system_create), in shard order; a shard per group when
+  // every shard has its own stream. Work of one group is enqueued by one
+  // host thread in shard order.
+  std::vector<std::vector<int>> groups;
+  // host threads, one per further stream group (in-process, KR_HOST_THREADS != 0)
   std::unique_ptr<ShardPool> pool;
-  // fn(shard, li) for every local shard: on the pool when there is one, else
-  // in order on this thread (each fn sets its shard's device)
+  // fn(group) for every stream group: on the pool when there is one, else in
+  // order on this thread
+  void for_groups(const std::function<void(const std::vector<int>&)>& fn);
+  // fn(shard, li) for every local shard, group by group (each fn sets its
+  // shard's device)
   void for_shards(const std::function<void(Shard&, size_t)>& fn);
 
   ~System();
@@ -251,6 +265,7 @@ struct System {
   // signalling ev_out (overlapped path).
   void halo_async(int id1, int id2, int id3 = -1);
   void halo_in_process(Shard& s, int id1, int id2, int id3);
+  void halo_group(const std::vector<int>& grp, int id1, int id2, int id3);
   void spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int b, int slot0,
             const StepOps* st = nullptr);
   // Two chained EPI_DUAL_MRR basis SpMVs in one launch (spmv_stencil2_kernel):

@@ -6,6 +6,7 @@
 
 #include <atomic>
 #include <cstdint>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -52,6 +53,31 @@ inline void opt_in_lds(std::atomic<uint64_t>& done, const void* fn, size_t lds) 
   KR_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   done.fetch_or(bit, std::memory_order_acq_rel);
 }
+
+// Environment knobs (KR_* A/B switches) on the launch path, read through a
+// cache: the hot path reads several per kernel launch, and getenv walks the
+// whole environment each time. A cached value is refreshed once g_env_epoch
+// moved, which every C-ABI entry point except kr_solve_step does -- so a
+// knob changed between two calls (as the tests do) takes effect at the next
+// call, and one solve's steps see the values of its kr_solve_begin.
+extern std::atomic<uint64_t> g_env_epoch;
+// cache word: (epoch + 1) << 33 | set << 32 | uint32 value; 0 = empty
+inline int env_cached(std::atomic<uint64_t>& cache, const char* name, int dflt) {
+  const uint64_t ep = g_env_epoch.load(std::memory_order_relaxed) + 1;
+  const uint64_t c = cache.load(std::memory_order_relaxed);
+  if ((c >> 33) == ep) return ((c >> 32) & 1) ? (int)(uint32_t)c : dflt;
+  const char* e = getenv(name);
+  const int v = e ? atoi(e) : 0;
+  cache.store((ep << 33) | ((uint64_t)(e != nullptr) << 32) | (uint32_t)v,
+              std::memory_order_relaxed);
+  return e ? v : dflt;
+}
+// KR_ENV("KR_X", d): the knob's integer value, d when unset (one cache per use)
+#define KR_ENV(name, dflt)                                     \
+  ([]() -> int {                                               \
+    static std::atomic<uint64_t> kr_env_cache_{0};             \
+    return ::kr::env_cached(kr_env_cache_, (name), (dflt));    \
+  }())
 
 // KR_POISON_ALLOC=1 (debug): every device buffer the engine allocates starts
 // as all-ones bytes (a NaN in every double) instead of zeros or whatever
@@ -392,7 +418,9 @@ void launch_finalize_counts(const double* partials, int stride, const SlotCounts
 // Halo rows of in-process shards on one device: every (src, dst, count)
 // piece of one shard's receive list (all vectors) in ONE launch instead of a
 // hipMemcpyAsync per piece (2.4 us of host time each; a launch is 2.5).
-constexpr int kHaloPieces = 12;
+// pieces per gather launch: a stream group of 8 shards, 2 neighbours each,
+// 3 vectors (the fused first k-skip MrR steps)
+constexpr int kHaloPieces = 48;
 struct HaloGatherArgs {
   const double* src[kHaloPieces];
   double* dst[kHaloPieces];

@@ -458,8 +458,7 @@ void ew_dispatch_op(const EwArgs& a, hipStream_t s) {
       aligned = false;
   // KR_EW_VARIANT (A/B only): 0 = 1 pair/thread/iteration, 1 = 2 pairs,
   // 2 = 2 pairs + non-temporal stores.
-  const char* env = getenv("KR_EW_VARIANT");
-  const int variant = env ? atoi(env) : 0;
+  const int variant = KR_ENV("KR_EW_VARIANT", 0);
   if (!aligned)
     ew_kernel<OP, false><<<a.grid, kBlock, 0, s>>>(a);
   else if (variant == 1)

@@ -2173,8 +2173,7 @@ bool use_dia(const SpmvArgs& a) {
   const bool vec = ((reinterpret_cast<uintptr_t>(a.val) | reinterpret_cast<uintptr_t>(a.col)) &
                     15) == 0;
   if (!vec || a.nnz_total < 4) return true;
-  const char* env = getenv("KR_DIA_ALL");
-  return env && atoi(env) == 1;
+  return KR_ENV("KR_DIA_ALL", 0) == 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -2264,10 +2263,10 @@ void spmv_dispatch_epi(const SpmvArgs& a, int nblocks, hipStream_t s) {
   // overrides for A/B runs: 0 row walk v1, 8 product-then-sum v1, 10 row
   // walk v2 with plain loads, 12 row walk v2 single-buffered, 15
   // product-then-sum v2 with plain loads.
-  const char* env = getenv("KR_SPMV_VARIANT");
+  const int forced = KR_ENV("KR_SPMV_VARIANT", -1);
   // Two-vector long-row SpMVs stay on v1: v2's extra gather registers cost a
   // wave per SIMD there (144 VGPRs) and it measured 7 % slower (C5 dual).
-  int variant = env ? atoi(env) : (a.long_rows ? (EpiTraits<E>::NV == 1 ? 14 : 8) : 13);
+  int variant = forced >= 0 ? forced : (a.long_rows ? (EpiTraits<E>::NV == 1 ? 14 : 8) : 13);
   // the v2 kernels need 16-byte aligned bases and >= 4 entries
   if (variant >= 10 && (!VEC || a.nnz_total < 4)) variant = a.long_rows ? 8 : 0;
   if constexpr (is_virtual<E>()) {  // implemented by the row walk v2 only

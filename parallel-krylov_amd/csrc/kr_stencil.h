@@ -674,8 +674,7 @@ void spmv_stencil_kernel_po(SpmvArgs a) {
 
 // KR_STENCIL_DEPTH=2 (A/B): the dual SpMVs load two visits ahead.
 inline int st_depth() {
-  const char* e = getenv("KR_STENCIL_DEPTH");
-  return e ? atoi(e) : 1;
+  return KR_ENV("KR_STENCIL_DEPTH", 1);
 }
 // The DPP neighbour path (NTM bit 5) for 7-point shards whose NEAR slots are
 // -1 and +1. Measured on C4 (one box, A/B): the products-only dual 0.645 ->
@@ -684,8 +683,7 @@ inline int st_depth() {
 // KR_STENCIL_DPP = 1 (default): products-only launches only; 2: every
 // 7-point launch; 0: none (A/B).
 inline bool st_dpp(const SpmvArgs& a, bool products_only) {
-  const char* e = getenv("KR_STENCIL_DPP");  // read per launch: tests switch it
-  const int v = e ? atoi(e) : 1;
+  const int v = KR_ENV("KR_STENCIL_DPP", 1);
   return (v == 2 || (v == 1 && products_only)) && a.st_off[2] == -1 && a.st_off[4] == 1;
 }
 
@@ -701,8 +699,7 @@ inline bool st_pair(const SpmvArgs& a, int nblocks) {
   if constexpr (E == EPI_XY_VP || E == EPI_MRR_V) {
     return false;
   } else {
-    const char* e = getenv("KR_STENCIL_PAIR");  // read per launch: tests switch it
-    const int m = e ? atoi(e) : 0;
+    const int m = KR_ENV("KR_STENCIL_PAIR", 0);
     constexpr bool dual = E == EPI_DUAL_MRR || E == EPI_DUAL_KCG || E == EPI_DUAL_NONE;
     const int bit = (dual && a.products_only) ? 1
                     : dual                        ? 2
@@ -753,10 +750,8 @@ void spmv_stencil_launch_r(const SpmvArgs& a, int nblocks, hipStream_t s) {
   // L2 (C4 +4-7 %). KR_STENCIL_NT=0..2 (A/B; 7-point pattern, 8-bit codes).
   // KR_STENCIL_LDS (A/B): extra LDS per workgroup, i.e. fewer resident
   // workgroups per CU.
-  const char* env = getenv("KR_STENCIL_NT");
-  const int ntm = env ? atoi(env) : 3;
-  const char* lenv = getenv("KR_STENCIL_LDS");
-  const size_t lds = lenv ? (size_t)atoi(lenv) : 0;
+  const int ntm = KR_ENV("KR_STENCIL_NT", 3);
+  const size_t lds = (size_t)KR_ENV("KR_STENCIL_LDS", 0);
   if constexpr (E == EPI_DUAL_MRR || E == EPI_DUAL_KCG) {
     // products only (SpmvArgs::products_only): NTM bit 2 drops the y1/y2
     // stores (the last basis pair of a k-skip outer iteration feeds only the

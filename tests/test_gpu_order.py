@@ -171,6 +171,34 @@ def test_gpu_bitwise_equals_gpu_order_oracle(monkeypatch, case):
         assert (np.nonzero(np.diff(info["khistory"]))[0] + 1).tolist() == changes
 
 
+STREAM_CASES = [c for c in CASES if c[3] > 1]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shared", ["0", "2"])
+@pytest.mark.parametrize("case", STREAM_CASES, ids=[IDS[CASES.index(c)] for c in STREAM_CASES])
+def test_stream_groups_bitwise_gpu_order(monkeypatch, case, shared):
+    """Stream groups (kr_system_create, System::groups): by default the
+    in-process shards of one device share its stream (the group's halo pieces
+    in one gather launch, stream order as the only edge); KR_SHARED_STREAM=0
+    gives each shard its own stream (pieces on the comm streams, event edges),
+    2 groups the shards in pairs -- on one device, the mixed geometry several
+    devices with several shards each would have (gather within a pair, comm
+    streams and events between pairs). Every layout is bitwise the same
+    GPU-order oracle: streams change the issue, not the arithmetic."""
+    method, spec, k, shards, changes = case
+    A = golden_matrix(spec)
+    b = _rhs(A.shape[0])
+    sc = _engine_scheds(A, shards)
+    monkeypatch.setenv("KRYLOV_AMD_SHARDS", ",".join(["0"] * shards))
+    monkeypatch.setenv("KR_SHARED_STREAM", shared)
+    kw = dict(tol=1e-10, k=k)
+    with contextlib.redirect_stdout(io.StringIO()):
+        x, info = _solver(method)(A, b, **kw)
+    x_ref, info_ref = gpu_order.run(method, A, b, sc, **kw)
+    _assert_bitwise(x, info, x_ref, info_ref)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("maxiter", [40, 66, 67, 80, 92])
 def test_gpu_rollback_bookkeeping_under_maxiter(maxiter):
