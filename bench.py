@@ -237,8 +237,13 @@ def stored_format_delta(nnz, n, lay, long_row=12.0):
     dictionary the 8-byte values by 1-byte codes; long masked rows use the
     diagonal-offset values (8 bytes per offset and row, no rowptr); the
     stencil SpMV streams code_bits bytes of codes per row (8 slots of
-    code_bits bits) and nothing else of A."""
+    code_bits bits) and nothing else of A -- or, with code patterns, one
+    4-byte pattern id per 512-row block plus the pattern table once."""
     if lay.get("stencil_walk"):
+        if lay.get("code_patterns"):
+            cb = float(lay.get("code_bits") or 8)
+            a_bytes = 4.0 * -(-n // 512) + lay["code_patterns"] * 512 * cb
+            return 12.0 * nnz + 4.0 * (n + 1) - a_bytes
         return 12.0 * nnz + 4.0 * (n + 1) - float(lay.get("code_bits") or 8) * n
     mw = lay["mask_bits"]
     if mw and lay["dict_values"] == 0 and nnz >= long_row * n:  # DIA (KR_DIA=1)
@@ -258,7 +263,9 @@ def stored_format_delta(nnz, n, lay, long_row=12.0):
 def format_name(lay):
     if lay.get("stencil_walk"):
         cb = lay.get("code_bits") or 8
-        return (f"stencil codes (8 x {cb}-bit dictionary codes per row, "
+        codes = (f"{lay['code_patterns']} distinct 512-row code blocks, a 4-byte pattern id per "
+                 f"block" if lay.get("code_patterns") else "per row")
+        return (f"stencil codes (8 x {cb}-bit dictionary codes per row, {codes}; "
                 f"{lay['dict_values']}-entry table; walk {lay['stencil_walk']} blocks)")
     if lay.get("dia_sym"):
         return (f"diagonal-offset values, {lay['n_offsets']} offsets, symmetric (upper half + "

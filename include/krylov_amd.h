@@ -56,8 +56,9 @@ extern "C" {
  *   200  kr_solve_params gained nan_guard and kr_solve_result diverged (both
  *        structs changed size); maxiter = 0 is honoured instead of meaning
  *        the default (CG / k-skip CG return r0, the MrR family is refused).
- *   201  kr_solve_set_precond_ilu added (no struct or behaviour change). */
-#define KR_ABI_VERSION 201
+ *   201  kr_solve_set_precond_ilu added (no struct or behaviour change).
+ *   202  kr_system_shard_code_patterns added (no struct or behaviour change). */
+#define KR_ABI_VERSION 202
 int kr_version(void);
 const char* kr_last_error(void);
 /* Number of HIP devices visible to this process (0 when none). */
@@ -254,6 +255,14 @@ int kr_system_shard_values(kr_system* sys, int shard, int* dict_values);
  * values on the 7-point pattern), i.e. the bytes of A one row streams.
  * Replaces nothing in the reference (cuSPARSE csrmv streams CSR). */
 int kr_system_shard_codes(kr_system* sys, int shard, int* code_bits);
+/* Stencil code patterns of shard s (after finalize): 0 when the stencil
+ * SpMV streams its codes per row, else the number (<= 256) of distinct
+ * 512-row code blocks; each is stored once and every row block holds one
+ * 4-byte pattern id, so the walk reads its codes from that small table (L2)
+ * instead of code_bits bytes per row (a constant-coefficient stencil on a
+ * box: 9 blocks at 512^3). Lossless, compared byte for byte at finalize;
+ * KR_STENCIL_PATTERNS=0 disables. Replaces nothing in the reference. */
+int kr_system_shard_code_patterns(kr_system* sys, int shard, int* patterns);
 /* Symmetric diagonal-offset values of shard s (after finalize): 1 when the
  * shard's offsets and stored values are symmetric (checked bitwise at
  * finalize) and the DIA SpMV reads each lower entry as the mirrored upper

@@ -677,6 +677,15 @@ int kr_system_shard_codes(kr_system* sys, int shard, int* code_bits) {
   });
 }
 
+int kr_system_shard_code_patterns(kr_system* sys, int shard, int* patterns) {
+  return guarded([&] {
+    KR_REQUIRE(sys && shard >= 0 && shard < (int)sys->shards.size(), "bad shard");
+    KR_REQUIRE(sys->finalized, "system not finalized");
+    const Shard& s = sys->shards[shard];
+    if (patterns) *patterns = s.scode && s.st_pid ? s.st_npat : 0;
+  });
+}
+
 int kr_system_shard_dia_sym(kr_system* sys, int shard, int* sym) {
   return guarded([&] {
     KR_REQUIRE(sys && shard >= 0 && shard < (int)sys->shards.size(), "bad shard");

@@ -104,6 +104,10 @@ struct Shard {
   double* scratch = nullptr;        // SpmvArgs::scratch (stencil SpMV), owned
   int st_P = 0, st_nfar = 0;
   int32_t st_kind[8] = {}, st_far[4] = {};
+  // code patterns (SpmvArgs::st_pid / st_pat, System::build_code_patterns), owned
+  uint32_t* st_pid = nullptr;
+  void* st_pat = nullptr;
+  int st_npat = 0;
   hipStream_t comm_stream = nullptr;  // halo exchange, overlapped with interior rows
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   int grid = 1;                 // workgroups of the vector kernels
@@ -259,6 +263,7 @@ struct System {
   void build_masks(Shard& s);
   void build_vdict(Shard& s);
   void build_stencil(Shard& s);
+  void build_code_patterns(Shard& s);
   void plan_window(Shard& s, const std::vector<int32_t>& M);
   void halo(int id1, int id2 = -1, int id3 = -1);
   // The same exchange on the shards' comm streams, ordered after ev_in and

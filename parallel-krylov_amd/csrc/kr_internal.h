@@ -233,6 +233,15 @@ struct SpmvArgs {
   // values), so a row streams st_cb bytes of A.
   const void* scode = nullptr;
   int st_cb = 8;
+  // Code patterns (optional, with scode): the codes of row block b (512 rows,
+  // 512 * st_cb bytes) are pattern st_pid[b] of the table st_pat (st_npat
+  // patterns, row blocks past n zero-padded) -- a constant-coefficient
+  // stencil on a box has a handful of distinct blocks (interior, faces,
+  // edges), so the walk reads its codes from L2 instead of streaming st_cb
+  // bytes per row. Same codes, same arithmetic. scode stays valid.
+  const uint32_t* st_pid = nullptr;
+  const void* st_pat = nullptr;
+  int st_npat = 0;
   int st_P = 0, st_nm = 0, st_nfar = 0;
   // 1: position-major walk (st_P % 8 == 0): XCD q takes positions
   // [q P/8, (q+1) P/8) of every plane segment; grid = P x segments.

@@ -112,14 +112,18 @@ struct SRes {
 };
 
 template <int NX, int CB>
-__device__ __forceinline__ SRes st_res(const SpmvArgs& a, const double* const (&xs)[3]) {
+__device__ __forceinline__ SRes st_res(const SpmvArgs& a, const double* const (&xs)[3],
+                                       bool pat = false) {
   SRes r;
 #pragma unroll
   for (int v = 0; v < NX; ++v)
     r.x[v] = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(xs[v]), 0,
                                                (int)(a.xlen * 8), 0x00020000);
-  r.code = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.scode), 0, (int)(a.n * CB),
-                                             0x00020000);
+  // codes: the pattern table (SpmvArgs::st_pid) or the per-row stream
+  r.code = pat ? __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.st_pat), 0,
+                                                   a.st_npat * kStencilBlock * CB, 0x00020000)
+               : __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.scode), 0,
+                                                   (int)(a.n * CB), 0x00020000);
   return r;
 }
 
@@ -129,35 +133,41 @@ __device__ __forceinline__ dbl2v st_bld2(__amdgpu_buffer_rsrc_t r, uint32_t off)
   return __builtin_bit_cast(dbl2v, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX));
 }
 
+// Codes of rows 2t, 2t+1 at byte cbase + 2 CB t of the code buffer (lanes
+// past the last row read 0: inactive). AUX 2: non-temporal (the per-row
+// stream is read once); a pattern table is re-read by every block (AUX 0).
+template <int CB, int AUX, typename Code>
+__device__ __forceinline__ void st_codes(Code& clo, Code& chi, __amdgpu_buffer_rsrc_t r,
+                                         uint32_t coff) {
+  if constexpr (CB == 8) {
+    typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+    const u64x2 c = __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(r, coff, 0, AUX));
+    clo = c.x;
+    chi = c.y;
+  } else if constexpr (CB == 4) {
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    const u32x2 c = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(r, coff, 0, AUX));
+    clo = c.x;
+    chi = c.y;
+  } else {  // CB == 2: both rows' uint16 codes in one dword
+    const uint32_t c = __builtin_amdgcn_raw_buffer_load_b32(r, coff, 0, AUX);
+    clo = c & 0xFFFFu;
+    chi = c >> 16;
+  }
+}
+
 // row0: the visit's first row (launch-relative, uniform); the lane's rows are
 // row0 + 2 tid, row0 + 2 tid + 1 (may lie past the last own row: x loads use
 // them as is -- rows past the own rows are halo rows, which the +-1
 // neighbours of the last own rows need); rr: the lane's first row clamped to
-// the own rows (own-row operands).
+// the own rows (own-row operands); cbase: byte offset of the block's codes
+// (row0 * CB in the row stream, or its pattern's in the table: pat).
 template <int EPI, bool RELOAD, int NTM, int NX, int NFAR, int CB>
 __device__ __forceinline__ void st_issue(SStage<NX, NFAR, CB>& st, const SpmvArgs& a,
-                                         const SRes& res, int64_t row0, int tid, int64_t rr) {
+                                         const SRes& res, int64_t row0, int tid, int64_t rr,
+                                         uint32_t cbase, bool pat) {
   using T = EpiTraits<EPI>;
   constexpr int kCodeAux = (NTM & 1) ? 2 : 0;  // codes: streamed once (non-temporal)
-  // codes of rows 2t, 2t+1 (lanes past the last row read 0: inactive)
-  const uint32_t coff = (uint32_t)(row0 * CB) + (uint32_t)tid * (2 * CB);
-  if constexpr (CB == 8) {
-    typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-    const u64x2 c = __builtin_bit_cast(
-        u64x2, __builtin_amdgcn_raw_buffer_load_b128(res.code, coff, 0, kCodeAux));
-    st.clo = c.x;
-    st.chi = c.y;
-  } else if constexpr (CB == 4) {
-    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-    const u32x2 c = __builtin_bit_cast(
-        u32x2, __builtin_amdgcn_raw_buffer_load_b64(res.code, coff, 0, kCodeAux));
-    st.clo = c.x;
-    st.chi = c.y;
-  } else {  // CB == 2: both rows' uint16 codes in one dword
-    const uint32_t c = __builtin_amdgcn_raw_buffer_load_b32(res.code, coff, 0, kCodeAux);
-    st.clo = c & 0xFFFFu;
-    st.chi = c >> 16;
-  }
   // x offsets: uniform (xoff + row0 + o) * 8, plus 16 bytes per lane
   const int64_t ub = (a.xoff + row0) * 8;
   const uint32_t lb = (uint32_t)tid * 16u;
@@ -186,6 +196,13 @@ __device__ __forceinline__ void st_issue(SStage<NX, NFAR, CB>& st, const SpmvArg
       st.prv[v] = st_bld2(res.x[v], (uint32_t)(ub - W * 8) + lb);
     }
   }
+  // the codes last: with patterns (pat) the block's pattern id comes through
+  // the scalar cache, and the wait for it then holds back no vector load
+  const uint32_t coff = cbase + (uint32_t)tid * (2 * CB);
+  if (pat)  // uniform; one code load on either path
+    st_codes<CB, 0>(st.clo, st.chi, res.code, coff);
+  else
+    st_codes<CB, kCodeAux>(st.clo, st.chi, res.code, coff);
 }
 
 // The line's edge pairs (uniform: scalar loads, counted by lgkmcnt). Issued
@@ -349,12 +366,20 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
   constexpr bool DPP = (NTM & 32) && PAT == kPat7;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   SStage<NX, NFAR, CB> sA, sB, sC;
-  const SRes res = st_res<NX, CB>(a, xs);
+  // Code patterns (SpmvArgs::st_pid; carried walks with one visit of
+  // prefetch): the pattern id of the block the NEXT issue loads is fetched
+  // through the scalar cache one visit ahead, after the visit's barrier with
+  // the edge pairs (pid_n), so no issue waits on it.
+  const bool pat = !RELOAD && DEPTH == 1 && a.st_pid != nullptr;
+  const SRes res = st_res<NX, CB>(a, xs, pat);
+  uint32_t pid_n = 0;
+  auto pid_of = [&](int64_t z) -> uint32_t { return load_uniform(a.st_pid, phys(blk(z))); };
   int buf = 0;
-  auto issue = [&](SStage<NX, NFAR, CB>& st, int64_t z) {
+  auto issue = [&](SStage<NX, NFAR, CB>& st, int64_t z, uint32_t pid) {
     const int64_t row0 = phys(blk(z)) * kSBlock;
     const int64_t rl = row0 + 2 * tid;
-    st_issue<EPI, RELOAD, NTM>(st, a, res, row0, tid, rl < a.n ? rl : a.n - 2);
+    const uint32_t cbase = pat ? pid * (uint32_t)(kSBlock * CB) : (uint32_t)(row0 * CB);
+    st_issue<EPI, RELOAD, NTM>(st, a, res, row0, tid, rl < a.n ? rl : a.n - 2, cbase, pat);
   };
   auto issue_edges = [&](SStage<NX, NFAR, CB>& st, int64_t z) {
     if constexpr (DPP)
@@ -390,7 +415,7 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
     // unconditionally (the last visit re-reads its own rows): a load under a
     // branch makes the compiler's wait counts assume the shorter path.
     const int64_t zn = visit_ok(z + DEPTH) ? z + DEPTH : z;
-    issue(nxs, zn);
+    issue(nxs, zn, pid_n);
     // (2) operand values at the rows: centers, the previous plane's centers
     dbl2v opc[NV], opp[NV];
     if constexpr (VIRT) {
@@ -426,6 +451,7 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
         xp2[v] = st_dpp_shl1(opc[v].x, er[v]);
       }
       issue_edges(nxs, zn);
+      if (pat) pid_n = pid_of(visit_ok(zn + 1) ? zn + 1 : zn);
     } else {
 #pragma unroll
       for (int v = 0; v < NV; ++v)
@@ -444,6 +470,7 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
       }
       __syncthreads();
       issue_edges(nxs, zn);
+      if (pat) pid_n = pid_of(visit_ok(zn + 1) ? zn + 1 : zn);
     }
     // (4) the two rows' sums, slot by slot in ascending offset order. A
     // visit whose rows (every lane of the wave) have all nm slots present --
@@ -595,11 +622,12 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
 
   int64_t z = RELOAD ? 0 : z0;
   if (visit_ok(z)) {
-    issue(sA, z);
+    issue(sA, z, pat ? pid_of(z) : 0u);
     issue_edges(sA, z);
+    if (pat) pid_n = pid_of(visit_ok(z + 1) ? z + 1 : z);
     if constexpr (DEPTH == 2) {
       const int64_t z1n = visit_ok(z + 1) ? z + 1 : z;
-      issue(sB, z1n);
+      issue(sB, z1n, 0u);
       issue_edges(sB, z1n);
     }
     if constexpr (!RELOAD) {  // CENTER and PREV of the segment's first visit

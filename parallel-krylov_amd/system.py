@@ -297,20 +297,23 @@ class KrylovSystem:
         """SpMV storage of shard s: mask_bits (0 = CSR columns), n_offsets,
         interior row range [interior_lo, interior_hi), dict_values (0 = 8-byte
         values, else the size of the value dictionary), code_bits (stencil
-        SpMV: bits per slot code = bytes of A per row; 0 otherwise), dia_sym
+        SpMV: bits per slot code = bytes of A per row; 0 otherwise),
+        code_patterns (stencil SpMV: distinct 512-row code blocks read from a
+        table instead of the per-row stream; 0 = per-row stream), dia_sym
         (1: symmetric diagonal-offset values, lower entries read as the
         mirrored upper ones)."""
         mb, no = ctypes.c_int(), ctypes.c_int()
         lo, hi = ctypes.c_int64(), ctypes.c_int64()
         call("kr_system_shard_layout", self.handle, s, ctypes.byref(mb), ctypes.byref(no),
              ctypes.byref(lo), ctypes.byref(hi))
-        dv, cb, ds = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        dv, cb, ds, cp = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         call("kr_system_shard_values", self.handle, s, ctypes.byref(dv))
         call("kr_system_shard_codes", self.handle, s, ctypes.byref(cb))
+        call("kr_system_shard_code_patterns", self.handle, s, ctypes.byref(cp))
         call("kr_system_shard_dia_sym", self.handle, s, ctypes.byref(ds))
         return dict(mask_bits=mb.value, n_offsets=no.value, interior_lo=lo.value,
                     interior_hi=hi.value, dict_values=dv.value, code_bits=cb.value,
-                    dia_sym=ds.value)
+                    code_patterns=cp.value, dia_sym=ds.value)
 
     def shard_sched(self, s: int) -> dict:
         """Launch geometry of shard s: elementwise and SpMV grids plus the

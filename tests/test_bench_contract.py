@@ -120,6 +120,11 @@ def test_stored_format_bytes():
     st2 = dict(st, code_bits=2)
     assert bench.stored_format_delta(nnz, n, st2) == 12.0 * nnz + 4.0 * (n + 1) - 2.0 * n
     assert "2-bit" in bench.format_name(st2)
+    # code patterns: a 4-byte pattern id per 512-row block + the table once
+    stp = dict(st2, code_patterns=9)
+    assert bench.stored_format_delta(nnz, n, stp) == (
+        12.0 * nnz + 4.0 * (n + 1) - (4.0 * 2 + 9 * 512 * 2.0))
+    assert "9 distinct 512-row code blocks" in bench.format_name(stp)
 
 
 def test_step_roofline_survey_figures():

@@ -215,6 +215,46 @@ def test_stencil_code_width_bitwise_scipy(monkeypatch, name, want):
         np.testing.assert_array_equal(y, A @ x)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["p3d32", "p3d64", "box64x64x20", "box48x32x5", "p2d512x6",
+                                  "vals15_64x64x9", "random_codes"])
+def test_stencil_code_patterns_bitwise_scipy(monkeypatch, name):
+    """Code patterns (System::build_code_patterns): a constant-coefficient
+    box stencil has a handful of distinct 512-row code blocks, which the walk
+    reads from a table instead of the per-row code stream; random values give
+    one pattern per block (a 3-value dictionary over 320 blocks: more than
+    the 256-pattern cap, so the row stream stays). y = A x is bitwise scipy's
+    either way, on 1 and 3 shards, and equals the row-stream result
+    (KR_STENCIL_PATTERNS=0)."""
+    A = revalued(box(64, 64, 40), 3) if name == "random_codes" else MATRICES[name]()
+    n = A.shape[0]
+    x = np.random.default_rng(11).standard_normal(n)
+    for shards in (1, 3):
+        sysm = _system(A, shards)
+        lay = [sysm.shard_layout(s) for s in range(shards)]
+        walks = [sysm.shard_sched(s)["stencil_walk"] for s in range(shards)]
+        y = sysm.gather(sysm.spmv(sysm.split(x))).cpu().numpy()
+        sysm.close()
+        np.testing.assert_array_equal(y, A @ x)
+        for lo, w in zip(lay, walks):
+            if not w:
+                assert lo["code_patterns"] == 0
+            elif name == "random_codes":  # one pattern per block: 320 > 256 on one shard
+                if shards == 1:
+                    assert lo["code_patterns"] == 0
+                else:  # ~107 blocks per shard, all distinct
+                    assert lo["code_patterns"] > 100
+            elif name.startswith("vals"):
+                assert lo["code_patterns"] > 16  # random values: ~one per block
+            else:
+                assert 1 <= lo["code_patterns"] <= 16
+    sysm = _system(A, 1, {"KR_STENCIL_PATTERNS": "0"}, monkeypatch)
+    assert sysm.shard_layout(0)["code_patterns"] == 0
+    y0 = sysm.gather(sysm.spmv(sysm.split(x))).cpu().numpy()
+    sysm.close()
+    np.testing.assert_array_equal(y0, A @ x)
+
+
 def _solver(method):
     mod = importlib.import_module(f"parallel_krylov_amd.v3.gpu.{method}")
     return getattr(mod, method)
