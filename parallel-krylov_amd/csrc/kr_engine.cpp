@@ -486,6 +486,20 @@ std::unique_ptr<IluFactors> build_ilu(int dev, hipStream_t stream, int64_t n, co
         inverse_perm(n, lo ? perm_r : perm_c, lo ? "perm_r" : "perm_c");
     a.perm = static_cast<const int32_t*>(up(inv.data(), 4 * inv.size()));
     f->nnz += (int64_t)scol.size();
+    // launches: runs of levels of <= KR_ILU_WIDE rows in one workgroup, each
+    // wider level over the grid (0: every level in the one workgroup)
+    const int64_t wide = KR_ENV("KR_ILU_WIDE", 4096);
+    std::vector<IluSeg>& segs = lo ? f->lseg : f->useg;
+    for (int64_t l = 0; l < a.nlev; ++l) {
+      const int64_t w = ptr[(size_t)l + 1] - ptr[(size_t)l];
+      if (wide > 0 && w > wide) {
+        segs.push_back({l, l + 1, w});
+      } else if (!segs.empty() && segs.back().rows == 0 && segs.back().lev1 == l) {
+        segs.back().lev1 = l + 1;
+      } else {
+        segs.push_back({l, l + 1, 0});
+      }
+    }
   }
   f->y = static_cast<double*>(up(nullptr, 8 * (size_t)n));
   f->z = static_cast<double*>(up(nullptr, 8 * (size_t)n));
@@ -599,8 +613,8 @@ void System::ilu_apply(const IluFactors& f, int in, int out) {
   hi.in = ilu->y;
   hi.x = ilu->z;
   hi.out = s.own(out);
-  launch_ilu_sweep(true, lo, s.stream);
-  launch_ilu_sweep(false, hi, s.stream);
+  launch_ilu_sweep(true, lo, ilu->lseg.data(), (int)ilu->lseg.size(), s.stream);
+  launch_ilu_sweep(false, hi, ilu->useg.data(), (int)ilu->useg.size(), s.stream);
   // values + columns + row pointers of both factors, the diagonals, and the
   // vectors: v, y (written, read), z (written), out
   prof_end(s, "ilu_sweeps", t0,

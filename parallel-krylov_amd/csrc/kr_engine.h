@@ -172,6 +172,7 @@ struct IluFactors {
   int dev = 0;
   int64_t n = 0, nnz = 0;           // nnz: strictly-triangular entries of L and U
   IluSweepArgs lower, upper;        // in / out / x pointers set per apply
+  std::vector<IluSeg> lseg, useg;   // their launches (launch_ilu_sweep)
   double* y = nullptr;              // L^-1 Pr v
   double* z = nullptr;              // U^-1 y
   std::vector<void*> owned;

@@ -558,6 +558,7 @@ void launch_cg_persist(const CgPersistArgs& a, int grid, hipStream_t s);
 // diag[i], also stored at out[perm[i]] (perm = the inverse column permutation).
 struct IluSweepArgs {
   int64_t nlev = 0;
+  int64_t lev0 = 0, lev1 = 0;  // the levels one launch sweeps
   const int64_t* lvl_ptr = nullptr;
   const int32_t* lvl_rows = nullptr;
   const int64_t* rp = nullptr;
@@ -569,7 +570,17 @@ struct IluSweepArgs {
   double* x = nullptr;
   double* out = nullptr;
 };
-void launch_ilu_sweep(bool lower, const IluSweepArgs& a, hipStream_t s);
+// A sweep as launches over its level segments: a run of narrow levels in
+// one workgroup (ilu_sweep_kernel), a wide level (more than KR_ILU_WIDE rows)
+// over the whole GPU in its own launch (ilu_level_kernel); the kernel
+// boundary orders the levels. Every row is computed by one thread with the
+// same arithmetic either way: the result does not depend on the split.
+struct IluSeg {
+  int64_t lev0 = 0, lev1 = 0;  // levels [lev0, lev1)
+  int64_t rows = 0;            // wide: the level's rows (0: a narrow run)
+};
+void launch_ilu_sweep(bool lower, const IluSweepArgs& a, const IluSeg* segs, int nseg,
+                      hipStream_t s);
 
 int default_grid(int64_t n);
 // Workgroups of the SpMV kernels for a block of n rows with column reach `reach` rows.

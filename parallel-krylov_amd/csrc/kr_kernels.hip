@@ -1605,40 +1605,69 @@ void launch_vdict_encode(const double* val, int64_t nnz, const unsigned long lon
 // parallel step; the levels run in ONE workgroup, separated by barriers: a
 // sweep is one launch with no inter-workgroup synchronisation (nothing to
 // time out), and the typical level holds tens of rows (a 256^2 Poisson spilu
-// has ~1000 levels of ~65 rows), which one workgroup covers. Row i: s = rhs,
+// has ~1000 levels of ~65 rows), which one workgroup covers. Levels wider
+// than KR_ILU_WIDE rows (a 3-D ILU(0) of 256^3: up to ~49,000) get a launch
+// of their own over the whole GPU instead (IluSeg). Row i: s = rhs,
 // s -= T[i][j] x[j] over the stored strictly-triangular entries in ascending
 // column order, x[i] = s / T[i][i].
 // ---------------------------------------------------------------------------
 namespace {
 constexpr int kIluThreads = 1024;
 
+// One row of a sweep (the entry t of the level lists).
+template <bool LOWER>
+__device__ __forceinline__ void ilu_row(const IluSweepArgs& a, int64_t t) {
+  const int32_t i = a.lvl_rows[t];
+  double s = LOWER ? a.in[a.perm[i]] : a.in[i];  // lower: (Pr v)[i] = v[prinv[i]]
+  const int64_t j1 = a.rp[i + 1];
+  for (int64_t jj = a.rp[i]; jj < j1; ++jj) s = s - a.val[jj] * a.x[a.col[jj]];
+  const double xi = s / a.diag[i];
+  a.x[i] = xi;
+  if (!LOWER) a.out[a.perm[i]] = xi;  // (Pc z)[j] = z[pc[j]]: out[pcinv[i]] = z[i]
+}
+
+// Levels [lev0, lev1) in one workgroup, a barrier between levels.
 template <bool LOWER>
 __global__ __launch_bounds__(kIluThreads) void ilu_sweep_kernel(IluSweepArgs a) {
   const int tid = threadIdx.x;
-  for (int64_t lev = 0; lev < a.nlev; ++lev) {
+  for (int64_t lev = a.lev0; lev < a.lev1; ++lev) {
     const int64_t beg = a.lvl_ptr[lev];  // uniform: scalar loads
     const int64_t end = a.lvl_ptr[lev + 1];
-    for (int64_t t = beg + tid; t < end; t += kIluThreads) {
-      const int32_t i = a.lvl_rows[t];
-      double s = LOWER ? a.in[a.perm[i]] : a.in[i];  // lower: (Pr v)[i] = v[prinv[i]]
-      const int64_t j1 = a.rp[i + 1];
-      for (int64_t jj = a.rp[i]; jj < j1; ++jj) s = s - a.val[jj] * a.x[a.col[jj]];
-      const double xi = s / a.diag[i];
-      a.x[i] = xi;
-      if (!LOWER) a.out[a.perm[i]] = xi;  // (Pc z)[j] = z[pc[j]]: out[pcinv[i]] = z[i]
-    }
+    for (int64_t t = beg + tid; t < end; t += kIluThreads) ilu_row<LOWER>(a, t);
     __syncthreads();  // this level's x visible to the next level's rows
   }
 }
+
+// One wide level over the grid: a row per thread.
+template <bool LOWER>
+__global__ __launch_bounds__(kBlock) void ilu_level_kernel(IluSweepArgs a) {
+  const int64_t t = a.lvl_ptr[a.lev0] + (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (t < a.lvl_ptr[a.lev0 + 1]) ilu_row<LOWER>(a, t);
+}
 }  // namespace
 
-void launch_ilu_sweep(bool lower, const IluSweepArgs& a, hipStream_t s) {
-  if (a.nlev <= 0) return;
-  if (lower)
-    ilu_sweep_kernel<true><<<1, kIluThreads, 0, s>>>(a);
-  else
-    ilu_sweep_kernel<false><<<1, kIluThreads, 0, s>>>(a);
-  KR_HIP_CHECK(hipGetLastError());
+void launch_ilu_sweep(bool lower, const IluSweepArgs& a, const IluSeg* segs, int nseg,
+                      hipStream_t s) {
+  for (int q = 0; q < nseg; ++q) {
+    IluSweepArgs b = a;
+    b.lev0 = segs[q].lev0;
+    b.lev1 = segs[q].lev1;
+    KR_REQUIRE(b.lev0 >= 0 && b.lev0 < b.lev1 && b.lev1 <= a.nlev, "ILU: bad level segment");
+    if (segs[q].rows > 0) {
+      KR_REQUIRE(b.lev1 == b.lev0 + 1, "ILU: a wide segment is one level");
+      const int64_t g = (segs[q].rows + kBlock - 1) / kBlock;
+      KR_REQUIRE(g < ((int64_t)1 << 31), "ILU: level too wide");
+      if (lower)
+        ilu_level_kernel<true><<<(unsigned)g, kBlock, 0, s>>>(b);
+      else
+        ilu_level_kernel<false><<<(unsigned)g, kBlock, 0, s>>>(b);
+    } else if (lower) {
+      ilu_sweep_kernel<true><<<1, kIluThreads, 0, s>>>(b);
+    } else {
+      ilu_sweep_kernel<false><<<1, kIluThreads, 0, s>>>(b);
+    }
+    KR_HIP_CHECK(hipGetLastError());
+  }
 }
 
 }  // namespace kr

@@ -317,6 +317,32 @@ def test_gpu_ilu_matches_oracle(monkeypatch, method, sysname, spec, drop_tol, sh
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("spec,drop_tol", [(("poisson", 32, 2), 1e-2), (("poisson", 10, 3), 1e-2),
+                                           (("banded", 2000, 13, 64, 0), 1e-4)])
+@pytest.mark.parametrize("method", ["pcg", "pipeline"])
+def test_gpu_ilu_wide_levels_bitwise(monkeypatch, method, spec, drop_tol):
+    """Wide levels get a launch of their own over the grid (IluSeg,
+    KR_ILU_WIDE rows): with the threshold at 4 rows nearly every level of
+    these small factors takes that path, and the solve is bitwise the one
+    with every level in the single workgroup (KR_ILU_WIDE=0) -- every row is
+    one thread's same arithmetic either way."""
+    import importlib
+    mod = importlib.import_module(f"parallel_krylov_amd.v1.threads.pipeline.{method}")
+    A = golden_matrix(spec)
+    b = np.random.default_rng(1).standard_normal(A.shape[0])
+    ilu = _spilu(A, drop_tol)
+    out = {}
+    for wide in ("0", "4"):
+        monkeypatch.setenv("KR_ILU_WIDE", wide)
+        with contextlib.redirect_stdout(io.StringIO()):
+            _, nosl, res, x, conv = getattr(mod, method)(A, b, ilu, 1e-10, return_x=True)
+        out[wide] = (nosl, res, x.cpu().numpy(), conv)
+    assert out["0"][3] and out["4"][3]
+    for q in range(3):
+        np.testing.assert_array_equal(out["4"][q], out["0"][q])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("method", METHODS)
 def test_gpu_ilu_against_superlu_solve(method):
     """The same solve against the oracle driven by SuperLU's own `solve` (the
@@ -354,3 +380,27 @@ def test_gpu_ilu_refused_on_several_shards():
             sysm.set_precond_ilu((ilu.L, ilu.U, ilu.perm_r, ilu.perm_c))
     finally:
         sysm.close()
+
+
+def test_ilu0_c2_tool_factors():
+    """tools/ilu_c2.py's ILU(0) of the 3-D Poisson matrix (the factors its
+    C2-size measurement feeds kr_solve_set_precond_ilu): L unit lower, U upper
+    with A's pattern, and L U equal to A on A's pattern (fill dropped)."""
+    import importlib.util
+    import os
+    import scipy.sparse as sp
+    from conftest import REPO
+    spec = importlib.util.spec_from_file_location("ilu_c2", os.path.join(REPO, "tools", "ilu_c2.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    n = 6
+    L, U, pr, pc = mod.ilu0_poisson3d(n)
+    A = golden_matrix(("poisson", n, 3))
+    assert np.array_equal(L.diagonal(), np.ones(n ** 3))
+    assert sp.triu(L, 1).nnz == 0 and sp.tril(U, -1).nnz == 0
+    assert (sp.tril(L, -1) != 0).sum() + (sp.triu(U) != 0).sum() == A.nnz
+    D = (L @ U - A).tocsr()
+    on = A.copy()
+    on.data[:] = 1.0
+    assert np.max(np.abs(D.multiply(on).data)) < 1e-14
+    assert np.array_equal(pr, np.arange(n ** 3)) and np.array_equal(pc, pr)
