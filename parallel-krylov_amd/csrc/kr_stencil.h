@@ -162,10 +162,13 @@ __device__ __forceinline__ void st_codes(Code& clo, Code& chi, __amdgpu_buffer_r
 // neighbours of the last own rows need); rr: the lane's first row clamped to
 // the own rows (own-row operands); cbase: byte offset of the block's codes
 // (row0 * CB in the row stream, or its pattern's in the table: pat).
+// LF (position pairs with the +-n lines from LDS, NTM bit 8): one FAR load,
+// the pair's outer neighbour line at row offset fo, into far[0].
 template <int EPI, bool RELOAD, int NTM, int NX, int NFAR, int CB>
 __device__ __forceinline__ void st_issue(SStage<NX, NFAR, CB>& st, const SpmvArgs& a,
                                          const SRes& res, int64_t row0, int tid, int64_t rr,
-                                         uint32_t cbase, bool pat) {
+                                         uint32_t cbase, bool pat, int64_t fo = 0) {
+  constexpr bool LF = (NTM & 256) && (NTM & 64) && !RELOAD;
   using T = EpiTraits<EPI>;
   constexpr int kCodeAux = (NTM & 1) ? 2 : 0;  // codes: streamed once (non-temporal)
   // x offsets: uniform (xoff + row0 + o) * 8, plus 16 bytes per lane
@@ -174,11 +177,16 @@ __device__ __forceinline__ void st_issue(SStage<NX, NFAR, CB>& st, const SpmvArg
   const int64_t W = (int64_t)a.st_P * kSBlock;
 #pragma unroll
   for (int v = 0; v < NX; ++v) st.nxt[v] = st_bld2(res.x[v], (uint32_t)(ub + W * 8) + lb);
+  if constexpr (LF) {
 #pragma unroll
-  for (int f = 0; f < NFAR; ++f)
+    for (int v = 0; v < NX; ++v) st.far[0][v] = st_bld2(res.x[v], (uint32_t)(ub + fo * 8) + lb);
+  } else {
 #pragma unroll
-    for (int v = 0; v < NX; ++v)
-      st.far[f][v] = st_bld2(res.x[v], (uint32_t)(ub + (int64_t)a.st_far[f] * 8) + lb);
+    for (int f = 0; f < NFAR; ++f)
+#pragma unroll
+      for (int v = 0; v < NX; ++v)
+        st.far[f][v] = st_bld2(res.x[v], (uint32_t)(ub + (int64_t)a.st_far[f] * 8) + lb);
+  }
   if constexpr (is_step<EPI>()) {
     st.u1 = *reinterpret_cast<const dbl2v*>(a.u1 + rr);
     st.u2 = *reinterpret_cast<const dbl2v*>(a.u2 + rr);
@@ -299,6 +307,11 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
   // same order and writes the same partials as an unpaired launch with twice
   // the grid (the host launches it only where both halves' walks agree).
   constexpr bool PAIRW = (NTM & 64) && !RELOAD;
+  // NTM bit 8 (with the pairs, the LDS line path, FAR offsets -+512 = the
+  // positions p -+ 1): the inner +-n line of each half is the other half's
+  // CENTER line, already in LDS after the visit's barrier -- only the outer
+  // one is loaded (half 0: -n, half 1: +n), half the FAR traffic
+  constexpr bool LFAR = PAIRW && (NTM & 256) && !(NTM & 32) && PAT == kPat7;
   const int half = PAIRW ? __builtin_amdgcn_readfirstlane(threadIdx.x / kBlock) : 0;
   const int tid = PAIRW ? (int)(threadIdx.x % kBlock) : (int)threadIdx.x;
   const int64_t pb = (!RELOAD && a.st_rev) ? (int64_t)gridDim.x - 1 - blockIdx.x : blockIdx.x;
@@ -379,7 +392,8 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
     const int64_t row0 = phys(blk(z)) * kSBlock;
     const int64_t rl = row0 + 2 * tid;
     const uint32_t cbase = pat ? pid * (uint32_t)(kSBlock * CB) : (uint32_t)(row0 * CB);
-    st_issue<EPI, RELOAD, NTM>(st, a, res, row0, tid, rl < a.n ? rl : a.n - 2, cbase, pat);
+    st_issue<EPI, RELOAD, NTM>(st, a, res, row0, tid, rl < a.n ? rl : a.n - 2, cbase, pat,
+                               LFAR ? (int64_t)a.st_far[half] : 0);
   };
   auto issue_edges = [&](SStage<NX, NFAR, CB>& st, int64_t z) {
     if constexpr (DPP)
@@ -534,6 +548,27 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
             xlo[v] = s_line[buf][v][kSNear + 2 * lp + o];
             xhi[v] = s_line[buf][v][kSNear + 2 * lp + 1 + o];
           }
+        }
+      } else if (LFAR && kind != SK_NEXT) {
+        // FAR f of half h (position pairs, NTM bit 8): outer (-n of half 0,
+        // +n of half 1) the staged load, inner the other half's line in LDS
+        // (operand values, as the NEAR slots read their own)
+        const bool outer = (kind == SK_FAR) == (half == 0);
+        const auto& other = s_linex[PAIRW ? half ^ 1 : 0][buf];
+        const dbl2v* o = cur.far[0];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          const double ilo = other[v][kSNear + 2 * lp], ihi = other[v][kSNear + 2 * lp + 1];
+          double olo, ohi;
+          if constexpr (VIRT) {
+            olo = virt_in<EPI>(a, o[0].x, o[1].x, o[NX - 1].x);
+            ohi = virt_in<EPI>(a, o[0].y, o[1].y, o[NX - 1].y);
+          } else {
+            olo = o[v].x;
+            ohi = o[v].y;
+          }
+          xlo[v] = outer ? olo : ilo;
+          xhi[v] = outer ? ohi : ihi;
         }
       } else {
         // NEXT or FAR f: a staged pair
@@ -721,13 +756,21 @@ inline bool st_dpp(const SpmvArgs& a, bool products_only) {
 // EPIs whose kernel entry runs a block-wide prologue sized for kBlock.
 // KR_STENCIL_PAIR (bit mask, A/B): 1 products-only duals, 2 storing duals,
 // 4 the single-vector fused steps (is_step), 8 the fused first two steps,
-// 16 every other 7-point launch.
+// 16 every other 7-point launch, 32 the inner +-n line from LDS (n = 512);
+// unset: 2 | 8 | 32 where bit 32 applies, else no pairs.
 template <int E>
 inline bool st_pair(const SpmvArgs& a, int nblocks) {
   if constexpr (E == EPI_XY_VP || E == EPI_MRR_V) {
     return false;
   } else {
-    const int m = KR_ENV("KR_STENCIL_PAIR", 0);
+    // Default (unset): the storing duals and the fused first steps, and only
+    // where the inner +-n line can come from LDS (bit 32: n = 512) -- measured
+    // on C4 (one box, three rounds, profiles/r04h): dual 0.838 -> 0.813-0.823
+    // ms, first steps 1.71 -> 1.65 ms, 560.7 -> 563-567 it/s; plain pairs
+    // (the ±n lines loaded by both halves) made the dual 7 % slower instead.
+    const int env = KR_ENV("KR_STENCIL_PAIR", -1);
+    const bool lfar = a.st_far[0] == -kSBlock && a.st_far[1] == kSBlock;
+    const int m = env >= 0 ? env : (lfar ? 2 | 8 | 32 : 0);
     constexpr bool dual = E == EPI_DUAL_MRR || E == EPI_DUAL_KCG || E == EPI_DUAL_NONE;
     const int bit = (dual && a.products_only) ? 1
                     : dual                        ? 2
@@ -745,6 +788,15 @@ template <int E, bool RELOAD, int NTM, bool W4>
 void st_launch_pat7(const SpmvArgs& a, int nblocks, size_t lds, hipStream_t s) {
   if constexpr (!RELOAD && !(NTM & 64)) {
     if (st_pair<E>(a, nblocks)) {
+      // KR_STENCIL_PAIR bit 32: the inner +-n line from the other half's LDS
+      // line (needs the LDS path and FAR offsets -+512: n = 512)
+      if constexpr (!(NTM & 32)) {
+        const int env = KR_ENV("KR_STENCIL_PAIR", -1);
+        if ((env < 0 || (env & 32)) && a.st_far[0] == -kSBlock && a.st_far[1] == kSBlock) {
+          st_launch_pat7<E, RELOAD, NTM | 64 | 256, W4>(a, nblocks, lds, s);
+          return;
+        }
+      }
       st_launch_pat7<E, RELOAD, NTM | 64, W4>(a, nblocks, lds, s);
       return;
     }

@@ -514,10 +514,17 @@ def test_stencil_dpp_neighbours_bitwise(monkeypatch, method, name, k, shards):
     ("cg", "box128x128x16", 0, "0"),
     ("mrr", "box128x64x20", 0, "0,0"),
     ("kskipmrr", "box64x64x20", 4, "0"),     # P = 8: never paired
+    # n = 512 (FAR offsets -+512 = the positions p -+ 1): bit 32 takes the
+    # inner +-n line of each half from the other half's LDS line
+    ("kskipmrr", "box512x32x10", 4, "0"),
+    ("adaptivekskipmrr", "aniso512x16x12", 6, "0"),
+    ("kskipcg", "box512x16x64", 3, "0,0"),
+    ("cg", "box512x32x10", 0, "0"),
 ])
 def test_stencil_position_pairs_bitwise(monkeypatch, method, name, k, shards):
     """Two adjacent positions per workgroup (KR_STENCIL_PAIR bit mask: 1
-    products-only duals, 2 storing duals, 4/8 the fused steps, 16 the rest) run
+    products-only duals, 2 storing duals, 4/8 the fused steps, 16 the rest;
+    32: the inner +-n line from the other half's LDS line where n = 512) run
     the same virtual workgroups as the unpaired walk, and so does the reversed
     dispatch order of every other launch (KR_ZIGZAG): the same histories and
     x bit for bit, sharded (boundary launches stay unpaired) or not."""
@@ -528,7 +535,7 @@ def test_stencil_position_pairs_bitwise(monkeypatch, method, name, k, shards):
         kw["k"] = k
     monkeypatch.setenv("KRYLOV_AMD_SHARDS", shards)
     out = []
-    for mask, zz in (("0", "0"), ("0", "1"), ("3", "1"), ("31", "0")):
+    for mask, zz in (("0", "0"), ("0", "1"), ("3", "1"), ("31", "0"), ("63", "0")):
         monkeypatch.setenv("KR_STENCIL_PAIR", mask)
         monkeypatch.setenv("KR_ZIGZAG", zz)
         with contextlib.redirect_stdout(io.StringIO()):
