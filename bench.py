@@ -25,6 +25,9 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# the guide's measured float4 copy (MI355X_MICROARCH.md: 6.29 TB/s, 79 % of
+# spec): reported beside frac as what a streaming kernel can reach in practice
+HBM_COPY_GBS = 6290.0
 
 # BASELINE.json configs. C4 is the headline (metric) and the default; the others
 # are available as --config for parity/perf runs.
@@ -513,6 +516,7 @@ def main():
         # DESIGN.md 9); the CSR figure of SURVEY.md 8(d) is csr_equiv_gbs
         roofline = dict(bound="hbm", kernel=dom, achieved=ach, peak=HBM_PEAK_GBS, unit="GB/s",
                         frac=round(ach / HBM_PEAK_GBS, 4),
+                        copy_peak=HBM_COPY_GBS, frac_of_copy=round(ach / HBM_COPY_GBS, 4),
                         traffic=pmc_traffic(args.config, dom),
                         traffic_source=f"profiles/pmc/{args.config}.json",
                         bytes_per_launch=stored[dom][0], csr_bytes_per_launch=stored[dom][1],
