@@ -356,6 +356,23 @@ void ShardPool::run(int n, const std::function<void(int)>& fn) {
     if (e) std::rethrow_exception(e);
 }
 
+// The solver's sync points (reduce, scalar_state_read): the host needs the
+// result as soon as the copy lands, to compute the next scalars and enqueue
+// the next launches while the GPU idles. KR_SPIN_SYNC (A/B, default on):
+// poll the stream instead of hipStreamSynchronize's wait.
+void host_sync(hipStream_t st) {
+  if (KR_ENV("KR_SPIN_SYNC", 1) == 0) {
+    KR_HIP_CHECK(hipStreamSynchronize(st));
+    return;
+  }
+  for (;;) {
+    const hipError_t e = hipStreamQuery(st);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) KR_HIP_CHECK(e);
+    for (int i = 0; i < 16; ++i) __builtin_ia32_pause();
+  }
+}
+
 void System::for_groups(const std::function<void(const std::vector<int>&)>& fn) {
   if (pool && groups.size() > 1) {
     pool->run((int)groups.size(), [&](int g) { fn(groups[(size_t)g]); });
@@ -2179,7 +2196,7 @@ void System::scalar_state_read() {
   KR_HIP_CHECK(hipMemcpyAsync(s.hst, s.st, sizeof(double) * kScalarState,
                               hipMemcpyDeviceToHost, s.stream));
   const double w0 = now_seconds();
-  KR_HIP_CHECK(hipStreamSynchronize(s.stream));
+  host_sync(s.stream);
   host_wait_s += now_seconds() - w0;
   size_t pend = s.pending.size();
   if (pend > 512) harvest_profile();
@@ -2265,7 +2282,7 @@ std::vector<double> System::reduce(int nslots) {
   const double w0 = now_seconds();
   for (auto& s : shards) {
     KR_HIP_CHECK(hipSetDevice(s.dev));
-    KR_HIP_CHECK(hipStreamSynchronize(s.stream));
+    host_sync(s.stream);
   }
   host_wait_s += now_seconds() - w0;
   // KR_POISON=1 (debug): the consumed slots' partials become NaN, so a later

@@ -398,5 +398,7 @@ std::unique_ptr<IluFactors> build_ilu(int dev, hipStream_t stream, int64_t n, co
                                       const int32_t* ucol, const double* uval,
                                       const int64_t* perm_r, const int64_t* perm_c);
 double now_seconds();
+// wait until a stream's work is done (the solver's sync points; KR_SPIN_SYNC)
+void host_sync(hipStream_t st);
 
 }  // namespace kr
