@@ -503,6 +503,34 @@ std::unique_ptr<IluFactors> build_ilu(int dev, hipStream_t stream, int64_t n, co
         inverse_perm(n, lo ? perm_r : perm_c, lo ? "perm_r" : "perm_c");
     a.perm = static_cast<const int32_t*>(up(inv.data(), 4 * inv.size()));
     f->nnz += (int64_t)scol.size();
+    // level-ordered rows when every row has <= kIluEll entries (KR_ILU_ELL=0:
+    // the CSR chain, A/B)
+    int64_t wmax = 0;
+    for (int64_t i = 0; i < n; ++i) wmax = std::max(wmax, srp[(size_t)i + 1] - srp[(size_t)i]);
+    if (KR_ENV("KR_ILU_ELL", 1) != 0 && wmax <= kIluEll) {
+      const int ew = (int)std::max<int64_t>(wmax, 1);
+      std::vector<int32_t> ecol((size_t)n * ew, 0), ein((size_t)n);
+      std::vector<double> eval((size_t)n * ew, 0.0), ediag((size_t)n);
+      std::vector<uint8_t> ecnt((size_t)n);
+      for (int64_t t = 0; t < n; ++t) {
+        const int64_t i = rows[(size_t)t];
+        const int64_t b = srp[(size_t)i], e = srp[(size_t)i + 1];
+        ecnt[(size_t)t] = (uint8_t)(e - b);
+        for (int64_t jj = b; jj < e; ++jj) {
+          ecol[(size_t)t * ew + (jj - b)] = scol[(size_t)jj];
+          eval[(size_t)t * ew + (jj - b)] = sval[(size_t)jj];
+        }
+        ediag[(size_t)t] = diag[(size_t)i];
+        ein[(size_t)t] = lo ? inv[(size_t)i] : (int32_t)i;
+      }
+      a.ew = ew;
+      a.ecol = static_cast<const int32_t*>(up(ecol.data(), 4 * ecol.size()));
+      a.eval = static_cast<const double*>(up(eval.data(), 8 * eval.size()));
+      a.ecnt = static_cast<const uint8_t*>(up(ecnt.data(), ecnt.size()));
+      a.ediag = static_cast<const double*>(up(ediag.data(), 8 * ediag.size()));
+      a.ein = static_cast<const int32_t*>(up(ein.data(), 4 * ein.size()));
+      KR_HIP_CHECK(hipStreamSynchronize(stream));  // the host vectors go out of scope
+    }
     // launches: runs of levels of <= KR_ILU_WIDE rows in one workgroup, each
     // wider level over the grid (0: every level in the one workgroup)
     const int64_t wide = KR_ENV("KR_ILU_WIDE", 4096);

@@ -569,7 +569,21 @@ struct IluSweepArgs {
   const int32_t* perm = nullptr;
   double* x = nullptr;
   double* out = nullptr;
+  // Level-ordered rows (optional, ew > 0: every row has <= kIluEll
+  // strictly-triangular entries, e.g. an ILU(0) of a 7-point stencil): entry
+  // t of the level lists holds its row's entries at ecol/eval[t * ew + j],
+  // j < ecnt[t] (ascending columns), its diagonal at ediag[t] and the index
+  // of its right-hand side in `in` at ein[t] (lower: the inverse row
+  // permutation; upper: the row), so a row needs one round of loads indexed
+  // by t before the x loads instead of a chain through lvl_rows, rp and col.
+  int ew = 0;
+  const int32_t* ecol = nullptr;
+  const double* eval = nullptr;
+  const uint8_t* ecnt = nullptr;
+  const double* ediag = nullptr;
+  const int32_t* ein = nullptr;
 };
+constexpr int kIluEll = 8;
 // A sweep as launches over its level segments: a run of narrow levels in
 // one workgroup (ilu_sweep_kernel), a wide level (more than KR_ILU_WIDE rows)
 // over the whole GPU in its own launch (ilu_level_kernel); the kernel

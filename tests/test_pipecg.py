@@ -404,3 +404,36 @@ def test_ilu0_c2_tool_factors():
     on.data[:] = 1.0
     assert np.max(np.abs(D.multiply(on).data)) < 1e-14
     assert np.array_equal(pr, np.arange(n ** 3)) and np.array_equal(pc, pr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [10, 17])
+def test_gpu_ilu0_level_ordered_rows_bitwise(monkeypatch, n):
+    """ILU(0) factors of a 3-D Poisson matrix (tools/ilu_c2.py; <= 3 entries
+    per factor row) take the level-ordered rows (IluSweepArgs::ew, one round
+    of loads indexed by the level position before the x loads); the solve is
+    bitwise the CSR-chain sweep (KR_ILU_ELL=0), with and without the wide-level
+    launches."""
+    import importlib.util
+    import os
+    from conftest import REPO
+    spec = importlib.util.spec_from_file_location("ilu_c2", os.path.join(REPO, "tools", "ilu_c2.py"))
+    tool = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(tool)
+    from parallel_krylov_amd.v1.threads.pipeline.pcg import pcg
+    A = golden_matrix(("poisson", n, 3))
+    b = np.random.default_rng(1).standard_normal(A.shape[0])
+    factors = tool.ilu0_poisson3d(n)
+    out = {}
+    for ell in ("0", "1"):
+        for wide in ("0", "8"):
+            monkeypatch.setenv("KR_ILU_ELL", ell)
+            monkeypatch.setenv("KR_ILU_WIDE", wide)
+            with contextlib.redirect_stdout(io.StringIO()):
+                _, nosl, res, x, conv = pcg(A, b, factors, 1e-10, return_x=True)
+            out[ell, wide] = (nosl, res, x.cpu().numpy(), conv)
+    ref = out["0", "0"]
+    assert ref[3]
+    for key, got in out.items():
+        for q in range(3):
+            np.testing.assert_array_equal(got[q], ref[q], err_msg=str(key))
