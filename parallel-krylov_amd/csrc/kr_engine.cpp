@@ -268,6 +268,10 @@ System::~System() {
     if (s.ev_a) (void)hipEventDestroy(s.ev_a);
     if (s.ev_b) (void)hipEventDestroy(s.ev_b);
   }
+  for (auto& g : gslots) {
+    if (g.dev) (void)hipFree(g.dev);
+    if (g.host) (void)hipHostFree(g.host);
+  }
   // streams last, each once (shards of one device may share one)
   for (size_t li = 0; li < shards.size(); ++li) {
     Shard& s = shards[li];
@@ -1299,6 +1303,19 @@ void System::finalize() {
     shards[li].lead = groups[g].empty();
     groups[g].push_back((int)li);
   }
+  for (auto& g : gslots) {
+    if (g.dev) (void)hipFree(g.dev);
+    if (g.host) (void)hipHostFree(g.host);
+  }
+  gslots.assign(groups.size(), GroupSlots{});
+  for (size_t g = 0; g < groups.size(); ++g) {
+    if (comm || groups[g].size() < 2 || groups[g].size() > (size_t)kGroupMax) continue;
+    const size_t bytes = sizeof(double) * kMaxSlots * groups[g].size();
+    KR_HIP_CHECK(hipSetDevice(shards[(size_t)groups[g][0]].dev));
+    KR_HIP_CHECK(hipMalloc(&gslots[g].dev, bytes));
+    fresh_fill(gslots[g].dev, bytes, shards[(size_t)groups[g][0]].stream);
+    KR_HIP_CHECK(hipHostMalloc(&gslots[g].host, bytes, 0));
+  }
   // The split SpMV needs interior rows on every shard; with RCCL ranks the
   // decision is global, so the summation order (interior + boundary partials)
   // is the one of the same partition in one process (oracle/gpu_order.py).
@@ -2287,10 +2304,45 @@ std::vector<double> System::reduce(int nslots) {
     }
     prof_end(s, "reduce", t0, 8.0 * nslots * s.pstride);
   };
-  if (!comm)
-    for_shards(finalize_shard);  // in-process: per-shard host threads
-  else
+  // In-process stream groups whose shards share stride and counts: one
+  // finalize launch and one copy for the group (the same sums per shard).
+  std::vector<char> grouped(groups.size(), 0);
+  if (!comm) {
+    for (size_t g = 0; g < groups.size(); ++g) {
+      if (!gslots[g].dev) continue;
+      const Shard& s0 = shards[(size_t)groups[g][0]];
+      bool same = true;
+      for (int li : groups[g]) {
+        const Shard& s = shards[(size_t)li];
+        same = same && s.pstride == s0.pstride;
+        for (int q = 0; q < nslots && same; ++q) same = s.slot_n[q] == s0.slot_n[q];
+      }
+      grouped[g] = same ? 1 : 0;
+    }
+    for_groups([&](const std::vector<int>& grp) {
+      size_t g = 0;
+      while (groups[g][0] != grp[0]) ++g;
+      if (!grouped[g]) {
+        for (int li : grp) finalize_shard(shards[(size_t)li], (size_t)li);
+        return;
+      }
+      Shard& s0 = shards[(size_t)grp[0]];
+      KR_HIP_CHECK(hipSetDevice(s0.dev));
+      hipEvent_t t0 = nullptr;
+      prof_begin(s0, "reduce", t0);
+      SlotCounts cnt{};
+      for (int q = 0; q < nslots; ++q) cnt.n[q] = s0.slot_n[q];
+      FinalizeGroup fg;
+      for (int li : grp) fg.part[fg.n++] = shards[(size_t)li].partials;
+      launch_finalize_group(fg, s0.pstride, cnt, nslots, gslots[g].dev, kMaxSlots, s0.stream);
+      KR_HIP_CHECK(hipMemcpyAsync(gslots[g].host, gslots[g].dev,
+                                  sizeof(double) * ((grp.size() - 1) * kMaxSlots + nslots),
+                                  hipMemcpyDeviceToHost, s0.stream));
+      prof_end(s0, "reduce", t0, 8.0 * nslots * s0.pstride * grp.size());
+    });
+  } else {
     for (size_t li = 0; li < shards.size(); ++li) finalize_shard(shards[li], li);
+  }
   if (hybrid()) {
     // every local shard's slots side by side (kMaxLocal x nslots), one
     // all-gather for the rank; the stride stays fixed so any rank can index
@@ -2337,8 +2389,14 @@ std::vector<double> System::reduce(int nslots) {
     for (int r = 0; r < comm->nranks; ++r)
       for (int q = 0; q < nslots; ++q) tot[q] = tot[q] + h[r * nslots + q];
   } else {
-    for (auto& s : shards)
-      for (int q = 0; q < nslots; ++q) tot[q] = tot[q] + s.host[q];
+    // shard order (a group need not be a run of it: devices 0, 1, 0, 1)
+    std::vector<const double*> h(shards.size());
+    for (size_t g = 0; g < groups.size(); ++g)
+      for (size_t j = 0; j < groups[g].size(); ++j)
+        h[(size_t)groups[g][j]] = grouped[g] ? gslots[g].host + j * kMaxSlots
+                                             : shards[(size_t)groups[g][j]].host;
+    for (size_t li = 0; li < shards.size(); ++li)
+      for (int q = 0; q < nslots; ++q) tot[q] = tot[q] + h[li][q];
   }
   // Profiling events are read back lazily (every few hundred kernels and on
   // kr_solve_kernel_stats), not at every sync point: reading ~30 event pairs

@@ -246,6 +246,14 @@ struct System {
   // every shard has its own stream. Work of one group is enqueued by one
   // host thread in shard order.
   std::vector<std::vector<int>> groups;
+  // per group of several shards: slot totals of all its shards side by side
+  // (kMaxSlots apart), device and pinned, for one finalize launch and one
+  // copy per group (System::reduce)
+  struct GroupSlots {
+    double* dev = nullptr;
+    double* host = nullptr;
+  };
+  std::vector<GroupSlots> gslots;
   // host threads, one per further stream group (in-process, KR_HOST_THREADS != 0)
   std::unique_ptr<ShardPool> pool;
   // fn(group) for every stream group: on the pool when there is one, else in

@@ -423,6 +423,16 @@ struct SlotCounts {
 void launch_sqrt(double* p, hipStream_t s);  // p[0] = sqrt(p[0]) (cupy.linalg.norm)
 void launch_finalize_counts(const double* partials, int stride, const SlotCounts& counts,
                             int nslots, double* out, hipStream_t s);
+// The same for the shards of one stream group in one launch (blockIdx.y =
+// shard): shard j's slot totals at out + j * out_stride. Every shard has the
+// same stride and counts (System::reduce checks).
+constexpr int kGroupMax = 16;
+struct FinalizeGroup {
+  const double* part[kGroupMax];
+  int n = 0;
+};
+void launch_finalize_group(const FinalizeGroup& g, int stride, const SlotCounts& counts,
+                           int nslots, double* out, int out_stride, hipStream_t s);
 
 // Halo rows of in-process shards on one device: every (src, dst, count)
 // piece of one shard's receive list (all vectors) in ONE launch instead of a

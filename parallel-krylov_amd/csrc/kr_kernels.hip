@@ -507,6 +507,15 @@ __global__ __launch_bounds__(kBlock) void finalize_counts_kernel(const double* _
   if (threadIdx.x == 0) out[slot] = r;
 }
 
+__global__ __launch_bounds__(kBlock) void finalize_group_kernel(FinalizeGroup g, int stride,
+                                                                SlotCounts c, double* out,
+                                                                int out_stride) {
+  __shared__ double s_red[4];
+  const int slot = blockIdx.x, j = blockIdx.y;
+  const double r = block_slot_sum(g.part[j] + (int64_t)slot * stride, c.n[slot], s_red);
+  if (threadIdx.x == 0) out[(int64_t)j * out_stride + slot] = r;
+}
+
 // ---------------------------------------------------------------------------
 // Device-resident CG / MrR scalars (one workgroup): the reductions of one
 // sync point, summed exactly like finalize_counts + the host's shard sum
@@ -1192,6 +1201,16 @@ void launch_finalize_counts(const double* partials, int stride, const SlotCounts
   if (nslots <= 0) return;
   KR_REQUIRE(nslots <= kFinalizeSlots, "too many reduction slots");
   finalize_counts_kernel<<<nslots, kBlock, 0, s>>>(partials, stride, counts, out);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_finalize_group(const FinalizeGroup& g, int stride, const SlotCounts& counts,
+                           int nslots, double* out, int out_stride, hipStream_t s) {
+  if (nslots <= 0 || g.n <= 0) return;
+  KR_REQUIRE(nslots <= kFinalizeSlots && g.n <= kGroupMax && out_stride >= nslots,
+             "grouped finalize: bad sizes");
+  finalize_group_kernel<<<dim3((unsigned)nslots, (unsigned)g.n), kBlock, 0, s>>>(
+      g, stride, counts, out, out_stride);
   KR_HIP_CHECK(hipGetLastError());
 }
 
