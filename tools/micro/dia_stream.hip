@@ -28,6 +28,9 @@
 //     blocks store the previous block's rows and their own: 4 KiB per vector)
 //  12 as 5 with every workgroup storing into its own 2 x 2 KiB (L2-resident:
 //     the store path without the HBM writes)
+//  14 the stream + x1, x2 rows + y1, y2 stores, no LDS work and no barriers
+//     (~100 VGPRs: run at 2, 3 and 4 workgroups per CU)
+//  15 as 14 without the stores
 //   hipcc -O3 --offload-arch=gfx950 -o tools/micro/dia_stream tools/micro/dia_stream.hip
 #include <hip/hip_runtime.h>
 
@@ -53,6 +56,7 @@ __global__ __launch_bounds__(256, 2) void walk(const double* __restrict__ dia, i
                                                const double* __restrict__ x2 = nullptr,
                                                double* y1 = nullptr, double* y2 = nullptr) {
   constexpr bool STREAMS = MODE >= 4;
+  constexpr bool PLAIN = MODE == 14 || MODE == 15;
   constexpr bool MASK = MODE == 4 || MODE == 6;
   constexpr bool DEFER = MODE == 9;
   double q1 = 0.0, q2 = 0.0;
@@ -105,7 +109,18 @@ __global__ __launch_bounds__(256, 2) void walk(const double* __restrict__ dia, i
       }
     }
     double s = 0.0;
-    if constexpr (MODE == 0 || MODE == 1) {
+    if constexpr (PLAIN) {
+#pragma unroll
+      for (int u = 0; u < kU; ++u) s = s + cur[u] * (double)(u + 1);
+      const int64_t r = v * kB + tid;
+      const double s2 = s * c1 + c2;
+      if constexpr (MODE == 14) {
+        y1[r] = s;
+        y2[r] = s2;
+      } else {
+        s += s2;
+      }
+    } else if constexpr (MODE == 0 || MODE == 1) {
 #pragma unroll
       for (int u = 0; u < kU; ++u) s = s + cur[u] * (double)(u + 1);
       if constexpr (MODE == 1) __syncthreads();
@@ -250,6 +265,11 @@ int main(int argc, char** argv) {
     run(walk<63, 1, 5>, "  no mask (again)", 2, 77824, 4.0 * vb);
     run(walk<63, 1, 12>, "  no mask, L2-resident stores", 2, 77824, 2.0 * vb);
     run(walk<63, 1, 7>, "  no mask, no stores (again)", 2, 77824, 2.0 * vb);
+    for (int per_cu : {2, 3, 4}) {
+      const size_t lds = per_cu == 2 ? 77824 : per_cu == 3 ? 52000 : 38000;
+      run(walk<63, 1, 14>, "plain stream+x+stores", per_cu, lds, 4.0 * vb);
+      run(walk<63, 1, 15>, "plain stream+x", per_cu, lds, 2.0 * vb);
+    }
     run(walk<63, 1, 0>, "stride63 stream", 2, 77824);
     return 0;
   }
