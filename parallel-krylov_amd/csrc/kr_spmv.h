@@ -306,12 +306,13 @@ __device__ __forceinline__ void epi_products(double x, double x2, double y, doub
 struct EpiIn {
   double u1 = 0, u2 = 0, us = 0, e = 0, x = 0, x2 = 0;
 };
-template <int EPI>
+// NOX: the caller fills EpiIn::x / x2 itself (the DIA walk, from its window)
+template <int EPI, bool NOX = false>
 __device__ __forceinline__ EpiIn epi_load(const SpmvArgs& a, int64_t row) {
   using T = EpiTraits<EPI>;
   EpiIn in;
-  if constexpr (is_step<EPI>() || T::kX) in.x = a.x1[a.xoff + row];
-  if constexpr (T::kX2) in.x2 = a.x2[a.xoff + row];
+  if constexpr (!NOX && (is_step<EPI>() || T::kX)) in.x = a.x1[a.xoff + row];
+  if constexpr (!NOX && T::kX2) in.x2 = a.x2[a.xoff + row];
   if constexpr (is_step<EPI>()) {
     in.u1 = a.u1[row];
     in.u2 = a.u2[row];
@@ -1980,6 +1981,15 @@ __global__ __launch_bounds__(kBlock, NH > 15 ? 2 : 1) void spmv_diawalk_kernel(S
   auto xload = [&](const double* __restrict__ x, int64_t xi) {
     return x[min(max(xi, (int64_t)0), a.xlen - 1)];
   };
+  // The epilogue's own-row x1 / x2 (EpiIn::x, x2) are the window's middle
+  // rows, written by this lane: read from LDS instead of loaded again (not
+  // for virtual inputs, whose window holds the formed vector). Same values.
+  // KR_DIAW_WINX=0 (compile time, A/B builds) loads them as the other kernels.
+#ifndef KR_DIAW_WINX
+#define KR_DIAW_WINX 1
+#endif
+  constexpr bool kWinX = KR_DIAW_WINX && !VIRT && (is_step<EPI>() || T::kX);
+  static_assert(!(kWinX && T::kX2) || NV == 2, "x2 window for the own-row x2");
   auto xform = [&](double r1, double r2, double r3) {  // the window value of vector 0
     if constexpr (VIRT)
       return virt_in<EPI>(a, r1, r2, r3);
@@ -2019,7 +2029,7 @@ __global__ __launch_bounds__(kBlock, NH > 15 ? 2 : 1) void spmv_diawalk_kernel(S
 #pragma unroll
     for (int u = 0; u <= NH; ++u)
       upn[u] = __builtin_nontemporal_load(blk + (int64_t)(NH + u) * a.dia_ks);
-    pinn = epi_load<EPI>(a, rrb);
+    pinn = epi_load<EPI, kWinX>(a, rrb);
     const int64_t xi = a.xoff + bb * kBlock + kBlock + tid;
     xr1 = xload(a.x1, xi);
     if constexpr (NV == 2 || VIRT) xr2 = xload(a.x2, xi);
@@ -2046,7 +2056,7 @@ __global__ __launch_bounds__(kBlock, NH > 15 ? 2 : 1) void spmv_diawalk_kernel(S
 #pragma unroll
     for (int u = 0; u <= NH; ++u) up[u] = upn[u];
     const W m = mn;
-    const EpiIn pin = pinn;
+    EpiIn pin = pinn;
     const double c1 = xr1, c2 = xr2, c3 = xr3;
     // the next block's loads (the last block re-reads itself: no branch, so
     // nothing below waits for them)
@@ -2125,6 +2135,10 @@ __global__ __launch_bounds__(kBlock, NH > 15 ? 2 : 1) void spmv_diawalk_kernel(S
       for (int k = 0; k < NH; ++k) add(k, ll[k * kBlock]);
 #pragma unroll
       for (int u = 0; u <= NH; ++u) add(NH + u, up[u]);
+    }
+    if constexpr (kWinX) {
+      pin.x = wl[0];
+      if constexpr (T::kX2) pin.x2 = wl[kWalkWin];
     }
     if (active) epi_row_in<EPI>(a, row, sum1, sum2, a.x1, a.x2, pin, acc);
     __syncthreads();
