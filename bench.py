@@ -241,7 +241,8 @@ def stored_format_delta(nnz, n, lay, long_row=12.0):
     diagonal-offset values (8 bytes per offset and row, no rowptr); the
     stencil SpMV streams code_bits bytes of codes per row (8 slots of
     code_bits bits) and nothing else of A -- or, with code patterns, one
-    4-byte pattern id per 512-row block plus the pattern table once."""
+    4-byte pattern id per 512-row block plus the pattern table once. The DIA
+    walk loads no masks over its run of full blocks (dia_full_blocks)."""
     if lay.get("stencil_walk"):
         if lay.get("code_patterns"):
             cb = float(lay.get("code_bits") or 8)
@@ -254,7 +255,8 @@ def stored_format_delta(nnz, n, lay, long_row=12.0):
         # symmetric values: the lower entries are read as the mirrored upper
         # ones (L2 hits), so only the upper half + diagonal must stream
         slots = (lay["n_offsets"] + 1) // 2 if lay.get("dia_sym") else lay["n_offsets"]
-        return 12.0 * nnz + 4.0 * (n + 1) - (8.0 * slots * n_pad + mw / 8 * n)
+        mask_rows = max(n - 256 * int(lay.get("dia_full_blocks") or 0), 0)
+        return 12.0 * nnz + 4.0 * (n + 1) - (8.0 * slots * n_pad + mw / 8 * mask_rows)
     d = 0.0
     if mw:
         d += 4.0 * nnz - mw / 8 * n

@@ -57,8 +57,9 @@ extern "C" {
  *        structs changed size); maxiter = 0 is honoured instead of meaning
  *        the default (CG / k-skip CG return r0, the MrR family is refused).
  *   201  kr_solve_set_precond_ilu added (no struct or behaviour change).
- *   202  kr_system_shard_code_patterns added (no struct or behaviour change). */
-#define KR_ABI_VERSION 202
+ *   202  kr_system_shard_code_patterns added (no struct or behaviour change).
+ *   203  kr_system_shard_dia_full_blocks added (no struct or behaviour change). */
+#define KR_ABI_VERSION 203
 int kr_version(void);
 const char* kr_last_error(void);
 /* Number of HIP devices visible to this process (0 when none). */
@@ -263,6 +264,13 @@ int kr_system_shard_codes(kr_system* sys, int shard, int* code_bits);
  * box: 9 blocks at 512^3). Lossless, compared byte for byte at finalize;
  * KR_STENCIL_PATTERNS=0 disables. Replaces nothing in the reference. */
 int kr_system_shard_code_patterns(kr_system* sys, int shard, int* patterns);
+/* Full-block run of shard s's symmetric DIA walk (after finalize): the
+ * longest run of 256-row blocks [first, first + count) that are whole and
+ * whose rows hold every offset (a band matrix: all but its first and last
+ * blocks). The walk does not load their offset masks (all ones); count = 0
+ * when the shard has no DIA walk. KR_DIAW_FULLRUN=0 disables. Replaces
+ * nothing in the reference. */
+int kr_system_shard_dia_full_blocks(kr_system* sys, int shard, int64_t* first, int64_t* count);
 /* Symmetric diagonal-offset values of shard s (after finalize): 1 when the
  * shard's offsets and stored values are symmetric (checked bitwise at
  * finalize) and the DIA SpMV reads each lower entry as the mirrored upper

@@ -686,6 +686,17 @@ int kr_system_shard_code_patterns(kr_system* sys, int shard, int* patterns) {
   });
 }
 
+int kr_system_shard_dia_full_blocks(kr_system* sys, int shard, int64_t* first, int64_t* count) {
+  return guarded([&] {
+    KR_REQUIRE(sys && shard >= 0 && shard < (int)sys->shards.size(), "bad shard");
+    KR_REQUIRE(sys->finalized, "system not finalized");
+    const Shard& s = sys->shards[shard];
+    const bool on = s.dia && s.dia_walk;
+    if (first) *first = on ? s.dia_full_lo : 0;
+    if (count) *count = on ? s.dia_full_hi - s.dia_full_lo : 0;
+  });
+}
+
 int kr_system_shard_dia_sym(kr_system* sys, int shard, int* sym) {
   return guarded([&] {
     KR_REQUIRE(sys && shard >= 0 && shard < (int)sys->shards.size(), "bad shard");

@@ -794,6 +794,28 @@ void System::build_masks(Shard& s) {
     if (s.dia_sym && M[nm - 1] <= kDiaRows && dia_walk_h_supported(nm / 2) &&
         !(we && atoi(we) == 0))
       s.dia_walk = 1;
+    // The walk skips the mask loads of the longest run of full row blocks
+    // (a band matrix: all but its first and last blocks; C5 -0.4 GB per
+    // SpMV). KR_DIAW_FULLRUN=0 loads every mask (A/B).
+    const char* fe = getenv("KR_DIAW_FULLRUN");
+    if (s.dia_walk && !(fe && atoi(fe) == 0)) {
+      uint8_t* dfull = nullptr;
+      KR_HIP_CHECK(hipMalloc(&dfull, (size_t)nb));
+      launch_dia_block_full(mask, mw, s.n, nm, dfull, s.stream);
+      std::vector<uint8_t> full((size_t)nb);
+      KR_HIP_CHECK(hipMemcpyAsync(full.data(), dfull, (size_t)nb, hipMemcpyDeviceToHost, s.stream));
+      KR_HIP_CHECK(hipStreamSynchronize(s.stream));
+      KR_HIP_CHECK(hipFree(dfull));
+      int64_t best = 0, run = 0;
+      for (int64_t b = 0; b < nb; ++b) {
+        run = full[(size_t)b] ? run + 1 : 0;
+        if (run > best) {
+          best = run;
+          s.dia_full_hi = b + 1;
+          s.dia_full_lo = b + 1 - run;
+        }
+      }
+    }
   }
   KR_HIP_CHECK(hipStreamSynchronize(s.stream));
   s.mask = mask;
@@ -1797,6 +1819,13 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
         a.dia_ks = s.dia_ks;
         a.dia_sym = s.dia_sym;
         a.dia_walk = s.dia_walk;
+        if (s.dia_walk && s.dia_full_hi > s.dia_full_lo) {
+          // launch-relative, whole blocks of this launch only
+          const int64_t rb = r_begin / kDiaRows;
+          a.full_lo = std::max<int64_t>(s.dia_full_lo - rb, 0);
+          a.full_hi = std::min<int64_t>(s.dia_full_hi - rb, rows / kDiaRows);
+          if (a.full_hi < a.full_lo) a.full_hi = a.full_lo;
+        }
         a.dia_wlen = s.dia_wlen;
         a.nseg = s.nseg;
         for (int g = 0; g < s.nseg; ++g) {

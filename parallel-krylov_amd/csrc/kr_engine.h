@@ -88,6 +88,7 @@ struct Shard {
   int64_t dia_bs = 0, dia_ks = 0;  // SpmvArgs::dia_bs / dia_ks
   int dia_sym = 0;                  // SpmvArgs::dia_sym
   int dia_walk = 0;                 // SpmvArgs::dia_walk (spmv_grid = dia_walk_grid)
+  int64_t dia_full_lo = 0, dia_full_hi = 0;  // longest run of full row blocks (SpmvArgs::full_lo)
   int dia_wlen = 0, nseg = 0;       // SpmvArgs x window (dia_wlen, nseg, seg_*, woff)
   int seg_lo[4] = {}, seg_len[4] = {}, seg_base[4] = {};
   int32_t* woff = nullptr;

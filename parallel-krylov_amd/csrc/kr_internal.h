@@ -180,6 +180,9 @@ struct SpmvArgs {
   // (spmv_diawalk_kernel; symmetric shards with a band <= 256 rows). The
   // grid (the launch's block count) fixes each workgroup's run of blocks.
   int dia_walk = 0;
+  // The walk's run of whole, full row blocks [full_lo, full_hi) (launch-
+  // relative): their masks are all-ones and are not loaded. Empty by default.
+  int64_t full_lo = 0, full_hi = 0;
   // x window in LDS (spmv_dia_kernel): nseg segments, segment g = rows
   // row0 + seg_lo[g] .. + seg_len[g] - 1 of the row block at s_xw[seg_base[g]]
   // (starts and lengths even), dia_wlen doubles in all (0: gathers from global
@@ -501,6 +504,10 @@ constexpr int kDiaRows = 256;  // rows per DIA row block (== kBlock)
 // equals dia(i + M[k], nm-1-k) bitwise wherever i + M[k] >= 0.
 void launch_dia_symcheck(const void* mask, int mw, int64_t n, const int32_t* M, int nm,
                          const double* dia, int64_t bs, int64_t ks, int* flag, hipStream_t s);
+// full[b] = 1 when DIA row block b is whole (256 rows < n) and every row
+// holds all nm offsets (the walk's full-block run, Shard::dia_full_lo/hi).
+void launch_dia_block_full(const void* mask, int mw, int64_t n, int nm, uint8_t* full,
+                           hipStream_t s);
 void launch_dia_fill(const void* rowptr, int rowptr64, int64_t n, const int32_t* col,
                      const double* val, int64_t base, const int32_t* M, int nm, double* dia,
                      int64_t bs, int64_t ks, hipStream_t s);

@@ -1457,6 +1457,35 @@ void launch_dia_symcheck(const void* mask, int mw, int64_t n, const int32_t* M, 
   KR_HIP_CHECK(hipGetLastError());
 }
 
+namespace {
+// full[b] = 1 when every row of DIA row block b exists (b * 256 + 255 < n)
+// and holds all nm offsets.
+__global__ void dia_block_full_kernel(const uint8_t* __restrict__ mask, int mb, int64_t n, int nm,
+                                      uint8_t* full, int64_t nb) {
+  for (int64_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    const int64_t i = b * kDiaRows + threadIdx.x;
+    bool ok = i < n;
+    for (int j = 0; ok && j < mb; ++j) {
+      const int lo = 8 * j, hi = min(nm, lo + 8);
+      const unsigned want = hi > lo ? (1u << (hi - lo)) - 1u : 0u;
+      ok = mask[i * mb + j] == want;
+    }
+    const int all = __syncthreads_and(ok ? 1 : 0);
+    if (threadIdx.x == 0) full[b] = all ? 1 : 0;
+  }
+}
+}  // namespace
+
+void launch_dia_block_full(const void* mask, int mw, int64_t n, int nm, uint8_t* full,
+                           hipStream_t s) {
+  const int64_t nb = (n + kDiaRows - 1) / kDiaRows;
+  if (nb <= 0) return;
+  const unsigned g = (unsigned)std::min<int64_t>(nb, 65535);
+  dia_block_full_kernel<<<g, kDiaRows, 0, s>>>(static_cast<const uint8_t*>(mask), mw / 8, n, nm,
+                                               full, nb);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
 void launch_dia_fill(const void* rowptr, int rowptr64, int64_t n, const int32_t* col,
                      const double* val, int64_t base, const int32_t* M, int nm, double* dia,
                      int64_t bs, int64_t ks, hipStream_t s) {

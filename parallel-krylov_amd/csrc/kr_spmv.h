@@ -2024,7 +2024,10 @@ __global__ __launch_bounds__(kBlock, NH > 15 ? 2 : 1) void spmv_diawalk_kernel(S
     const int64_t rowb = bb * kBlock + tid;
     const bool act = rowb < a.n;
     const int64_t rrb = act ? rowb : a.n - 1;
-    mn = act ? (W)mask[rrb] : (W)0;
+    if (bb >= a.full_lo && bb < a.full_hi)  // uniform: a whole, full block
+      mn = kFull;
+    else
+      mn = act ? (W)mask[rrb] : (W)0;
     const double* blk = a.dia + bb * a.dia_bs + tid;
 #pragma unroll
     for (int u = 0; u <= NH; ++u)

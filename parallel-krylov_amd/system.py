@@ -301,7 +301,8 @@ class KrylovSystem:
         code_patterns (stencil SpMV: distinct 512-row code blocks read from a
         table instead of the per-row stream; 0 = per-row stream), dia_sym
         (1: symmetric diagonal-offset values, lower entries read as the
-        mirrored upper ones)."""
+        mirrored upper ones), dia_full_blocks (DIA walk: 256-row blocks whose
+        all-ones offset masks are not loaded)."""
         mb, no = ctypes.c_int(), ctypes.c_int()
         lo, hi = ctypes.c_int64(), ctypes.c_int64()
         call("kr_system_shard_layout", self.handle, s, ctypes.byref(mb), ctypes.byref(no),
@@ -311,9 +312,11 @@ class KrylovSystem:
         call("kr_system_shard_codes", self.handle, s, ctypes.byref(cb))
         call("kr_system_shard_code_patterns", self.handle, s, ctypes.byref(cp))
         call("kr_system_shard_dia_sym", self.handle, s, ctypes.byref(ds))
+        fb0, fbn = ctypes.c_int64(), ctypes.c_int64()
+        call("kr_system_shard_dia_full_blocks", self.handle, s, ctypes.byref(fb0), ctypes.byref(fbn))
         return dict(mask_bits=mb.value, n_offsets=no.value, interior_lo=lo.value,
                     interior_hi=hi.value, dict_values=dv.value, code_bits=cb.value,
-                    code_patterns=cp.value, dia_sym=ds.value)
+                    code_patterns=cp.value, dia_sym=ds.value, dia_full_blocks=fbn.value)
 
     def shard_sched(self, s: int) -> dict:
         """Launch geometry of shard s: elementwise and SpMV grids plus the

@@ -112,6 +112,10 @@ def test_stored_format_bytes():
     nnz_long = 27 * n
     assert bench.stored_format_delta(nnz_long, n, dia) == (
         12.0 * nnz_long + 4.0 * (n + 1) - (8.0 * 27 * 1024 + 4.0 * n))
+    # the DIA walk's full-block run: no mask bytes for its rows
+    dia_run = dict(dia, dia_sym=1, dia_full_blocks=2)
+    assert bench.stored_format_delta(nnz_long, n, dia_run) == (
+        12.0 * nnz_long + 4.0 * (n + 1) - (8.0 * 14 * 1024 + 4.0 * (n - 512)))
     assert "dictionary" in bench.format_name(both) and "masks" in bench.format_name(both)
     st = dict(mask_bits=8, n_offsets=7, dict_values=2, stencil_walk=512)
     assert bench.stored_format_delta(nnz, n, st) == 12.0 * nnz + 4.0 * (n + 1) - 8.0 * n
