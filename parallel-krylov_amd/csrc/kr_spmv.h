@@ -306,21 +306,22 @@ __device__ __forceinline__ void epi_products(double x, double x2, double y, doub
 struct EpiIn {
   double u1 = 0, u2 = 0, us = 0, e = 0, x = 0, x2 = 0;
 };
-// NOX: the caller fills EpiIn::x / x2 itself (the DIA walk, from its window)
-template <int EPI, bool NOX = false>
+// NOX: operands the caller fills itself (the DIA walk, from its window):
+// bit 0 EpiIn::x, bit 1 EpiIn::x2, bit 2 the virtual step's e (x3 at the row)
+template <int EPI, int NOX = 0>
 __device__ __forceinline__ EpiIn epi_load(const SpmvArgs& a, int64_t row) {
   using T = EpiTraits<EPI>;
   EpiIn in;
-  if constexpr (!NOX && (is_step<EPI>() || T::kX)) in.x = a.x1[a.xoff + row];
-  if constexpr (!NOX && T::kX2) in.x2 = a.x2[a.xoff + row];
+  if constexpr (!(NOX & 1) && (is_step<EPI>() || T::kX)) in.x = a.x1[a.xoff + row];
+  if constexpr (!(NOX & 2) && T::kX2) in.x2 = a.x2[a.xoff + row];
   if constexpr (is_step<EPI>()) {
     in.u1 = a.u1[row];
     in.u2 = a.u2[row];
     if constexpr (EPI == EPI_STEP_MRR_X2 || EPI == EPI_STEP_MRR_X || is_vstep<EPI>())
       in.us = a.us[row];
     if constexpr (is_vstep<EPI>()) {
-      in.x2 = a.x2[a.xoff + row];  // y0
-      in.e = a.x3[a.xoff + row];   // Ar1
+      if constexpr (!(NOX & 2)) in.x2 = a.x2[a.xoff + row];  // y0
+      if constexpr (!(NOX & 4)) in.e = a.x3[a.xoff + row];   // Ar1
     }
   } else if constexpr (EPI == EPI_BMINUS) {
     in.e = a.b[row];
@@ -1990,6 +1991,11 @@ __global__ __launch_bounds__(kBlock, NH > 15 ? 2 : 1) void spmv_diawalk_kernel(S
 #endif
   constexpr bool kWinX = KR_DIAW_WINX && !VIRT && (is_step<EPI>() || T::kX);
   static_assert(!(kWinX && T::kX2) || NV == 2, "x2 window for the own-row x2");
+  // A virtual step's window holds the formed vector, but its own-row raw
+  // x1 / x2 / x3 (r, y, Ar) are the rows this lane loaded for the window one
+  // block earlier: kept in registers (own*) instead of loaded again.
+  constexpr bool kOwnRaw = KR_DIAW_WINX && is_vstep<EPI>();
+  constexpr int kNoX = kWinX ? 3 : kOwnRaw ? 7 : 0;
   auto xform = [&](double r1, double r2, double r3) {  // the window value of vector 0
     if constexpr (VIRT)
       return virt_in<EPI>(a, r1, r2, r3);
@@ -2032,7 +2038,7 @@ __global__ __launch_bounds__(kBlock, NH > 15 ? 2 : 1) void spmv_diawalk_kernel(S
 #pragma unroll
     for (int u = 0; u <= NH; ++u)
       upn[u] = __builtin_nontemporal_load(blk + (int64_t)(NH + u) * a.dia_ks);
-    pinn = epi_load<EPI, kWinX>(a, rrb);
+    pinn = epi_load<EPI, kNoX>(a, rrb);
     const int64_t xi = a.xoff + bb * kBlock + kBlock + tid;
     xr1 = xload(a.x1, xi);
     if constexpr (NV == 2 || VIRT) xr2 = xload(a.x2, xi);
@@ -2042,6 +2048,8 @@ __global__ __launch_bounds__(kBlock, NH > 15 ? 2 : 1) void spmv_diawalk_kernel(S
   double up[NH + 1];
 #pragma unroll
   for (int u = 0; u <= NH; ++u) up[u] = 0.0;
+  double own1 = 0.0, own2 = 0.0, own3 = 0.0;  // kOwnRaw: this block's row
+  double nxt1 = 0.0, nxt2 = 0.0, nxt3 = 0.0;  // kOwnRaw: the next block's row
   if (v0 < v1) prefetch(phys(v0));
   int64_t prev = -2;
   for (int64_t v = v0; v < v1; ++v) {
@@ -2076,6 +2084,13 @@ __global__ __launch_bounds__(kBlock, NH > 15 ? 2 : 1) void spmv_diawalk_kernel(S
         if constexpr (VIRT && EPI != EPI_XY_VP) r3 = xload(a.x3, xi);
         s_win[t] = xform(r1, r2, r3);
         if constexpr (NV == 2) s_win[kWalkWin + t] = r2;
+        if constexpr (kOwnRaw) {
+          if (t == tid + kBlock) {
+            own1 = r1, own2 = r2, own3 = r3;
+          } else if (t == tid + 2 * kBlock) {
+            nxt1 = r1, nxt2 = r2, nxt3 = r3;
+          }
+        }
       }
       // positions l < o: the block's own lower values (all loads, then the stores)
       const double* blk = a.dia + b * a.dia_bs + tid;
@@ -2094,6 +2109,10 @@ __global__ __launch_bounds__(kBlock, NH > 15 ? 2 : 1) void spmv_diawalk_kernel(S
       }
       s_win[2 * kBlock + tid] = xform(c1, c2, c3);
       if constexpr (NV == 2) s_win[kWalkWin + 2 * kBlock + tid] = c2;
+      if constexpr (kOwnRaw) {
+        own1 = nxt1, own2 = nxt2, own3 = nxt3;
+        nxt1 = c1, nxt2 = c2, nxt3 = c3;
+      }
     }
 #pragma unroll
     for (int u = 1; u <= NH; ++u) {  // heads: rows p + o < 256 of this block
@@ -2142,6 +2161,10 @@ __global__ __launch_bounds__(kBlock, NH > 15 ? 2 : 1) void spmv_diawalk_kernel(S
     if constexpr (kWinX) {
       pin.x = wl[0];
       if constexpr (T::kX2) pin.x2 = wl[kWalkWin];
+    } else if constexpr (kOwnRaw) {
+      pin.x = own1;
+      pin.x2 = own2;
+      pin.e = own3;
     }
     if (active) epi_row_in<EPI>(a, row, sum1, sum2, a.x1, a.x2, pin, acc);
     __syncthreads();
