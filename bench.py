@@ -327,8 +327,12 @@ def run_system(args, cfg, mat, n, world, rank, local, comm, method, k, env=None)
             else:
                 os.environ[key] = v
     info = sysm.shard_info(0)
-    lay = sysm.shard_layout(0)
-    lay["stencil_walk"] = sysm.shard_sched(0)["stencil_walk"]
+    shards = []  # (info, layout) per local shard: the stored-format bytes per shard
+    for j in range(S):
+        l_ = sysm.shard_layout(j)
+        l_["stencil_walk"] = sysm.shard_sched(j)["stencil_walk"]
+        shards.append((sysm.shard_info(j), l_))
+    lay = shards[0][1]
     # b = default_rng(1).standard_normal(N), the global
     # vector's own rows per shard; --rhs hash: the device counter hash (2u-1)
     b = sysm.split(rhs_host(n)) if args.rhs == "normal" else sysm.rhs(1)
@@ -362,8 +366,8 @@ def run_system(args, cfg, mat, n, world, rank, local, comm, method, k, env=None)
     sysm.close()
     del b
     torch.cuda.empty_cache()
-    return dict(info=info, lay=lay, per_step=per_step, elapsed=elapsed, stats=stats,
-                history=out.info)
+    return dict(info=info, lay=lay, shards=shards, per_step=per_step, elapsed=elapsed,
+                stats=stats, history=out.info)
 
 
 def parallelism(world: int, local_shards: int) -> str:
@@ -396,23 +400,44 @@ def workload_label(config, method, k, mat, n):
     return f"{config}: {m} on {a} (N={n})"
 
 
-def kernel_table(stats, delta):
-    """Per kernel: launches, average ms (HIP events on the solver's stream),
-    GB/s on the stored format's bytes and on SURVEY.md 8(d)'s CSR bytes."""
+def kernel_table(stats, deltas):
+    """Per kernel: launches, average ms and GB/s on the stored format's bytes
+    and on SURVEY.md 8(d)'s CSR bytes. A launch is one call of the op on the
+    first shard's device (kr_solve_kernel_stats): its time is the device
+    window of the `shards` shards it covers there, its CSR bytes theirs
+    summed, so the stored-format bytes subtract those shards' own deltas
+    (`deltas`: stored_format_delta per shard, in shard order; a float is one
+    shard's). The same figures whether the shards share a stream or not."""
+    if not isinstance(deltas, (list, tuple)):
+        deltas = [float(deltas)]
     kernels, stored = {}, {}
     for s_ in stats:
         if s_["name"].startswith("host_"):  # host-side timing (host_table)
             continue
         if s_["launches"]:
             avg = s_["total_ms"] / s_["launches"]
+            nsh = max(1, int(s_.get("shards", 1)))
             csr = s_["bytes_per_launch"]
-            st = csr - (delta if s_["name"].startswith("spmv") else 0.0)
+            # shards past the listed ones: the last listed shard's delta
+            d = sum(deltas[:nsh]) + max(0, nsh - len(deltas)) * deltas[-1]
+            st = csr - (d if s_["name"].startswith("spmv") else 0.0)
             stored[s_["name"]] = (st, csr)
             kernels[s_["name"]] = dict(launches=s_["launches"], avg_ms=round(avg, 5),
                                        gbs=round(st / avg / 1e6, 1),
                                        csr_gbs=round(csr / avg / 1e6, 1),
                                        total_ms=round(s_["total_ms"], 3))
+            if nsh > 1:
+                kernels[s_["name"]]["shards"] = nsh
     return kernels, stored
+
+
+def checked_frac(achieved_gbs, peak=None):
+    """achieved / peak, or None when that exceeds 1: a fraction above the HBM
+    peak is a bookkeeping error (bytes and time of different shard sets),
+    never a measurement, so it is not printed as one."""
+    peak = HBM_PEAK_GBS if peak is None else peak
+    f = achieved_gbs / peak
+    return round(f, 4) if f <= 1.0 else None
 
 
 def host_table(stats):
@@ -461,7 +486,7 @@ def step_roofline(kernels, stored, run, args, per_step, n, nnz_total, method, k)
     byts = sum(stored[n_][0] * v["launches"] for n_, v in kernels.items()) / sampled
     step_s = run["elapsed"] / args.steps
     out = dict(stored_bytes_per_step=round(byts), achieved=round(byts / step_s / 1e9, 1),
-               peak=HBM_PEAK_GBS, unit="GB/s", frac=round(byts / step_s / 1e9 / HBM_PEAK_GBS, 4))
+               peak=HBM_PEAK_GBS, unit="GB/s", frac=checked_frac(byts / step_s / 1e9))
     if method in ("kskipmrr", "adaptivekskipmrr") and k > 0 and nnz_total > 0:
         b_spmv = 12.0 * nnz_total + 4.0 * (n + 1) + 16.0 * n
         per_iter = ((3 * k + 1) * b_spmv + (2 * k + 3) * 8.0 * n + 9 * (k + 1) * 8.0 * n) / (k + 1)
@@ -504,10 +529,10 @@ def main():
 
     run = run_system(args, cfg, mat, n, world, rank, local, comm, method, k)
     info, lay, per_step = run["info"], run["lay"], run["per_step"]
-    delta = stored_format_delta(info["nnz"], info["n_local"], lay)
+    deltas = [stored_format_delta(i_["nnz"], i_["n_local"], l_) for i_, l_ in run["shards"]]
     iterations = args.steps * per_step
     value = iterations / run["elapsed"]
-    kernels, stored = kernel_table(run["stats"], delta)
+    kernels, stored = kernel_table(run["stats"], deltas)
     roofline = None
     if kernels:
         dom = dominant(kernels)
@@ -517,7 +542,7 @@ def main():
         # masks instead of columns, 1-byte dictionary codes instead of values:
         # DESIGN.md 9); the CSR figure of SURVEY.md 8(d) is csr_equiv_gbs
         roofline = dict(bound="hbm", kernel=dom, achieved=ach, peak=HBM_PEAK_GBS, unit="GB/s",
-                        frac=round(ach / HBM_PEAK_GBS, 4),
+                        frac=checked_frac(ach),
                         copy_peak=HBM_COPY_GBS, frac_of_copy=round(ach / HBM_COPY_GBS, 4),
                         traffic=pmc_traffic(args.config, dom),
                         traffic_source=f"profiles/pmc/{args.config}.json",
@@ -532,14 +557,14 @@ def main():
     if not args.no_csr and (lay["mask_bits"] or lay["dict_values"]):
         rc = run_system(args, cfg, mat, n, world, rank, local, comm, method, k,
                         env={"KR_MASK": "0", "KR_VDICT": "0", "KR_STENCIL": "0"})
-        kc, _ = kernel_table(rc["stats"], 0.0)
+        kc, _ = kernel_table(rc["stats"], [0.0])
         csr_rec = dict(value=round(iterations / rc["elapsed"], 3), unit="iterations/s",
                        ms_per_step=round(rc["elapsed"] / args.steps * 1e3, 4),
                        format=format_name(rc["lay"]), env="KR_MASK=0 KR_VDICT=0 KR_STENCIL=0")
         if kc:
             dc = dominant(kc)
             csr_rec.update(kernel=dc, avg_ms=kc[dc]["avg_ms"], achieved=kc[dc]["gbs"],
-                           frac=round(kc[dc]["gbs"] / HBM_PEAK_GBS, 4),
+                           frac=checked_frac(kc[dc]["gbs"]),
                            traffic=pmc_traffic(args.config + "_csr", dc),
                            traffic_source=f"profiles/pmc/{args.config}_csr.json",
                            kernels=kc)

@@ -59,7 +59,7 @@ extern "C" {
  *   201  kr_solve_set_precond_ilu added (no struct or behaviour change).
  *   202  kr_system_shard_code_patterns added (no struct or behaviour change).
  *   203  kr_system_shard_dia_full_blocks added (no struct or behaviour change). */
-#define KR_ABI_VERSION 203
+#define KR_ABI_VERSION 204
 int kr_version(void);
 const char* kr_last_error(void);
 /* Number of HIP devices visible to this process (0 when none). */
@@ -387,12 +387,18 @@ int kr_solve_end(kr_system* sys, double* const* x_dev, kr_solve_result* result);
 int kr_solve_history(kr_system* sys, double* residual_host, int64_t* nosl_host,
                      int64_t* khistory_host, int64_t capacity);
 
-/* Per-kernel-class timing (profile != 0): fills up to `cap` records. */
+/* Per-kernel-class timing (profile != 0): fills up to `cap` records, for the
+ * shards on the first shard's device. One launch = one call of the op:
+ * total_ms sums the device windows (earliest begin to latest end of those
+ * shards' events, whether they share a stream or not), bytes_per_launch is
+ * the algorithmic bytes of all of them and `shards` how many
+ * shards' launches one call covers (ABI 204). */
 typedef struct {
   char name[32];
   int64_t launches;
   double total_ms;
   double bytes_per_launch; /* algorithmic bytes, see DESIGN.md */
+  int64_t shards;
 } kr_kernel_stat;
 int kr_solve_kernel_stats(kr_system* sys, kr_kernel_stat* stats, int cap, int* count);
 /* Zero the per-kernel statistics (e.g. after warm-up) and restart the

@@ -20,7 +20,7 @@ KR_METHOD = {"cg": 0, "mrr": 1, "kskipcg": 2, "kskipmrr": 3, "adaptivekskipmrr":
              "pcg": 5, "chronopoulos_gear": 6, "gropp": 7, "pipeline": 8}
 # include/krylov_amd.h KR_ABI_VERSION: the struct layouts below (SolveParams,
 # SolveResult) are this version's; a library of another version is refused.
-KR_ABI_VERSION = 203
+KR_ABI_VERSION = 204
 KR_FORMAT = {0: "csr", 1: "stencil", 2: "dia", 3: "dense", 4: "dia_walk"}  # kr_system_shard_sched
 
 
@@ -47,7 +47,8 @@ class SolveResult(ctypes.Structure):
 
 class KernelStat(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char * 32), ("launches", ctypes.c_int64),
-                ("total_ms", ctypes.c_double), ("bytes_per_launch", ctypes.c_double)]
+                ("total_ms", ctypes.c_double), ("bytes_per_launch", ctypes.c_double),
+                ("shards", ctypes.c_int64)]
 
 
 def library_path() -> str:

@@ -779,7 +779,7 @@ int kr_solve_begin(kr_system* sys, const kr_solve_params* params, const double* 
     KR_REQUIRE(sys && params, "NULL argument");
     if (!sys->finalized) throw Failure(KR_ERR_STATE, "kr_system_finalize was not called");
     sys->session.reset();
-    for (auto& s : sys->shards) s.stats.clear();
+    sys->kstats.clear();
     sys->profile = params->profile != 0;
     sys->profile_every = params->profile > 0 ? params->profile : 1;
     sys->prof_tick = 0;
@@ -834,7 +834,7 @@ int kr_solve_step(kr_system* sys, int64_t max_outer, int* done) {
       ss.step_once();
       if (sys->profile) {  // host side of every outer iteration (profiled or not)
         const double wait = sys->host_wait_s - w0;
-        auto& st = sys->shards[0].stats;
+        auto& st = sys->kstats;
         st["host_enqueue"].launches += 1;
         st["host_enqueue"].total_ms += (now_seconds() - t0 - wait) * 1e3;
         st["host_wait"].launches += 1;
@@ -900,13 +900,14 @@ int kr_solve_kernel_stats(kr_system* sys, kr_kernel_stat* stats, int cap, int* c
     sys->harvest_profile();  // events still pending (harvested lazily, see reduce)
     int c = 0;
     if (!sys->shards.empty()) {
-      for (auto& kv : sys->shards[0].stats) {
+      for (auto& kv : sys->kstats) {
         if (c < cap && stats) {
           std::memset(&stats[c], 0, sizeof(kr_kernel_stat));
           std::strncpy(stats[c].name, kv.first.c_str(), sizeof(stats[c].name) - 1);
           stats[c].launches = kv.second.launches;
           stats[c].total_ms = kv.second.total_ms;
           stats[c].bytes_per_launch = kv.second.bytes;
+          stats[c].shards = kv.second.shards;
         }
         ++c;
       }
@@ -919,7 +920,7 @@ int kr_solve_kernel_stats_reset(kr_system* sys) {
   return guarded([&] {
     KR_REQUIRE(sys, "NULL system");
     sys->harvest_profile();
-    for (auto& s : sys->shards) s.stats.clear();
+    sys->kstats.clear();
     // restart the every-N-th sampling with the next outer iteration, so a
     // window of K steps after a reset samples exactly ceil(K / N) of them
     sys->prof_tick = 0;

@@ -1439,7 +1439,7 @@ void System::prof_begin(Shard& s, const char* name, hipEvent_t& t0) {
   KR_HIP_CHECK(hipEventRecord(t0, s.stream));
 }
 
-void System::prof_end(Shard& s, const char* name, hipEvent_t t0, double bytes) {
+void System::prof_end(Shard& s, const char* name, hipEvent_t t0, double bytes, int nsh) {
   if (!profile || !t0) return;
   if (s.event_pool.empty()) {
     hipEvent_t e;
@@ -1449,20 +1449,68 @@ void System::prof_end(Shard& s, const char* name, hipEvent_t t0, double bytes) {
   hipEvent_t t1 = s.event_pool.back();
   s.event_pool.pop_back();
   KR_HIP_CHECK(hipEventRecord(t1, s.stream));
-  s.pending.push_back({name, t0, t1});
-  s.stats[name].bytes = bytes;
+  s.pending.push_back({name, t0, t1, bytes, nsh});
 }
 
+// The k-th window of a kernel name on every shard of the first shard's
+// device belongs to the k-th call of that op (a shard records every call of
+// an op or none: group leads record the SpMVs of their group, every shard
+// its vector kernels, shard 0 the scalar steps). One call's time is its
+// device window, from the earliest begin to the latest end of those shards'
+// events (events of one device compare across streams), and its bytes are
+// theirs summed: so a call reads the same whether its shards share one
+// stream (one window per group) or run on a stream each (overlapping
+// windows), and the rate bytes / time is the device's.
 void System::harvest_profile() {
   if (!profile) return;
+  const int dev0 = shards.empty() ? 0 : shards[0].dev;
+  std::map<std::string, std::vector<std::vector<const Shard::Pending*>>> by;
+  for (size_t li = 0; li < shards.size(); ++li) {
+    const Shard& s = shards[li];
+    if (s.dev != dev0) continue;
+    for (const auto& p : s.pending) {
+      auto& lists = by[p.name];
+      lists.resize(shards.size());
+      lists[li].push_back(&p);
+    }
+  }
+  for (auto& kv : by) {
+    size_t calls = 0;
+    for (const auto& l : kv.second) calls = std::max(calls, l.size());
+    for (size_t k = 0; k < calls; ++k) {
+      hipEvent_t ref = nullptr;
+      float lo = 0.f, hi = 0.f;
+      double bytes = 0.0;
+      int64_t nsh = 0;
+      for (const auto& l : kv.second) {
+        if (k >= l.size()) continue;
+        const Shard::Pending* p = l[k];
+        KR_HIP_CHECK(hipEventSynchronize(p->t1));
+        float b = 0.f, e = 0.f;
+        if (!ref) {
+          ref = p->t0;
+          KR_HIP_CHECK(hipEventElapsedTime(&e, ref, p->t1));
+          lo = 0.f;
+          hi = e;
+        } else {
+          KR_HIP_CHECK(hipEventElapsedTime(&b, ref, p->t0));
+          KR_HIP_CHECK(hipEventElapsedTime(&e, ref, p->t1));
+          lo = std::min(lo, b);
+          hi = std::max(hi, e);
+        }
+        bytes += p->bytes;
+        nsh += p->nsh;
+      }
+      auto& st = kstats[kv.first];
+      st.launches += 1;
+      st.total_ms += (double)(hi - lo);
+      st.bytes = bytes;
+      st.shards = nsh;
+    }
+  }
   for (auto& s : shards) {
     for (auto& p : s.pending) {
-      float ms = 0;
-      KR_HIP_CHECK(hipEventSynchronize(p.t1));
-      KR_HIP_CHECK(hipEventElapsedTime(&ms, p.t0, p.t1));
-      auto& st = s.stats[p.name];
-      st.launches += 1;
-      st.total_ms += ms;
+      if (s.dev != dev0) KR_HIP_CHECK(hipEventSynchronize(p.t1));
       s.event_pool.push_back(p.t0);
       s.event_pool.push_back(p.t1);
     }
@@ -1729,6 +1777,9 @@ void System::halo_in_process(Shard& s, int id1, int id2, int id3) {
 void System::halo_group(const std::vector<int>& grp, int id1, int id2, int id3) {
   Shard& s0 = shards[(size_t)grp[0]];
   KR_HIP_CHECK(hipSetDevice(s0.dev));
+  // KR_HALO_KERNEL=0 (A/B, as in halo_in_process): one device copy per piece
+  // on the group's stream instead of the one gather launch
+  const bool gather = KR_ENV("KR_HALO_KERNEL", 1) != 0;
   HaloGatherArgs g;
   for (int li : grp) {
     Shard& s = shards[(size_t)li];
@@ -1737,6 +1788,13 @@ void System::halo_group(const std::vector<int>& grp, int id1, int id2, int id3) 
       if (t.stream != s.stream) continue;
       for (int id : {id1, id2, id3}) {
         if (id < 0) continue;
+        if (!gather) {
+          KR_HIP_CHECK(hipMemcpyAsync(s.vec[id] + s.local_index(p.g0),
+                                      t.vec[id] + t.local_index(p.g0),
+                                      sizeof(double) * (size_t)p.count,
+                                      hipMemcpyDeviceToDevice, s0.stream));
+          continue;
+        }
         if (g.n == kHaloPieces) {
           launch_halo_gather(g, s0.stream);
           g = HaloGatherArgs{};
@@ -1748,7 +1806,7 @@ void System::halo_group(const std::vector<int>& grp, int id1, int id2, int id3) 
       }
     }
   }
-  launch_halo_gather(g, s0.stream);
+  if (gather) launch_halo_gather(g, s0.stream);
 }
 
 void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int b,
@@ -2024,7 +2082,7 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
       }
       Shard& s0 = shards[(size_t)grp[0]];
       KR_HIP_CHECK(hipSetDevice(s0.dev));
-      prof_end(s0, nm, t0s[(size_t)grp[0]], bytes);
+      prof_end(s0, nm, t0s[(size_t)grp[0]], bytes, (int)grp.size());
     });
     return;
   }
@@ -2367,7 +2425,7 @@ std::vector<double> System::reduce(int nslots) {
       KR_HIP_CHECK(hipMemcpyAsync(gslots[g].host, gslots[g].dev,
                                   sizeof(double) * ((grp.size() - 1) * kMaxSlots + nslots),
                                   hipMemcpyDeviceToHost, s0.stream));
-      prof_end(s0, "reduce", t0, 8.0 * nslots * s0.pstride * grp.size());
+      prof_end(s0, "reduce", t0, 8.0 * nslots * s0.pstride * grp.size(), (int)grp.size());
     });
   } else {
     for (size_t li = 0; li < shards.size(); ++li) finalize_shard(shards[li], li);

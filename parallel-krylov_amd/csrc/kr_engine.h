@@ -53,10 +53,16 @@ struct HaloPiece {
   double* stage = nullptr;
 };
 
+// Per kernel name, aggregated over the shards on the first shard's device
+// (System::harvest_profile): one launch = one call of the op; total_ms sums
+// the device windows (first begin to last end of the call's shards on that
+// device); bytes = the algorithmic bytes of all of them; shards = how many
+// shards' launches one call covers there.
 struct KernelStat {
   int64_t launches = 0;
   double total_ms = 0;
   double bytes = 0;
+  int64_t shards = 1;
 };
 
 struct Shard {
@@ -139,10 +145,11 @@ struct Shard {
   struct Pending {
     std::string name;
     hipEvent_t t0, t1;
+    double bytes;  // algorithmic bytes of the window
+    int nsh;       // shards whose launches the window covers (a stream group: its size)
   };
   std::vector<Pending> pending;
   std::vector<hipEvent_t> event_pool;
-  std::map<std::string, KernelStat> stats;
 
   double* own(int id) const { return vec[id] + pad; }
   int64_t local_index(int64_t g) const { return g - row0 + pad; }
@@ -349,7 +356,9 @@ struct System {
 
   // profiling helpers
   void prof_begin(Shard& s, const char* name, hipEvent_t& t0);
-  void prof_end(Shard& s, const char* name, hipEvent_t t0, double bytes);
+  void prof_end(Shard& s, const char* name, hipEvent_t t0, double bytes, int nsh = 1);
+  // kernel statistics of the first shard's device (harvest_profile)
+  std::map<std::string, KernelStat> kstats;
 };
 
 // Solver session interface (one per kr_solve_begin).

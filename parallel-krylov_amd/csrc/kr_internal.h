@@ -61,9 +61,11 @@ inline void opt_in_lds(std::atomic<uint64_t>& done, const void* fn, size_t lds) 
 // knob changed between two calls (as the tests do) takes effect at the next
 // call, and one solve's steps see the values of its kr_solve_begin.
 extern std::atomic<uint64_t> g_env_epoch;
-// cache word: (epoch + 1) << 33 | set << 32 | uint32 value; 0 = empty
+// cache word: tag << 33 | set << 32 | uint32 value; 0 = empty. The tag is
+// the epoch folded into [1, 2^31 - 1] (31 bits above bit 33; never 0, so an
+// empty word never matches), so it keeps matching after 2^31 epochs.
 inline int env_cached(std::atomic<uint64_t>& cache, const char* name, int dflt) {
-  const uint64_t ep = g_env_epoch.load(std::memory_order_relaxed) + 1;
+  const uint64_t ep = 1 + g_env_epoch.load(std::memory_order_relaxed) % ((1ull << 31) - 1);
   const uint64_t c = cache.load(std::memory_order_relaxed);
   if ((c >> 33) == ep) return ((c >> 32) & 1) ? (int)(uint32_t)c : dflt;
   const char* e = getenv(name);

@@ -2343,6 +2343,7 @@ void spmv_dispatch_epi(const SpmvArgs& a, int nblocks, hipStream_t s) {
   }
 }
 
+#include "kr_csr.h"
 #include "kr_stencil.h"
 
 }  // namespace

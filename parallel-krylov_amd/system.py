@@ -301,8 +301,8 @@ class KrylovSystem:
         code_patterns (stencil SpMV: distinct 512-row code blocks read from a
         table instead of the per-row stream; 0 = per-row stream), dia_sym
         (1: symmetric diagonal-offset values, lower entries read as the
-        mirrored upper ones), dia_full_blocks (DIA walk: 256-row blocks whose
-        all-ones offset masks are not loaded)."""
+        mirrored upper ones), dia_full_blocks / dia_full_first (DIA walk: the
+        run of 256-row blocks whose all-ones offset masks are not loaded)."""
         mb, no = ctypes.c_int(), ctypes.c_int()
         lo, hi = ctypes.c_int64(), ctypes.c_int64()
         call("kr_system_shard_layout", self.handle, s, ctypes.byref(mb), ctypes.byref(no),
@@ -316,7 +316,8 @@ class KrylovSystem:
         call("kr_system_shard_dia_full_blocks", self.handle, s, ctypes.byref(fb0), ctypes.byref(fbn))
         return dict(mask_bits=mb.value, n_offsets=no.value, interior_lo=lo.value,
                     interior_hi=hi.value, dict_values=dv.value, code_bits=cb.value,
-                    code_patterns=cp.value, dia_sym=ds.value, dia_full_blocks=fbn.value)
+                    code_patterns=cp.value, dia_sym=ds.value, dia_full_blocks=fbn.value,
+                    dia_full_first=fb0.value)
 
     def shard_sched(self, s: int) -> dict:
         """Launch geometry of shard s: elementwise and SpMV grids plus the
@@ -524,7 +525,8 @@ class KrylovSystem:
         call("kr_solve_kernel_stats", self.handle, arr, cap, ctypes.byref(cnt))
         return [dict(name=arr[i].name.decode(), launches=int(arr[i].launches),
                      total_ms=float(arr[i].total_ms),
-                     bytes_per_launch=float(arr[i].bytes_per_launch))
+                     bytes_per_launch=float(arr[i].bytes_per_launch),
+                     shards=int(arr[i].shards))
                 for i in range(min(cnt.value, cap))]
 
     def close(self) -> None:

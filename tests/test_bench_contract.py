@@ -149,3 +149,45 @@ def test_step_roofline_survey_figures():
     assert abs(out["survey_csr_ideal_its"] - 165.7) < 0.2
     assert 0 < out["frac"] == round(out["achieved"] / 8000.0, 4) or abs(
         out["frac"] - out["achieved"] / 8000.0) < 1e-3
+
+
+def test_multi_shard_kernel_table_is_per_device():
+    """Review item (round 4): with several in-process shards the stats record
+    one device window per call covering `shards` shards, with their CSR bytes
+    summed (kr_solve_kernel_stats, ABI 204): the stored-format bytes must
+    subtract every covered shard's delta, not shard 0's alone, and a frac
+    above 1 is never printed (bench.checked_frac). The same stats read the
+    same whether the shards shared a stream (one group window) or ran on a
+    stream each (overlapping windows, merged by the engine)."""
+    import bench
+    n, nnz = 512 ** 3 // 8, 937951232 // 8  # one 64-plane shard of C4
+    lay = dict(mask_bits=8, n_offsets=7, dict_values=2, stencil_walk=512, code_bits=2,
+               code_patterns=9)
+    d = bench.stored_format_delta(nnz, n, lay)
+    csr = 12.0 * nnz + 4.0 * (n + 1) + 32.0 * n  # one shard's dual, CSR bytes
+    stored1 = csr - d
+    # 1 shard: 0.11 ms per dual; 8 shards on one device: 8 x 0.11 ms window
+    one = [dict(name="spmv2_gram_mrr", launches=10, total_ms=10 * 0.11, bytes_per_launch=csr,
+                shards=1)]
+    eight = [dict(name="spmv2_gram_mrr", launches=10, total_ms=10 * 0.88,
+                  bytes_per_launch=8 * csr, shards=8)]
+    k1, s1 = bench.kernel_table(one, [d])
+    k8, s8 = bench.kernel_table(eight, [d] * 8)
+    assert s1["spmv2_gram_mrr"][0] == stored1
+    assert s8["spmv2_gram_mrr"][0] == 8 * stored1
+    assert k8["spmv2_gram_mrr"]["shards"] == 8
+    f1 = bench.checked_frac(k1["spmv2_gram_mrr"]["gbs"])
+    f8 = bench.checked_frac(k8["spmv2_gram_mrr"]["gbs"])
+    assert f1 is not None and f8 is not None and f8 <= 1.0
+    assert abs(f8 - f1) / f1 < 0.01
+    # the round-4 bookkeeping (8 shards' bytes less ONE shard's delta) would
+    # have claimed more than the HBM peak: refused
+    bogus = (8 * csr - d) / (0.88 * 1e6)
+    assert bench.checked_frac(bogus) is None
+    # a shard count past the listed deltas reuses the last one
+    k2, s2 = bench.kernel_table([dict(eight[0], shards=2)], [d])
+    assert s2["spmv2_gram_mrr"][0] == 8 * csr - 2 * d
+    # non-SpMV kernels keep their bytes
+    kv, sv = bench.kernel_table([dict(name="update_mrr", launches=2, total_ms=1.0,
+                                      bytes_per_launch=1e9, shards=8)], [d] * 8)
+    assert sv["update_mrr"][0] == 1e9

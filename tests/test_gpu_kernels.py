@@ -580,3 +580,69 @@ def test_dia_symmetric_values_read_mirrored(torch_dev, monkeypatch, spec, shards
             np.testing.assert_array_equal(y.cpu().numpy(), M.dot(x))
         finally:
             sysm.close()
+
+
+def _longest_full_run(M, lo, hi):
+    """The DIA walk's run of full row blocks of shard rows [lo, hi), as
+    finalize picks it (kr_engine.cpp build_masks): a 256-row block is full
+    when it is whole and every row holds every offset of the shard; the
+    first of the longest runs wins. Returns (first block, count)."""
+    S = M[lo:hi]
+    rows = np.repeat(np.arange(lo, hi), np.diff(S.indptr))
+    nm = np.unique(S.indices - rows).size
+    per_row = np.diff(S.indptr)
+    nb = -(-(hi - lo) // 256)
+    best, run, first = 0, 0, 0
+    for b in range(nb):
+        r = per_row[256 * b:256 * b + 256]
+        full = r.size == 256 and bool(np.all(r == nm))
+        run = run + 1 if full else 0
+        if run > best:
+            best, first = run, b + 1 - run
+    return (first, best) if best else (0, 0)
+
+
+@pytest.mark.parametrize("grid", ["auto", "2", "5"])
+@pytest.mark.parametrize("shards", [1, 3])
+def test_dia_walk_full_block_run_split_mid_band(torch_dev, monkeypatch, shards, grid):
+    """The DIA walk's full-block run (masks not loaded, KR_DIAW_FULLRUN):
+    a band matrix with one symmetric off-diagonal pair dropped in the middle
+    of a shard splits its run of full blocks in two, so finalize must pick
+    the longer part (dia_full_blocks / dia_full_first against a restatement),
+    and the interior and boundary launches see the run shifted by their
+    first row block. y is bitwise scipy's with the run and with every mask
+    loaded (KR_DIAW_FULLRUN=0), over several forced walk grids."""
+    import scipy.sparse as sp
+    from parallel_krylov_amd.system import KrylovSystem, balanced_partition
+    if grid != "auto":
+        monkeypatch.setenv("KR_DIAW_GRID", grid)
+    A = golden_matrix(["banded", 6000, 13, 64, 0]).tocsr().tolil()
+    n = A.shape[0]
+    part = balanced_partition(n, shards)
+    # drop the pair (i, j), (j, i) 40 % into the last shard (symmetric values
+    # stay symmetric, so the shard keeps the walk)
+    i = part[-2] + (part[-1] - part[-2]) * 2 // 5
+    j = max(c for c in A.rows[i] if c > i)
+    A[i, j] = 0.0
+    A[j, i] = 0.0
+    A = sp.csr_matrix(A)
+    A.eliminate_zeros()
+    x = np.random.default_rng(5).standard_normal(n)
+    want = [_longest_full_run(A, part[s], part[s + 1]) for s in range(shards)]
+    # the dropped pair split the last shard's run: its longest part is shorter
+    # than the run of the untouched matrix would be
+    assert want[-1][1] < -(-(part[-1] - part[-2]) // 256) - 2
+    for fullrun in ("1", "0"):
+        monkeypatch.setenv("KR_DIAW_FULLRUN", fullrun)
+        sysm = KrylovSystem(n, part, [0] * shards)
+        try:
+            sysm.set_matrix(A)
+            sysm.finalize()
+            assert [sysm.shard_format(s) for s in range(shards)] == ["dia_walk"] * shards
+            got = [(sysm.shard_layout(s)["dia_full_first"], sysm.shard_layout(s)["dia_full_blocks"])
+                   for s in range(shards)]
+            assert got == (want if fullrun == "1" else [(0, 0)] * shards)
+            y = sysm.gather(sysm.spmv(sysm.split(x)))
+            np.testing.assert_array_equal(y.cpu().numpy(), A.dot(x))
+        finally:
+            sysm.close()
