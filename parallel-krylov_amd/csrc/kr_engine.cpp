@@ -1836,10 +1836,15 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
   // boundary launches ADD their reduction partials to the interior launch's
   // (same stream, fixed order: deterministic).
   const bool split = exchange && overlap && all_interior;
-  // products only: the stencil kernel and the windowed diagonal-offset
-  // kernel skip the y1/y2 stores (own stat name, and 16 N fewer bytes)
+  // products only: every SpMV kernel skips the y1/y2 stores of a dual whose
+  // outputs nobody reads (the stencil walk by its own flag, every other
+  // kernel in epi_store_row*: the row walks, the DIA kernels and their walk,
+  // the dense one; own stat name, and 16 N fewer bytes). Round 5: for every
+  // format, not only the stencil and the windowed DIA kernel -- stores mixed
+  // into the read stream cost ~3x their bytes (plain CSR dual at 512^3: 0.72
+  // of 3.3 ms for 2.15 GB; the C5 walk: 0.45-0.6 ms for 0.8 GB).
   bool po = products_only && products_only_on && dual;
-  auto po_shard = [&](const Shard& s) { return po && (s.scode || (s.dia && s.dia_wlen > 0)); };
+  auto po_shard = [&](const Shard& s) { (void)s; return po; };
   bool po_any = false;
   for (auto& s : shards) po_any = po_any || po_shard(s);
   const char* nm = po_any ? epi_name_po(epi) : epi_name(epi);

@@ -450,6 +450,38 @@ __device__ __forceinline__ void epi_store_row(const SpmvArgs& a, int64_t row, co
   }
 }
 
+// One row's epilogue stores with store kind SK: 0 plain, 1 non-temporal
+// (the row walks' default with a non-temporal matrix stream: a plain-CSR dual
+// SpMV at 512^3 spends 0.72 of its 3.3 ms on the 2.15 GB of y1 / y2 stores,
+// and non-temporal ones cut 0.15 ms of that; tools/micro/csr_micro), 2
+// agent-scope relaxed atomic stores (sc1: the line leaves the XCD's L2;
+// measured no faster than plain).
+template <int SK>
+__device__ __forceinline__ void st1(double* p, double v) {
+  if constexpr (SK == 1)
+    __builtin_nontemporal_store(v, p);
+  else if constexpr (SK == 2)
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    *p = v;
+}
+template <int EPI, int SK>
+__device__ __forceinline__ void epi_store_row_k(const SpmvArgs& a, int64_t row, const EpiVals& o) {
+  if constexpr (is_step<EPI>()) {
+    if constexpr (epi_writes_ud<EPI>()) st1<SK>(a.ud + row, o.ud);
+    st1<SK>(a.u1 + row, o.u1);
+    st1<SK>(a.u2 + row, o.u2);
+    st1<SK>(a.y1 + row, o.y1);
+    if constexpr (EPI == EPI_MRR_V) st1<SK>(a.y2 + row, o.y2);
+  } else {
+    if constexpr (EpiTraits<EPI>::NV == 2)
+      if (a.products_only) return;
+    st1<SK>(a.y1 + row, o.y1);
+    if constexpr (EpiTraits<EPI>::NV == 2) st1<SK>(a.y2 + row, o.y2);
+    if constexpr (EPI == EPI_XY_VP) st1<SK>(a.u1 + row, o.u1);
+  }
+}
+
 // Rows row, row + 1 (row even: own-row vectors are 16-byte aligned there);
 // ok = false sends the pair to SpmvArgs::scratch instead (lanes past the
 // last row store unconditionally, see kr_stencil.h).
@@ -1383,7 +1415,8 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
       first_window = false;
       continue;
     }
-    if (active) epi_row_in<EPI>(a, r0 + tid, sum1, sum2, x1, x2, pin, acc);
+    if (active)
+      epi_store_row_k<EPI, NT ? 1 : 0>(a, r0 + tid, epi_values<EPI>(a, sum1, sum2, pin, acc));
     if (!has_next) break;
     // advance to the next row block; its boundaries after it come through
     // the scalar cache now (used one row block later)

@@ -545,3 +545,50 @@ def test_stencil_position_pairs_bitwise(monkeypatch, method, name, k, shards):
         np.testing.assert_array_equal(i1["nosl"], out[0][1]["nosl"])
         np.testing.assert_array_equal(i1["residual"], out[0][1]["residual"])
         np.testing.assert_array_equal(x1, out[0][0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt", ["csr", "rowwalk", "dia_walk", "stencil"])
+@pytest.mark.parametrize("method,k", [("kskipmrr", 4), ("kskipmrr", 3), ("kskipcg", 3),
+                                      ("adaptivekskipmrr", 4)])
+@pytest.mark.parametrize("shards", [1, 2])
+def test_products_only_every_format_bitwise(monkeypatch, fmt, method, k, shards):
+    """Round 5: the last basis dual of every outer iteration (its outputs
+    feed only the Gram products) skips its y1/y2 stores in EVERY SpMV format
+    -- plain CSR row walk, the masked/dictionary row walk, the symmetric DIA
+    walk and the stencil walk -- and runs under its own stat name. Same
+    products, so the history, k structure and x equal the storing run
+    (KR_PRODUCTS_ONLY=0) bit for bit."""
+    env = {"csr": {"KR_MASK": "0", "KR_VDICT": "0", "KR_STENCIL": "0"},
+           "rowwalk": {"KR_STENCIL": "0"}, "dia_walk": {}, "stencil": {}}[fmt]
+    A = (golden_matrix(["banded", 3000, 31, 256, 0]) if fmt == "dia_walk"
+         else MATRICES["p3d32"]())
+    b = np.random.default_rng(4).standard_normal(A.shape[0])
+    tag = "kcg" if method == "kskipcg" else "mrr"
+    runs = []
+    for po in ("1", "0"):
+        monkeypatch.setenv("KR_PRODUCTS_ONLY", po)
+        sysm = _system(A, shards, env, monkeypatch)
+        try:
+            want = {"csr": "csr", "rowwalk": "csr", "dia_walk": "dia_walk", "stencil": "stencil"}
+            assert [sysm.shard_format(s) for s in range(shards)] == [want[fmt]] * shards
+            if fmt == "csr":  # plain CSR: no masks, no dictionary
+                assert all(sysm.shard_layout(s)["mask_bits"] == 0 and
+                           sysm.shard_layout(s)["dict_values"] == 0 for s in range(shards))
+            sysm.begin(method, sysm.split(b), None, tol=1e-10, maxiter=60, k=k, profile=1)
+            while not sysm.step(4):
+                pass
+            st = {r["name"]: r["launches"] for r in sysm.kernel_stats()}
+            out = sysm.finish(method)
+            x = np.concatenate([t.cpu().numpy() for t in out.x])
+        finally:
+            sysm.close()
+        runs.append((st, out.info, x))
+    (st1, i1, x1), (st0, i0, x0) = runs
+    assert st1.get(f"spmv2_gram_{tag}_last", 0) > 0, st1
+    assert st0.get(f"spmv2_gram_{tag}_last", 0) == 0, st0
+    np.testing.assert_array_equal(i1["nosl"], i0["nosl"])
+    if "khistory" in i0:
+        np.testing.assert_array_equal(i1["khistory"], i0["khistory"])
+    np.testing.assert_array_equal(i1["residual"], i0["residual"])
+    np.testing.assert_array_equal(x1, x0)

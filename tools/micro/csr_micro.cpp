@@ -217,6 +217,28 @@ void run_direct(Ctx& c, int grid, const char* name) {
   report(c, name, grid, ms);
 }
 
+template <int E, int FL>
+void run_k3(Ctx& c, int grid, const char* name) {
+  CK(hipMemset(c.y1, 0, c.n * 8));
+  CK(hipMemset(c.y2, 0, c.n * 8));
+  SpmvArgs a = args_for(c, grid);
+  const float ms = time_it(c, [&] {
+    spmv_kernel3<int32_t, E, FL><<<grid, kBlock>>>(a);
+  });
+  report(c, name, grid, ms);
+}
+
+template <int E, int FL>
+void run_k4(Ctx& c, int grid, const char* name) {
+  CK(hipMemset(c.y1, 0, c.n * 8));
+  CK(hipMemset(c.y2, 0, c.n * 8));
+  SpmvArgs a = args_for(c, grid);
+  const float ms = time_it(c, [&] {
+    spmv_kernel4<int32_t, E, FL><<<grid, kBlock>>>(a);
+  });
+  report(c, name, grid, ms);
+}
+
 int main(int argc, char** argv) {
   Ctx c;
   c.ns = argc > 1 ? atoll(argv[1]) : 512;
@@ -297,10 +319,47 @@ int main(int argc, char** argv) {
     run_direct<EPI_DUAL_MRR, 7, false, 2>(c, 8192, "direct AB2 no stores");
     run_direct<EPI_DUAL_MRR, 7, false, 3>(c, 8192, "direct AB3 own-row gathers");
   }
+  if (on("k3")) {
+    run_k3<EPI_DUAL_MRR, 0>(c, g8, "kernel3 FL0 (= kernel2)");
+    run_k3<EPI_DUAL_MRR, 1>(c, g8, "kernel3 FL1 diag");
+    run_k3<EPI_DUAL_MRR, 2>(c, g8, "kernel3 FL2 rp1");
+    run_k3<EPI_DUAL_MRR, 4>(c, g8, "kernel3 FL4 buf");
+    run_k3<EPI_DUAL_MRR, 7>(c, g8, "kernel3 FL7 all");
+    run_k3<EPI_DUAL_MRR, 7>(c, 4096, "kernel3 FL7 all");
+    run_k3<EPI_DUAL_MRR, 8>(c, g8, "kernel3 FL8 pairs");
+    run_k3<EPI_DUAL_MRR, 24>(c, g8, "kernel3 FL24 pairs NT");
+    run_k3<EPI_DUAL_MRR, 15>(c, g8, "kernel3 FL15 all+pairs");
+    run_k3<EPI_DUAL_MRR, 31>(c, g8, "kernel3 FL31 all+pairs NT");
+  }
+  if (on("k3ab")) {
+    run_k3<EPI_DUAL_MRR, 16>(c, g8, "kernel3 FL16 NT stores");
+    run_k3<EPI_DUAL_MRR, 16 + 64>(c, g8, "kernel3 NT, AB no stores");
+    run_k3<EPI_DUAL_MRR, 16 + 128>(c, g8, "kernel3 NT, AB no gathers");
+    run_k3<EPI_DUAL_MRR, 16 + 64 + 128>(c, g8, "kernel3 NT, AB no st/gathers");
+    run_k3<EPI_DUAL_MRR, 16 + 256>(c, g8, "kernel3 NT single-buf");
+    run_k3<EPI_DUAL_MRR, 16 + 256 + 64 + 128>(c, g8, "kernel3 NT SB no st/gathers");
+    run_k3<EPI_DUAL_MRR, 16 + 7>(c, g8, "kernel3 NT + diag/rp1/buf");
+  }
+  if (on("k4")) {
+    run_k4<EPI_DUAL_MRR, 0>(c, g8, "kernel4 depth-2 staging");
+    run_k4<EPI_DUAL_MRR, 64>(c, g8, "kernel4 AB no stores");
+    run_k4<EPI_DUAL_MRR, 64 + 128>(c, g8, "kernel4 AB no st/gathers");
+    run_k4<EPI_DUAL_MRR, 0>(c, 4096, "kernel4 depth-2 staging");
+    run_k4<EPI_DUAL_MRR, 0>(c, 16384, "kernel4 depth-2 staging");
+  }
+  if (on("k3s")) {
+    run_k3<EPI_DUAL_MRR, 16>(c, g8, "kernel3 FL16 NT stores");
+    run_k3<EPI_DUAL_MRR, 32>(c, g8, "kernel3 FL32 sc1 stores");
+    run_k3<EPI_DUAL_MRR, 24>(c, g8, "kernel3 FL24 pairs NT");
+    run_k3<EPI_DUAL_MRR, 24>(c, 6144, "kernel3 FL24 pairs NT");
+    run_k3<EPI_DUAL_MRR, 24>(c, 12288, "kernel3 FL24 pairs NT");
+    run_k3<EPI_DUAL_MRR, 24>(c, 16384, "kernel3 FL24 pairs NT");
+  }
   if (on("prof")) {  // one launch each for rocprofv3 --pmc
     c.reps = 3;
     run_k2<EPI_DUAL_MRR, 1, 1>(c, g8, "kernel2 dual_mrr DB NT (default)");
     run_direct<EPI_DUAL_MRR, 7, false>(c, 8192, "direct dual_mrr KC7");
+    run_k3<EPI_DUAL_MRR, 7>(c, g8, "kernel3 FL7 all");
   }
   return 0;
 }

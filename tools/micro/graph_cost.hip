@@ -19,8 +19,12 @@
 #include <cstring>
 #include <vector>
 
+// GRAPH_TRACE=1: every call of the capture section is printed before it runs
+// (stdout unbuffered), so a crash names the call it died in.
+static bool g_trace = false;
 #define CK(x)                                                               \
   do {                                                                      \
+    if (g_trace) printf("> %d %s\n", __LINE__, #x);                         \
     hipError_t e = (x);                                                     \
     if (e != hipSuccess) {                                                  \
       printf("%s:%d %s -> %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e)); \
@@ -49,8 +53,16 @@ int main(int argc, char** argv) {
   const int NSPMV = argc > 2 ? atoi(argv[2]) : 9;   // split SpMVs per outer iteration
   const int iters = argc > 3 ? atoi(argv[3]) : 200;
   const int G = argc > 4 ? atoi(argv[4]) : 64;      // workgroups per launch
+  // capture-crash bisection (round 5): 0 the engine's pattern; 1 no waits on
+  // the neighbours' events (each comm / compute stream waits its own shard's
+  // only); 2 a fresh event for every record (no event recorded twice in one
+  // capture); 3 both
+  const int MODE = argc > 5 ? atoi(argv[5]) : 0;
   std::vector<hipStream_t> st(S), cs(S);
   std::vector<hipEvent_t> ev_in(S), ev_out(S), ev_join(2 * S);
+  std::vector<hipEvent_t> ev_in_m(S * NSPMV), ev_out_m(S * NSPMV);  // MODE & 2
+  for (auto& ev : ev_in_m) CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  for (auto& ev : ev_out_m) CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   for (int s = 0; s < S; ++s) {
     CK(hipStreamCreateWithFlags(&st[s], hipStreamNonBlocking));
     CK(hipStreamCreateWithFlags(&cs[s], hipStreamNonBlocking));
@@ -72,13 +84,19 @@ int main(int argc, char** argv) {
     for (int m = 0; m < NSPMV; ++m) {
       const bool step = m < 4;  // the step SpMVs carry (eta, zeta)
       a.c[0] = m;
-      for (int s = 0; s < S; ++s) CK(hipEventRecord(ev_in[s], st[s]));
+      const bool fresh = capture && (MODE & 2);
+      const bool cross = !(MODE & 1);
+      auto EI = [&](int s) { return fresh ? ev_in_m[m * S + s] : ev_in[s]; };
+      auto EO = [&](int s) { return fresh ? ev_out_m[m * S + s] : ev_out[s]; };
+      for (int s = 0; s < S; ++s) CK(hipEventRecord(EI(s), st[s]));
       for (int s = 0; s < S; ++s) {
-        CK(hipStreamWaitEvent(cs[s], ev_in[s], 0));
-        if (s > 0) CK(hipStreamWaitEvent(cs[s], ev_in[s - 1], 0));
-        if (s + 1 < S) CK(hipStreamWaitEvent(cs[s], ev_in[s + 1], 0));
+        CK(hipStreamWaitEvent(cs[s], EI(s), 0));
+        if (cross && s > 0) CK(hipStreamWaitEvent(cs[s], EI(s - 1), 0));
+        if (cross && s + 1 < S) CK(hipStreamWaitEvent(cs[s], EI(s + 1), 0));
+        if (g_trace) printf("> launch gather s=%d m=%d\n", s, m);
         work<<<G, 256, 0, cs[s]>>>(a);
-        CK(hipEventRecord(ev_out[s], cs[s]));
+        CK(hipEventRecord(EO(s), cs[s]));
+        if (g_trace) printf("> launch interior s=%d m=%d\n", s, m);
         work<<<G, 256, 0, st[s]>>>(a);
         if (capture && step && coef) {
           hipStreamCaptureStatus cst;
@@ -95,9 +113,10 @@ int main(int argc, char** argv) {
         }
       }
       for (int s = 0; s < S; ++s) {
-        CK(hipStreamWaitEvent(st[s], ev_out[s], 0));
-        if (s > 0) CK(hipStreamWaitEvent(st[s], ev_out[s - 1], 0));
-        if (s + 1 < S) CK(hipStreamWaitEvent(st[s], ev_out[s + 1], 0));
+        CK(hipStreamWaitEvent(st[s], EO(s), 0));
+        if (cross && s > 0) CK(hipStreamWaitEvent(st[s], EO(s - 1), 0));
+        if (cross && s + 1 < S) CK(hipStreamWaitEvent(st[s], EO(s + 1), 0));
+        if (g_trace) printf("> launch boundary s=%d m=%d\n", s, m);
         work<<<G / 8 + 1, 256, 0, st[s]>>>(a);
         if (capture && step && coef) {
           hipStreamCaptureStatus cst;
@@ -140,6 +159,7 @@ int main(int argc, char** argv) {
 
   // ---- capture
   printf("capturing\n");
+  g_trace = getenv("GRAPH_TRACE") && atoi(getenv("GRAPH_TRACE")) != 0;
   hipGraph_t graph;
   std::vector<hipGraphNode_t> coef;
   double tc0 = now();
@@ -164,6 +184,7 @@ int main(int argc, char** argv) {
   hipGraphExec_t exec;
   CK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
   printf("instantiated\n");
+  g_trace = false;
   const double tc1 = now();
   printf("capture+instantiate %.3f ms, %zu nodes, %zu patched launches\n", 1e3 * (tc1 - tc0), nn,
          coef.size());
