@@ -126,41 +126,118 @@ def banded_offsets(h: int, width: int, seed: int) -> np.ndarray:
     return np.array(sorted(pool[:h]), dtype=np.int64)
 
 
+def banded_arrays(N: int, h: int, width: int, seed: int):
+    """The symmetric random banded SPD matrix as raw CSR arrays (indptr int64,
+    indices int32, data float64) -- the arrays ``banded`` wraps. Rows are built
+    in chunks on a thread pool (numpy releases the GIL; each chunk writes its
+    own slice), so the arrays are the sequential build's bit for bit; C5's
+    N = 50M (3.15 G entries) needs the int64 indptr."""
+    off = banded_offsets(h, width, seed)
+    # row i's entries: lower (offsets descending = columns ascending), the
+    # diagonal, upper (offsets ascending); a slot exists when its column does
+
+    def present(g):
+        ml = [(g - o) >= 0 for o in off[::-1]]
+        mu = [(g + o) < N for o in off]
+        return ml, mu
+
+    chunk = 1 << 20
+    starts = range(0, N, chunk)
+    indptr = np.zeros(N + 1, dtype=np.int64)
+
+    def count(c0):
+        g = np.arange(c0, min(N, c0 + chunk), dtype=np.int64)
+        ml, mu = present(g)
+        indptr[c0 + 1:c0 + 1 + g.size] = 1 + np.sum(ml, axis=0) + np.sum(mu, axis=0)
+
+    _pool_map(count, starts)
+    np.cumsum(indptr, out=indptr)
+    nnz = int(indptr[-1])
+    indices = np.empty(nnz, dtype=np.int32)
+    data = np.empty(nnz, dtype=np.float64)
+
+    def fill(c0):
+        g = np.arange(c0, min(N, c0 + chunk), dtype=np.int64)
+        cols, vals, masks = [], [], []
+        for o in off[::-1]:  # lower part, ascending column
+            lo = g - o
+            m = lo >= 0
+            cols.append(lo)
+            vals.append(-unit_uniform(seed, np.where(m, lo, 0), o))
+            masks.append(m)
+        upper = []
+        for o in off:
+            hi = g + o
+            m = hi < N
+            upper.append((hi, -unit_uniform(seed, g, o), m))
+        # diagonal: sum of |off| in column order (lower then upper), then + 1
+        s = np.zeros(g.size)
+        for v, m in zip(vals, masks):
+            s = s + np.where(m, np.abs(v), 0.0)
+        for _, v, m in upper:
+            s = s + np.where(m, np.abs(v), 0.0)
+        cols.append(g); vals.append(s + 1.0); masks.append(np.ones(g.size, bool))
+        for c, v, m in upper:
+            cols.append(c); vals.append(v); masks.append(m)
+        C = np.stack(cols, axis=1)
+        V = np.stack(vals, axis=1)
+        M = np.stack(masks, axis=1)
+        s0, s1 = indptr[c0], indptr[c0 + g.size]
+        indices[s0:s1] = C[M]
+        data[s0:s1] = V[M]
+
+    _pool_map(fill, starts)
+    return indptr, indices, data
+
+
 def banded(N: int, h: int, width: int, seed: int, dtype_index=np.int32) -> sp.csr_matrix:
     """Symmetric random banded SPD matrix (device twin: banded_fill_kernel)."""
-    off = banded_offsets(h, width, seed)
-    g = np.arange(N, dtype=np.int64)
-    cols, vals, masks = [], [], []
-    for o in off[::-1]:  # lower part, ascending column
-        lo = g - o
-        m = lo >= 0
-        cols.append(lo)
-        vals.append(-unit_uniform(seed, np.where(m, lo, 0), o))
-        masks.append(m)
-    upper = []
-    for o in off:
-        hi = g + o
-        m = hi < N
-        upper.append((hi, -unit_uniform(seed, g, o), m))
-    # diagonal: sum of |off| in column order (lower then upper), then + 1
-    s = np.zeros(N)
-    for v, m in zip(vals, masks):
-        s = s + np.where(m, np.abs(v), 0.0)
-    for _, v, m in upper:
-        s = s + np.where(m, np.abs(v), 0.0)
-    cols.append(g); vals.append(s + 1.0); masks.append(np.ones(N, bool))
-    for c, v, m in upper:
-        cols.append(c); vals.append(v); masks.append(m)
-    C = np.stack(cols, axis=1)
-    V = np.stack(vals, axis=1)
-    M = np.stack(masks, axis=1)
-    counts = M.sum(axis=1)
-    indptr = np.zeros(N + 1, dtype=np.int64)
-    np.cumsum(counts, out=indptr[1:])
-    A = sp.csr_matrix((V[M].copy(), C[M].astype(dtype_index), indptr.astype(dtype_index)),
-                      shape=(N, N))
+    indptr, indices, data = banded_arrays(N, h, width, seed)
+    A = sp.csr_matrix((data, indices.astype(dtype_index, copy=False),
+                       indptr.astype(dtype_index, copy=False)), shape=(N, N))
     A.has_sorted_indices = True
     return A
+
+
+class ParCSR:
+    """A CSR operator for the oracle whose ``dot`` is oracle/csrmv.c: every row
+    summed in stored order from 0.0 like scipy's csr_matvec (bitwise; pinned
+    in tests/test_oracle.py), rows spread over OpenMP threads. For the
+    full-size parity tests, where scipy's one-thread matvec over billions of
+    entries would take minutes (C5: 3.15 G entries at N = 50M). Needs
+    oracle/liboracle_csrmv.so (oracle/build.sh, run by build())."""
+
+    _lib = None
+
+    def __init__(self, indptr, indices, data, shape):
+        import ctypes
+        import os
+        if ParCSR._lib is None:
+            path = os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                "liboracle_csrmv.so")
+            lib = ctypes.CDLL(path)
+            P = ctypes.c_void_p
+            lib.oracle_csrmv.argtypes = [ctypes.c_int64, P, P, P, P, P]
+            lib.oracle_csrmv.restype = None
+            ParCSR._lib = lib
+        self.indptr = np.ascontiguousarray(indptr, dtype=np.int64)
+        self.indices = np.ascontiguousarray(indices, dtype=np.int32)
+        self.data = np.ascontiguousarray(data, dtype=np.float64)
+        self.shape = shape
+
+    @classmethod
+    def from_scipy(cls, A):
+        A = A.tocsr()
+        return cls(A.indptr, A.indices, A.data, A.shape)
+
+    def dot(self, v):
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        y = np.empty(self.shape[0], dtype=np.float64)
+        ParCSR._lib.oracle_csrmv(self.shape[0], self.indptr.ctypes.data, self.indices.ctypes.data,
+                                 self.data.ctypes.data, v.ctypes.data, y.ctypes.data)
+        return y
+
+    __matmul__ = dot
 
 
 def csr_digest(A: sp.csr_matrix) -> str:

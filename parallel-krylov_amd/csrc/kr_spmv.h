@@ -2376,7 +2376,6 @@ void spmv_dispatch_epi(const SpmvArgs& a, int nblocks, hipStream_t s) {
   }
 }
 
-#include "kr_csr.h"
 #include "kr_stencil.h"
 
 }  // namespace

@@ -86,6 +86,13 @@ case("p2d16_adaptivekskipmrr_k12", P2D16, "adaptivekskipmrr", k=12)
 # the reference's own history and x (tests/test_gpu_solvers.py picks every
 # manifest case up).
 case("p2d256_cg", ["poisson", 256, 2], "cg")
+# Round 5. The C4 family (3-D 7-point Poisson, k-skip MrR k = 4) into the
+# low-residual regime where the k-skip contract is defined:
+# 64^3 to tol 1e-12, 64 history entries, 18 of them below 1e-8 (envelope up
+# to ~2e-5 there: the k-skip recurrence amplifies rounding near convergence,
+# but every perturbed order keeps the same nosl). b is not stored for
+# N > 65536 (regenerated: default_rng(1).standard_normal(N), conftest).
+case("p3d64_kskipmrr_k4_tol1e-12", ["poisson", 64, 3], "kskipmrr", k=4, tol=1e-12)
 
 
 def build_matrix(spec):
@@ -195,6 +202,8 @@ def main(only=None):
         )
         if x0 is not None:
             out["x0"] = x0
+        if N > 65536:  # b = default_rng(1).standard_normal(N), regenerated by the loader
+            del out["b"]
         if "khistory" in info:
             out["khistory"] = np.asarray(info["khistory"], dtype=np.int64)
         np.savez_compressed(os.path.join(HERE, c["name"] + ".npz"), **out)

@@ -76,3 +76,39 @@ def test_scalar_recurrences_follow_reference_order():
         out = v3cpu.kskipmrr_scalars(k, a.copy(), b.copy(), d.copy())
         assert len(out) == k + 1
         assert all(np.isfinite(z) or True for z, _ in out)
+
+
+def test_parcsr_matvec_is_scipy_bitwise():
+    """oracle.matrices.ParCSR (oracle/csrmv.c: rows over OpenMP threads, each
+    summed in stored order from 0.0) equals scipy's csr_matvec bit for bit --
+    on the golden families, an irregular matrix with empty and long rows, and
+    x with wide exponents -- so the full-size parity tests may use it as the
+    oracle's A.dot."""
+    import scipy.sparse as sp
+    from oracle import matrices
+    rng = np.random.default_rng(7)
+    n = 4001
+    rows = np.repeat(np.arange(n), rng.integers(0, 40, n))
+    rows = np.concatenate([rows, np.full(3000, n // 2)])
+    cols = rng.integers(0, n, rows.size)
+    irr = sp.csr_matrix((rng.standard_normal(rows.size) * 10.0 ** rng.integers(-8, 8, rows.size),
+                         (rows, cols)), shape=(n, n))
+    irr.sum_duplicates()
+    mats = [matrices.poisson(17, 3), matrices.poisson(40, 2), matrices.banded(3000, 31, 256, 0),
+            matrices.banded(2000, 13, 64, 0), irr]
+    for A in mats:
+        x = rng.standard_normal(A.shape[0]) * 10.0 ** rng.integers(-5, 5, A.shape[0])
+        P = matrices.ParCSR.from_scipy(A)
+        np.testing.assert_array_equal(P.dot(x), A.dot(x))
+
+
+def test_banded_arrays_int64_rowptr():
+    """banded_arrays builds the same rows as the scipy matrix with an int64
+    row pointer (C5 at N = 50M has 3.15 G entries) and int32 columns."""
+    from oracle import matrices
+    ip, ix, dt = matrices.banded_arrays(5000, 31, 256, 3)
+    A = matrices.banded(5000, 31, 256, 3)
+    assert ip.dtype == np.int64 and ix.dtype == np.int32
+    np.testing.assert_array_equal(ip, A.indptr)
+    np.testing.assert_array_equal(ix, A.indices)
+    np.testing.assert_array_equal(dt, A.data)

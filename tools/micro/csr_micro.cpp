@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../../parallel-krylov_amd/csrc/kr_spmv.h"
+#include "csr_variants.h"
 
 #define CK(x)                                                           \
   do {                                                                  \

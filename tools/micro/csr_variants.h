@@ -1,4 +1,11 @@
-// CSR row walk without LDS (spmv_kernel_direct; included by kr_spmv.h).
+// Round-5 experiments on the plain-CSR SpMV (included by csr_micro.cpp only,
+// after kr_spmv.h; not part of the library). Results in profiles/r05a/README.txt:
+// the LDS-free walk, fewer requested bytes (diagonal reuse, one row-pointer
+// load, exact staging), paired and sc1 stores and a two-deep staging pipeline
+// were all within noise or slower; non-temporal stores (-5 %) went into
+// spmv_kernel2.
+//
+// CSR row walk without LDS (spmv_kernel_direct).
 //
 // The plain-CSR SpMV (column stream + 8-byte values: no offset masks, no
 // value dictionary, no stencil codes) of short-row shards. One lane owns one
@@ -24,8 +31,10 @@
 // finish in a plain per-entry loop (correct for any CSR; slow, and not the
 // shape this kernel is chosen for). Replaces cupy's cuSPARSE csrmv of
 // /root/reference/v3/gpu/common.py:119 (MultiGpu.dot) for such shards.
-// Included by kr_spmv.h inside namespace kr's anonymous namespace.
 #pragma once
+
+namespace kr {
+namespace {
 
 // KC entries per lane from the row's aligned chunks: NVL double2 loads cover
 // 2*NVL >= KC + 1 entries from the even entry at or below the row start, NCL
@@ -729,3 +738,6 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel4(SpmvArgs a) {
   __syncthreads();
   block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
 }
+
+}  // namespace
+}  // namespace kr
