@@ -1199,7 +1199,7 @@ __device__ __forceinline__ void stage_load2(Stage& st, const double* __restrict_
 // 16 KiB value window); entries are decoded through the LDS table on read.
 template <typename RP, int EPI, bool VEC, int MW, bool DB = true, bool NT = false,
           bool VI = false>
-__global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
+__device__ __forceinline__ void spmv2_body(SpmvArgs& a) {
   if (!spmv_entry<EPI>(a)) return;  // converged / the fused scalar step's test fired
   using T = EpiTraits<EPI>;
   constexpr int NP = T::NP;
@@ -1442,6 +1442,20 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
   block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
 }
 
+template <typename RP, int EPI, bool VEC, int MW, bool DB = true, bool NT = false,
+          bool VI = false>
+__global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
+  spmv2_body<RP, EPI, VEC, MW, DB, NT, VI>(a);
+}
+// The same kernel under its own symbol for products-only duals (the last
+// basis dual of a k-skip outer iteration: no y stores), so rocprofv3 tells
+// its launches from the storing duals' (tools/pmc_summary.py: "_last").
+template <typename RP, int EPI, bool VEC, int MW, bool DB = true, bool NT = false,
+          bool VI = false>
+__global__ __launch_bounds__(kBlock) void spmv_kernel2_po(SpmvArgs a) {
+  spmv2_body<RP, EPI, VEC, MW, DB, NT, VI>(a);
+}
+
 template <typename RP, int E, bool VEC, bool DB, bool NT>
 void spmv2_launch_vi(const SpmvArgs& a, dim3 grid, dim3 block, hipStream_t s) {
   switch (a.mask ? a.mw : 0) {
@@ -1466,7 +1480,15 @@ void spmv2_launch(const SpmvArgs& a, dim3 grid, dim3 block, hipStream_t s) {
     case 16: spmv_kernel2<RP, E, VEC, 16, DB, NT><<<grid, block, 0, s>>>(a); return;
     case 32: spmv_kernel2<RP, E, VEC, 32, DB, NT><<<grid, block, 0, s>>>(a); return;
     case 64: spmv_kernel2<RP, E, VEC, 64, DB, NT><<<grid, block, 0, s>>>(a); return;
-    default: spmv_kernel2<RP, E, VEC, 0, DB, NT><<<grid, block, 0, s>>>(a); return;
+    default:
+      if constexpr (EpiTraits<E>::NV == 2 && !is_step<E>()) {
+        if (a.products_only) {  // plain CSR: its own symbol (profiles)
+          spmv_kernel2_po<RP, E, VEC, 0, DB, NT><<<grid, block, 0, s>>>(a);
+          return;
+        }
+      }
+      spmv_kernel2<RP, E, VEC, 0, DB, NT><<<grid, block, 0, s>>>(a);
+      return;
   }
 }
 

@@ -26,6 +26,9 @@ EW = ["dot", "update_mrr_first", "update_mrr", "update_cg", "update_cg_p", "upda
 
 
 def short(name):
+    m = re.search(r"spmv_kernel2_po<(\w+), (\d+), (\w+)", name)
+    if m:  # the plain-CSR row walk's products-only dual (engine name ..._last)
+        return EPI[int(m.group(2))] + "_last" + ("" if m.group(1) == "int" else "_rp64")
     m = re.search(r"spmv_kernel\w*<(\w+), (\d+), (\w+)", name)
     if m:
         return EPI[int(m.group(2))] + ("" if m.group(1) == "int" else "_rp64")
