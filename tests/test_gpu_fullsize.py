@@ -66,6 +66,31 @@ def test_fullsize_matches_oracle(name, method, matrix, maxiter):
     assert np.linalg.norm(x - x_ref) <= 1e-12 * np.linalg.norm(x_ref)
 
 
+def _oracle_blocked_dots(method, A, b, **kw):
+    """The oracle with every dot / norm summed as 256-element block sums
+    added in block order (a GPU-like order; make_golden.py's blocked_dot,
+    vectorised): its distance from the plain oracle is the rounding
+    envelope of the §8(c) contract."""
+    import math
+    from oracle import v3cpu
+
+    def dot(u, v):
+        p = np.asarray(u, dtype=np.float64) * np.asarray(v, dtype=np.float64)
+        pad = (-p.size) % 256
+        if pad:
+            p = np.concatenate([p, np.zeros(pad)])
+        parts = p.reshape(-1, 256).sum(axis=1)
+        return np.float64(np.cumsum(parts)[-1])
+
+    saved = (v3cpu._dot, v3cpu._norm)
+    v3cpu._dot = dot
+    v3cpu._norm = lambda v: np.float64(math.sqrt(dot(v, v)))
+    try:
+        return method(A, b, **kw)
+    finally:
+        v3cpu._dot, v3cpu._norm = saved
+
+
 def _host_budget_bytes():
     """Memory the box lets one command use: MemAvailable, capped at 200 GiB
     (the GPU box's per-command host-memory cap is ~270 GiB)."""
@@ -101,14 +126,23 @@ def test_c5_fullsize_matches_oracle():
     sysm.close()
     A = matrices.ParCSR(*matrices.banded_arrays(n, 31, 256, 0), shape=(n, n))
     x_ref, ref = v3cpu.adaptivekskipmrr(A, bh, tol=0.0, maxiter=11, k=4)
-    msg = f"C5 parity at N = {n}"
+    # the envelope (as the golden fixtures measure it): the
+    # oracle again with its dots summed in 256-element blocks (a GPU-like
+    # order); x of a k-skip method moves far more under re-ordering than the
+    # residual history does (its coefficients come from the Gram recurrence)
+    x_p, ref_p = _oracle_blocked_dots(v3cpu.adaptivekskipmrr, A, bh, tol=0.0, maxiter=11, k=4)
+    env = np.abs(ref_p["residual"] - ref["residual"]) / np.abs(ref["residual"])
+    x_env = np.linalg.norm(x_p - x_ref) / np.linalg.norm(x_ref)
+    msg = f"C5 parity at N = {n} (envelope max {env.max():.1e}, x envelope {x_env:.1e})"
     assert list(ref["nosl"]) == [0, 1, 6, 11], msg
     np.testing.assert_array_equal(info["nosl"], ref["nosl"], err_msg=msg)
     np.testing.assert_array_equal(info["khistory"], ref["khistory"], err_msg=msg)
     rel = np.abs(info["residual"] - ref["residual"]) / np.abs(ref["residual"])
-    assert rel.max() <= 1e-12, (msg, rel)
-    assert np.linalg.norm(x - x_ref) <= 1e-11 * np.linalg.norm(x_ref), msg
-    print(f"{msg}: max rel {rel.max():.2e}, residual {ref['residual'][-1]:.6e}")
+    assert np.all(rel <= np.maximum(1e-12, 10.0 * env)), (msg, rel)
+    xrel = np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref)
+    assert xrel <= max(1e-11, 10.0 * x_env), (msg, xrel)
+    print(f"{msg}: residual max rel {rel.max():.2e}, x rel {xrel:.2e}, "
+          f"final residual {ref['residual'][-1]:.6e}")
 
 
 def test_c5_fullsize_true_residual():
