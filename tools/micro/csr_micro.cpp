@@ -240,6 +240,17 @@ void run_k4(Ctx& c, int grid, const char* name) {
   report(c, name, grid, ms);
 }
 
+template <int E, bool VL = false>
+void run_k5(Ctx& c, int grid, const char* name) {
+  CK(hipMemset(c.y1, 0, c.n * 8));
+  CK(hipMemset(c.y2, 0, c.n * 8));
+  SpmvArgs a = args_for(c, grid);
+  const float ms = time_it(c, [&] {
+    spmv_kernel5<int32_t, E, VL><<<grid, kBlock>>>(a);
+  });
+  report(c, name, grid, ms);
+}
+
 int main(int argc, char** argv) {
   Ctx c;
   c.ns = argc > 1 ? atoll(argv[1]) : 512;
@@ -340,6 +351,13 @@ int main(int argc, char** argv) {
     run_k3<EPI_DUAL_MRR, 16 + 256>(c, g8, "kernel3 NT single-buf");
     run_k3<EPI_DUAL_MRR, 16 + 256 + 64 + 128>(c, g8, "kernel3 NT SB no st/gathers");
     run_k3<EPI_DUAL_MRR, 16 + 7>(c, g8, "kernel3 NT + diag/rp1/buf");
+  }
+  if (on("k5")) {
+    run_k2<EPI_DUAL_MRR, 1, 1>(c, g8, "kernel2 dual_mrr DB NT (default)");
+    run_k5<EPI_DUAL_MRR>(c, g8, "kernel5 gathers one block ahead");
+    run_k5<EPI_DUAL_MRR>(c, 4096, "kernel5 gathers one block ahead");
+    run_k5<EPI_DUAL_MRR, true>(c, g8, "kernel5 VL (values from LDS)");
+    run_k5<EPI_DUAL_MRR, true>(c, 4096, "kernel5 VL (values from LDS)");
   }
   if (on("k4")) {
     run_k4<EPI_DUAL_MRR, 0>(c, g8, "kernel4 depth-2 staging");

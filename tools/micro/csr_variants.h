@@ -741,3 +741,170 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel4(SpmvArgs a) {
 
 }  // namespace
 }  // namespace kr
+
+namespace kr {
+namespace {
+
+// ---------------------------------------------------------------------------
+// CSR row walk v5 (spmv_kernel5, round 5 experiment): the x gathers software-
+// pipelined one row block ahead. Visit t commits block t+1's staged window,
+// reads its values and columns out of LDS into registers and issues its x
+// gathers, issues the staging loads of block t+2, and only then sums block t
+// from the values and gathers it read one visit earlier -- so a gather's
+// latency and the staging's both overlap a whole visit of work instead of
+// the gathers' being waited for in the visit that issued them. Two register
+// sets (values + gathers) alternate (loop unrolled x2); one window per block
+// (the host checks the largest block); rows longer than G entries finish
+// from the LDS window, behind one more barrier in the visits that have them.
+// ---------------------------------------------------------------------------
+template <int NV, bool VL = false>
+struct GSet {
+  double v[VL ? 1 : kGather], p1[kGather], p2[NV == 2 ? kGather : 1];
+  int js = 0, je = 0;
+  int64_t row = 0;
+  bool active = false;
+  EpiIn pin;
+};
+
+// VL: the values are read from the LDS window when the block is finished
+// (not kept in registers across the visit: 14 VGPRs per set fewer), which
+// needs a second barrier per visit (the window must outlive every wave's
+// finish before the next commit overwrites it).
+template <typename RP, int EPI, bool VL = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void spmv_kernel5(SpmvArgs a) {
+  if (!spmv_entry<EPI>(a)) return;
+  using T = EpiTraits<EPI>;
+  constexpr int NP = T::NP;
+  constexpr int NV = T::NV;
+  constexpr int G = kGather;
+  static_assert(!is_virtual<EPI>(), "experiment: plain inputs only");
+  __shared__ __attribute__((aligned(16))) double s_val[2][kWindow];
+  __shared__ __attribute__((aligned(16))) int32_t s_col[2][kWindow];
+  __shared__ double s_red[(NP > 0 ? NP : 1) * 4];
+
+  const RP* __restrict__ rowptr = static_cast<const RP*>(a.rowptr);
+  const double* __restrict__ val = a.val;
+  const int32_t* __restrict__ col = a.col;
+  const double* __restrict__ x1 = a.x1;
+  const double* __restrict__ x2 = a.x2;
+  const int tid = threadIdx.x;
+
+  double acc[NP > 0 ? NP : 1];
+#pragma unroll
+  for (int p = 0; p < (NP > 0 ? NP : 1); ++p) acc[p] = 0.0;
+
+  const int64_t nrb = (a.n + kBlock - 1) / kBlock - a.rb_gap;
+  RowSched sched;
+  sched.init(nrb, a.slab, a.slab_sub, true);
+  sched.gap_at = a.rb_gap_at;
+  sched.gap = a.rb_gap;
+  const int64_t jstep = sched.jstep, jcount = sched.jcount;
+  if (sched.j0 >= jcount) {
+    block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
+    return;
+  }
+  const int64_t jlast = sched.j0 + ((jcount - 1 - sched.j0) / jstep) * jstep;
+  auto bounds = [&](Blk<RP>& b, int64_t jj) __attribute__((always_inline)) {
+    b.valid = jj < jcount;
+    const int64_t rb = sched.rb(min(jj, jlast));
+    b.r0 = rb * kBlock;
+    b.nr = (int)min((int64_t)kBlock, a.n - b.r0);
+    b.bs = (int64_t)load_uniform(rowptr, b.r0);
+    b.be = (int64_t)load_uniform(rowptr, b.r0 + b.nr);
+  };
+  auto lane_rp = [&](Blk<RP>& b) __attribute__((always_inline)) {
+    const int64_t ri = min(b.r0 + tid, a.n - 1);
+    b.lo = rowptr[ri];
+    b.hi = rowptr[ri + 1];
+  };
+  Stage st;
+  auto stage = [&](const Blk<RP>& b) __attribute__((always_inline)) {
+    stage_load2<true, true>(st, val, col, b.bs & ~(int64_t)3, b.be, tid);
+  };
+
+  // gathers of block b from LDS buffer `buf` into set g (b's window committed)
+  auto gather = [&](GSet<NV, VL>& g, const Blk<RP>& b, int buf) __attribute__((always_inline)) {
+    const double* sv = s_val[buf];
+    const int32_t* sc = s_col[buf];
+    g.active = tid < b.nr && b.valid;
+    g.row = b.r0 + (g.active ? tid : 0);
+    const int64_t ws = b.bs & ~(int64_t)3;
+    g.js = g.active ? (int)((int64_t)b.lo - ws) : 0;
+    g.je = g.active ? (int)((int64_t)b.hi - ws) : 0;
+    g.pin = epi_load<EPI>(a, g.row);
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const bool ok = g.js + u < g.je;
+      if constexpr (!VL) g.v[u] = sv[ok ? g.js + u : 0];
+      const int64_t c = sc[ok ? g.js + u : 0];
+      g.p1[u] = x1[c];
+      if constexpr (NV == 2) g.p2[u] = x2[c];
+    }
+    (void)sv;
+  };
+  // sums + epilogue of the block whose gathers are in g (window still in `buf`)
+  auto finish = [&](GSet<NV, VL>& g, int buf) __attribute__((always_inline)) {
+    double sum1 = 0.0, sum2 = 0.0;
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const bool ok = g.js + u < g.je;
+      const double vu = VL ? s_val[buf][ok ? g.js + u : 0] : g.v[VL ? 0 : u];
+      if (ok) {
+        sum1 = sum1 + vu * g.p1[u];
+        if constexpr (NV == 2) sum2 = sum2 + vu * g.p2[u];
+      }
+    }
+    if (g.je - g.js > G) row_window<NV, G>(s_val[buf], s_col[buf], x1, x2, g.js + G, g.je, sum1, sum2);
+    if (g.active)
+      epi_store_row_k<EPI, 1>(a, g.row, epi_values<EPI>(a, sum1, sum2, g.pin, acc));
+  };
+
+  // prologue: block t0 staged + committed + gathered; block t0+1 staged
+  Blk<RP> b0, b1, b2;
+  int64_t j = sched.j0;
+  bounds(b0, j);
+  lane_rp(b0);
+  stage(b0);
+  bounds(b1, j + jstep);
+  lane_rp(b1);
+  GSet<NV, VL> gA, gB;
+  stage_commit<true>(st, s_val[0], s_col[0], tid);
+  int lng = __syncthreads_or(b0.valid && tid < b0.nr && (int64_t)(b0.hi - b0.lo) > G);
+  gather(gA, b0, 0);
+  stage(b1);
+  bounds(b2, j + 2 * jstep);
+  int buf = 0;  // LDS buffer of the block being finished
+
+  // visit: finish the block in `cur` (window in buf), gather the next one
+  // (its stage arrives now) into `nxt`
+  auto visit = [&](GSet<NV, VL>& cur, GSet<NV, VL>& nxt) __attribute__((always_inline)) {
+    const int nb = buf ^ 1;
+    stage_commit<true>(st, s_val[nb], s_col[nb], tid);
+    const int lng_n =
+        __syncthreads_or(b1.valid && tid < b1.nr && (int64_t)(b1.hi - b1.lo) > G);
+    gather(nxt, b1, nb);
+    // the stage of the block after next (its bounds read one visit ago)
+    b1 = b2;
+    lane_rp(b1);
+    stage(b1);
+    bounds(b2, j + 3 * jstep);
+    finish(cur, buf);
+    // a long row read the finished window from LDS: nobody may overwrite it
+    // (the next commit targets it) before every wave is done
+    if (VL || lng) __syncthreads();
+    lng = lng_n;
+    buf = nb;
+    j += jstep;
+  };
+  for (;;) {
+    visit(gA, gB);
+    if (j >= jcount) break;
+    visit(gB, gA);
+    if (j >= jcount) break;
+  }
+  __syncthreads();
+  block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
+}
+
+}  // namespace
+}  // namespace kr
