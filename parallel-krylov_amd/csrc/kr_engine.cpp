@@ -1930,6 +1930,7 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
     a.products_only = po_shard(s) ? 1 : 0;
     a.stop = dev_stop ? s.st + ST_STOP : nullptr;
     a.nnz_total = s.nnz;
+    a.nt_stores = KR_ENV("KR_DIA_NTS", 0);  // DIA kernels: non-temporal result stores (A/B)
     if (s.dense) {
       a.dense = 1;
       a.val = s.dense + r_begin * s.dld;

@@ -1907,7 +1907,13 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(SpmvArgs a) {
         }
       }
     }
-    if (active) epi_row_in<EPI>(a, row, sum1, sum2, x1, x2, pin, acc);
+    if (active) {
+      const EpiVals o = epi_values<EPI>(a, sum1, sum2, pin, acc);
+      if (a.nt_stores)  // uniform (SpmvArgs::nt_stores)
+        epi_store_row_k<EPI, 1>(a, row, o);
+      else
+        epi_store_row_k<EPI, 0>(a, row, o);
+    }
   }
   __syncthreads();
   block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
@@ -2221,7 +2227,13 @@ __global__ __launch_bounds__(kBlock, NH > 15 ? 2 : 1) void spmv_diawalk_kernel(S
       pin.x2 = own2;
       pin.e = own3;
     }
-    if (active) epi_row_in<EPI>(a, row, sum1, sum2, a.x1, a.x2, pin, acc);
+    if (active) {
+      const EpiVals o = epi_values<EPI>(a, sum1, sum2, pin, acc);
+      if (a.nt_stores)  // uniform (SpmvArgs::nt_stores)
+        epi_store_row_k<EPI, 1>(a, row, o);
+      else
+        epi_store_row_k<EPI, 0>(a, row, o);
+    }
     __syncthreads();
   }
   __syncthreads();
