@@ -214,8 +214,10 @@ struct SpmvArgs {
   // the fused basis pair (launch_spmv_stencil2): products of the second dual
   double* partials2 = nullptr;
   int64_t nnz_total = -1;  // entries of val/col (-1: unknown; spmv_kernel2 needs >= 4)
-  // 1: the diagonal-offset kernels store their results non-temporally
-  // (KR_DIA_NTS, A/B; the row walks and the stencil walk do by default)
+  // 1: the row walks and the diagonal-offset kernels store their results
+  // non-temporally (System::spmv: row walks of shards >= 4M rows, whose
+  // outputs outlive the caches anyway; KR_NT_STORES=0/1 forces it; the
+  // stencil walk has its own NTM bit)
   int nt_stores = 0;
   // Dense row block (gemv_kernel): val is n x ncols row-major with leading
   // dimension dld; x1 + xcol0 (x2 + xcol0) is the full input vector.

@@ -1415,8 +1415,13 @@ __device__ __forceinline__ void spmv2_body(SpmvArgs& a) {
       first_window = false;
       continue;
     }
-    if (active)
-      epi_store_row_k<EPI, NT ? 1 : 0>(a, r0 + tid, epi_values<EPI>(a, sum1, sum2, pin, acc));
+    if (active) {
+      const EpiVals o = epi_values<EPI>(a, sum1, sum2, pin, acc);
+      if (a.nt_stores)  // uniform (SpmvArgs::nt_stores: large shards)
+        epi_store_row_k<EPI, 1>(a, r0 + tid, o);
+      else
+        epi_store_row_k<EPI, 0>(a, r0 + tid, o);
+    }
     if (!has_next) break;
     // advance to the next row block; its boundaries after it come through
     // the scalar cache now (used one row block later)

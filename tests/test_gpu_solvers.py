@@ -521,3 +521,41 @@ def test_dense_fused_steps_bitwise_equal_unfused(monkeypatch, shards):
     x1, i1 = _run_env(monkeypatch, {**base, "KR_FUSE": "1"}, "kskipmrr", A, b, **kw)
     np.testing.assert_array_equal(i1["residual"], i0["residual"])
     np.testing.assert_array_equal(x1, x0)
+
+
+@pytest.mark.parametrize("streams", ["1", "0"], ids=["shared-stream", "stream-per-shard"])
+def test_kernel_stats_device_windows(monkeypatch, streams):
+    """kr_solve_kernel_stats (ABI 204) with three in-process shards of one
+    device: every SpMV record covers all three shards (`shards` = 3) with their
+    algorithmic bytes summed, one record per call, whether the shards share a
+    stream (one window per group) or run on a stream each (overlapping
+    windows merged into the device's), so bench.py's rates are the device's
+    in both layouts (round-4 review item 3)."""
+    from parallel_krylov_amd.system import KrylovSystem, balanced_partition
+    monkeypatch.setenv("KR_SHARED_STREAM", streams)
+    A = golden_matrix(["poisson", 32, 3])
+    n = A.shape[0]
+    part = balanced_partition(n, 3)
+    sysm = KrylovSystem(n, part, [0, 0, 0])
+    try:
+        sysm.set_matrix(A)
+        sysm.finalize()
+        b = sysm.split(np.random.default_rng(2).standard_normal(n))
+        k, outer = 4, 6
+        sysm.begin("kskipmrr", b, None, tol=0.0, maxiter=outer * (k + 1) + 1, k=k, profile=1)
+        sysm.step(outer)
+        st = {r["name"]: r for r in sysm.kernel_stats()}
+        sysm.finish("kskipmrr")
+    finally:
+        sysm.close()
+    dual = st["spmv2_gram_mrr"]
+    assert dual["shards"] == 3, st
+    # one record per call: 3 storing duals per outer iteration (the 4th is
+    # products-only), over the profiled outer iterations
+    assert dual["launches"] % 3 == 0 and dual["launches"] >= 3 * (outer - 1), dual
+    nnz = [A[part[s]:part[s + 1]].nnz for s in range(3)]
+    rows = [part[s + 1] - part[s] for s in range(3)]
+    want = sum(12.0 * z + 4.0 * (r + 1) + 32.0 * r for z, r in zip(nnz, rows))
+    assert dual["bytes_per_launch"] == want, (dual, want)
+    assert st["spmv2_gram_mrr_last"]["shards"] == 3
+    assert all(r["total_ms"] > 0 for r in st.values() if r["launches"])

@@ -175,6 +175,7 @@ SpmvArgs args_for(const Ctx& c, int grid) {
   a.partials = c.part;
   a.grid = grid;
   a.nnz_total = c.nnz;
+  a.nt_stores = 1;  // the engine's choice for a shard this size
   return a;
 }
 
@@ -342,6 +343,12 @@ int main(int argc, char** argv) {
     run_k3<EPI_DUAL_MRR, 24>(c, g8, "kernel3 FL24 pairs NT");
     run_k3<EPI_DUAL_MRR, 15>(c, g8, "kernel3 FL15 all+pairs");
     run_k3<EPI_DUAL_MRR, 31>(c, g8, "kernel3 FL31 all+pairs NT");
+  }
+  if (on("ntcmp")) {  // the library's runtime NT-store switch vs the compile-time one
+    for (int r = 0; r < 2; ++r) {
+      run_k2<EPI_DUAL_MRR, 1, 1>(c, g8, "kernel2 (runtime nt_stores=1)");
+      run_k3<EPI_DUAL_MRR, 16>(c, g8, "kernel3 FL16 (compile-time NT)");
+    }
   }
   if (on("k3ab")) {
     run_k3<EPI_DUAL_MRR, 16>(c, g8, "kernel3 FL16 NT stores");
