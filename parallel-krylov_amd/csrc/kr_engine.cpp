@@ -1933,7 +1933,8 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
     // Non-temporal result stores: the row walks of large shards (a plain-CSR
     // dual at 512^3 -5 %; C1's 64k rows, whose vectors stay in L2/MALL for
     // the next kernel, lost 8 % with them); not the DIA kernels (C3 / C5
-    // neutral, profiles/r05b/dia_nts). KR_NT_STORES=0/1 forces either.
+    // neutral as an A/B build, profiles/r05b/dia_nts). KR_NT_STORES=0/1
+    // forces either.
     {
       const int e = KR_ENV("KR_NT_STORES", -1);
       a.nt_stores = e >= 0 ? e : (!s.dia && s.n >= ((int64_t)1 << 22)) ? 1 : 0;

@@ -214,8 +214,8 @@ struct SpmvArgs {
   // the fused basis pair (launch_spmv_stencil2): products of the second dual
   double* partials2 = nullptr;
   int64_t nnz_total = -1;  // entries of val/col (-1: unknown; spmv_kernel2 needs >= 4)
-  // 1: the row walks and the diagonal-offset kernels store their results
-  // non-temporally (System::spmv: row walks of shards >= 4M rows, whose
+  // 1: the short-row row walk runs its non-temporal variant (matrix stream
+  // and result stores; System::spmv sets it for shards >= 4M rows, whose
   // outputs outlive the caches anyway; KR_NT_STORES=0/1 forces it; the
   // stencil walk has its own NTM bit)
   int nt_stores = 0;

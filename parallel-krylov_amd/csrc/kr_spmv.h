@@ -1415,13 +1415,12 @@ __device__ __forceinline__ void spmv2_body(SpmvArgs& a) {
       first_window = false;
       continue;
     }
-    if (active) {
-      const EpiVals o = epi_values<EPI>(a, sum1, sum2, pin, acc);
-      if (a.nt_stores)  // uniform (SpmvArgs::nt_stores: large shards)
-        epi_store_row_k<EPI, 1>(a, r0 + tid, o);
-      else
-        epi_store_row_k<EPI, 0>(a, r0 + tid, o);
-    }
+    // NT: the matrix stream AND the result stores non-temporal (variant 13,
+    // chosen at launch for shards >= 4M rows: SpmvArgs::nt_stores). A
+    // run-time choice between the two stores measured 2.6 % slower on the
+    // plain-CSR dual (a store under a branch shifts the compiler's waits).
+    if (active)
+      epi_store_row_k<EPI, NT ? 1 : 0>(a, r0 + tid, epi_values<EPI>(a, sum1, sum2, pin, acc));
     if (!has_next) break;
     // advance to the next row block; its boundaries after it come through
     // the scalar cache now (used one row block later)
@@ -1912,13 +1911,7 @@ __global__ __launch_bounds__(kBlock) void spmv_dia_kernel(SpmvArgs a) {
         }
       }
     }
-    if (active) {
-      const EpiVals o = epi_values<EPI>(a, sum1, sum2, pin, acc);
-      if (a.nt_stores)  // uniform (SpmvArgs::nt_stores)
-        epi_store_row_k<EPI, 1>(a, row, o);
-      else
-        epi_store_row_k<EPI, 0>(a, row, o);
-    }
+    if (active) epi_row_in<EPI>(a, row, sum1, sum2, x1, x2, pin, acc);
   }
   __syncthreads();
   block_reduce_store<NP>(acc, a.partials, a.grid, s_red, a.accumulate);
@@ -2232,13 +2225,7 @@ __global__ __launch_bounds__(kBlock, NH > 15 ? 2 : 1) void spmv_diawalk_kernel(S
       pin.x2 = own2;
       pin.e = own3;
     }
-    if (active) {
-      const EpiVals o = epi_values<EPI>(a, sum1, sum2, pin, acc);
-      if (a.nt_stores)  // uniform (SpmvArgs::nt_stores)
-        epi_store_row_k<EPI, 1>(a, row, o);
-      else
-        epi_store_row_k<EPI, 0>(a, row, o);
-    }
+    if (active) epi_row_in<EPI>(a, row, sum1, sum2, a.x1, a.x2, pin, acc);
     __syncthreads();
   }
   __syncthreads();
@@ -2378,13 +2365,20 @@ void spmv_dispatch_epi(const SpmvArgs& a, int nblocks, hipStream_t s) {
   const int forced = KR_ENV("KR_SPMV_VARIANT", -1);
   // Two-vector long-row SpMVs stay on v1: v2's extra gather registers cost a
   // wave per SIMD there (144 VGPRs) and it measured 7 % slower (C5 dual).
-  int variant = forced >= 0 ? forced : (a.long_rows ? (EpiTraits<E>::NV == 1 ? 14 : 8) : 13);
+  // short rows: v2 with the non-temporal matrix stream and result stores on
+  // large shards (13), plain loads and stores on small ones (10), whose
+  // vectors the next kernel finds in L2 / MALL (C1: +2.4 %)
+  int variant = forced >= 0 ? forced
+                            : (a.long_rows ? (EpiTraits<E>::NV == 1 ? 14 : 8) : a.nt_stores ? 13 : 10);
   // the v2 kernels need 16-byte aligned bases and >= 4 entries
   if (variant >= 10 && (!VEC || a.nnz_total < 4)) variant = a.long_rows ? 8 : 0;
   if constexpr (is_virtual<E>()) {  // implemented by the row walk v2 only
     if (!VEC || a.nnz_total < 4 || a.dense)
       throw Failure(KR_ERR_INVALID, "fused first step needs the row walk v2");
-    spmv2_launch<RP, E, VEC, true, true>(a, grid, block, s);
+    if (a.nt_stores)
+      spmv2_launch<RP, E, VEC, true, true>(a, grid, block, s);
+    else
+      spmv2_launch<RP, E, VEC, true, false>(a, grid, block, s);
     return;
   } else {
     if constexpr (VEC) {

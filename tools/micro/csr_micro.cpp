@@ -344,9 +344,9 @@ int main(int argc, char** argv) {
     run_k3<EPI_DUAL_MRR, 15>(c, g8, "kernel3 FL15 all+pairs");
     run_k3<EPI_DUAL_MRR, 31>(c, g8, "kernel3 FL31 all+pairs NT");
   }
-  if (on("ntcmp")) {  // the library's runtime NT-store switch vs the compile-time one
+  if (on("ntcmp")) {  // the library's NT variant vs kernel3 FL16
     for (int r = 0; r < 2; ++r) {
-      run_k2<EPI_DUAL_MRR, 1, 1>(c, g8, "kernel2 (runtime nt_stores=1)");
+      run_k2<EPI_DUAL_MRR, 1, 1>(c, g8, "kernel2 NT (compile-time NT stores)");
       run_k3<EPI_DUAL_MRR, 16>(c, g8, "kernel3 FL16 (compile-time NT)");
     }
   }
