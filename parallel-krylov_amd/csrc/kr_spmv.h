@@ -431,7 +431,22 @@ __device__ __forceinline__ EpiVals epi_values(const SpmvArgs& a, double sum1, do
   return o;
 }
 
-template <int EPI>
+// POM: how a two-vector SpMV honours SpmvArgs::products_only (outputs nobody
+// reads: no y stores). -1 tests it at run time; 0 / 1 are kernels the host
+// launches only for storing / products-only SpMVs (no store under a run-time
+// branch: such a branch shifts the compiler's vmcnt waits, 2.6 % on the
+// plain-CSR dual).
+template <int EPI, int POM>
+__device__ __forceinline__ bool epi_po_skip(const SpmvArgs& a) {
+  if constexpr (EpiTraits<EPI>::NV != 2 || is_step<EPI>() || POM == 0)
+    return false;
+  else if constexpr (POM == 1)
+    return true;
+  else
+    return a.products_only != 0;
+}
+
+template <int EPI, int POM = -1>
 __device__ __forceinline__ void epi_store_row(const SpmvArgs& a, int64_t row, const EpiVals& o) {
   if constexpr (is_step<EPI>()) {
     if constexpr (epi_writes_ud<EPI>()) a.ud[row] = o.ud;
@@ -440,10 +455,7 @@ __device__ __forceinline__ void epi_store_row(const SpmvArgs& a, int64_t row, co
     a.y1[row] = o.y1;
     if constexpr (EPI == EPI_MRR_V) a.y2[row] = o.y2;
   } else {
-    // a two-vector SpMV whose outputs nobody reads (SpmvArgs::products_only:
-    // the windowed diagonal-offset kernel; the stencil kernel stores pairs)
-    if constexpr (EpiTraits<EPI>::NV == 2)
-      if (a.products_only) return;
+    if (epi_po_skip<EPI, POM>(a)) return;
     a.y1[row] = o.y1;
     if constexpr (EpiTraits<EPI>::NV == 2) a.y2[row] = o.y2;
     if constexpr (EPI == EPI_XY_VP) a.u1[row] = o.u1;
@@ -465,7 +477,7 @@ __device__ __forceinline__ void st1(double* p, double v) {
   else
     *p = v;
 }
-template <int EPI, int SK>
+template <int EPI, int SK, int POM = -1>
 __device__ __forceinline__ void epi_store_row_k(const SpmvArgs& a, int64_t row, const EpiVals& o) {
   if constexpr (is_step<EPI>()) {
     if constexpr (epi_writes_ud<EPI>()) st1<SK>(a.ud + row, o.ud);
@@ -474,8 +486,7 @@ __device__ __forceinline__ void epi_store_row_k(const SpmvArgs& a, int64_t row, 
     st1<SK>(a.y1 + row, o.y1);
     if constexpr (EPI == EPI_MRR_V) st1<SK>(a.y2 + row, o.y2);
   } else {
-    if constexpr (EpiTraits<EPI>::NV == 2)
-      if (a.products_only) return;
+    if (epi_po_skip<EPI, POM>(a)) return;
     st1<SK>(a.y1 + row, o.y1);
     if constexpr (EpiTraits<EPI>::NV == 2) st1<SK>(a.y2 + row, o.y2);
     if constexpr (EPI == EPI_XY_VP) st1<SK>(a.u1 + row, o.u1);
@@ -508,14 +519,14 @@ __device__ __forceinline__ void epi_store_pair(const SpmvArgs& a, int64_t row, c
   }
 }
 
-template <int EPI>
+template <int EPI, int POM = -1>
 __device__ __forceinline__ void epi_row_in(const SpmvArgs& a, int64_t row, double sum1,
                                            double sum2, const double* __restrict__ x1,
                                            const double* __restrict__ x2, const EpiIn& in,
                                            double (&acc)[EpiTraits<EPI>::NP > 0
                                                              ? EpiTraits<EPI>::NP
                                                              : 1]) {
-  epi_store_row<EPI>(a, row, epi_values<EPI>(a, sum1, sum2, in, acc));
+  epi_store_row<EPI, POM>(a, row, epi_values<EPI>(a, sum1, sum2, in, acc));
 }
 
 template <int EPI>
@@ -1198,7 +1209,7 @@ __device__ __forceinline__ void stage_load2(Stage& st, const double* __restrict_
 // multiple of 8) and commits them to an LDS code window (2 KiB instead of the
 // 16 KiB value window); entries are decoded through the LDS table on read.
 template <typename RP, int EPI, bool VEC, int MW, bool DB = true, bool NT = false,
-          bool VI = false>
+          bool VI = false, bool PO = false>
 __device__ __forceinline__ void spmv2_body(SpmvArgs& a) {
   if (!spmv_entry<EPI>(a)) return;  // converged / the fused scalar step's test fired
   using T = EpiTraits<EPI>;
@@ -1420,7 +1431,8 @@ __device__ __forceinline__ void spmv2_body(SpmvArgs& a) {
     // run-time choice between the two stores measured 2.6 % slower on the
     // plain-CSR dual (a store under a branch shifts the compiler's waits).
     if (active)
-      epi_store_row_k<EPI, NT ? 1 : 0>(a, r0 + tid, epi_values<EPI>(a, sum1, sum2, pin, acc));
+      epi_store_row_k<EPI, NT ? 1 : 0, PO ? 1 : 0>(a, r0 + tid,
+                                                   epi_values<EPI>(a, sum1, sum2, pin, acc));
     if (!has_next) break;
     // advance to the next row block; its boundaries after it come through
     // the scalar cache now (used one row block later)
@@ -1449,25 +1461,38 @@ __device__ __forceinline__ void spmv2_body(SpmvArgs& a) {
 template <typename RP, int EPI, bool VEC, int MW, bool DB = true, bool NT = false,
           bool VI = false>
 __global__ __launch_bounds__(kBlock) void spmv_kernel2(SpmvArgs a) {
-  spmv2_body<RP, EPI, VEC, MW, DB, NT, VI>(a);
+  spmv2_body<RP, EPI, VEC, MW, DB, NT, VI, false>(a);
 }
-// The same kernel under its own symbol for products-only duals (the last
-// basis dual of a k-skip outer iteration: no y stores), so rocprofv3 tells
-// its launches from the storing duals' (tools/pmc_summary.py: "_last").
+// Products-only duals (the last basis dual of a k-skip outer iteration: no y
+// stores) as their own kernel, under their own symbol (rocprofv3 tells them
+// from the storing duals: tools/pmc_summary.py "_last").
 template <typename RP, int EPI, bool VEC, int MW, bool DB = true, bool NT = false,
           bool VI = false>
 __global__ __launch_bounds__(kBlock) void spmv_kernel2_po(SpmvArgs a) {
-  spmv2_body<RP, EPI, VEC, MW, DB, NT, VI>(a);
+  spmv2_body<RP, EPI, VEC, MW, DB, NT, VI, true>(a);
+}
+
+// Every spmv_kernel2 launch: the products-only kernel for a products-only
+// dual (spmv_kernel2 itself always stores).
+template <typename RP, int E, bool VEC, int MW, bool DB, bool NT, bool VI = false>
+void spmv2_go(const SpmvArgs& a, dim3 grid, dim3 block, hipStream_t s) {
+  if constexpr (EpiTraits<E>::NV == 2 && !is_step<E>()) {
+    if (a.products_only) {
+      spmv_kernel2_po<RP, E, VEC, MW, DB, NT, VI><<<grid, block, 0, s>>>(a);
+      return;
+    }
+  }
+  spmv_kernel2<RP, E, VEC, MW, DB, NT, VI><<<grid, block, 0, s>>>(a);
 }
 
 template <typename RP, int E, bool VEC, bool DB, bool NT>
 void spmv2_launch_vi(const SpmvArgs& a, dim3 grid, dim3 block, hipStream_t s) {
   switch (a.mask ? a.mw : 0) {
-    case 8: spmv_kernel2<RP, E, VEC, 8, DB, NT, true><<<grid, block, 0, s>>>(a); return;
-    case 16: spmv_kernel2<RP, E, VEC, 16, DB, NT, true><<<grid, block, 0, s>>>(a); return;
-    case 32: spmv_kernel2<RP, E, VEC, 32, DB, NT, true><<<grid, block, 0, s>>>(a); return;
-    case 64: spmv_kernel2<RP, E, VEC, 64, DB, NT, true><<<grid, block, 0, s>>>(a); return;
-    default: spmv_kernel2<RP, E, VEC, 0, DB, NT, true><<<grid, block, 0, s>>>(a); return;
+    case 8: return spmv2_go<RP, E, VEC, 8, DB, NT, true>(a, grid, block, s);
+    case 16: return spmv2_go<RP, E, VEC, 16, DB, NT, true>(a, grid, block, s);
+    case 32: return spmv2_go<RP, E, VEC, 32, DB, NT, true>(a, grid, block, s);
+    case 64: return spmv2_go<RP, E, VEC, 64, DB, NT, true>(a, grid, block, s);
+    default: return spmv2_go<RP, E, VEC, 0, DB, NT, true>(a, grid, block, s);
   }
 }
 
@@ -1480,19 +1505,11 @@ void spmv2_launch(const SpmvArgs& a, dim3 grid, dim3 block, hipStream_t s) {
     }
   }
   switch (a.mask ? a.mw : 0) {
-    case 8: spmv_kernel2<RP, E, VEC, 8, DB, NT><<<grid, block, 0, s>>>(a); return;
-    case 16: spmv_kernel2<RP, E, VEC, 16, DB, NT><<<grid, block, 0, s>>>(a); return;
-    case 32: spmv_kernel2<RP, E, VEC, 32, DB, NT><<<grid, block, 0, s>>>(a); return;
-    case 64: spmv_kernel2<RP, E, VEC, 64, DB, NT><<<grid, block, 0, s>>>(a); return;
-    default:
-      if constexpr (EpiTraits<E>::NV == 2 && !is_step<E>()) {
-        if (a.products_only) {  // plain CSR: its own symbol (profiles)
-          spmv_kernel2_po<RP, E, VEC, 0, DB, NT><<<grid, block, 0, s>>>(a);
-          return;
-        }
-      }
-      spmv_kernel2<RP, E, VEC, 0, DB, NT><<<grid, block, 0, s>>>(a);
-      return;
+    case 8: return spmv2_go<RP, E, VEC, 8, DB, NT>(a, grid, block, s);
+    case 16: return spmv2_go<RP, E, VEC, 16, DB, NT>(a, grid, block, s);
+    case 32: return spmv2_go<RP, E, VEC, 32, DB, NT>(a, grid, block, s);
+    case 64: return spmv2_go<RP, E, VEC, 64, DB, NT>(a, grid, block, s);
+    default: return spmv2_go<RP, E, VEC, 0, DB, NT>(a, grid, block, s);
   }
 }
 
@@ -2001,7 +2018,7 @@ constexpr int kWalkWin = 768;  // x window, rows per vector (band <= 256)
 // behind a run-time bound (the runtime-h version ran at 3 TB/s on C5).
 // (2 workgroups per CU for NH > 15: at most 256 VGPRs; the LDS allows no
 // more anyway)
-template <int EPI, int NH>
+template <int EPI, int NH, bool PO = false>
 __global__ __launch_bounds__(kBlock, NH > 15 ? 2 : 1) void spmv_diawalk_kernel(SpmvArgs a) {
   if (!spmv_entry<EPI>(a)) return;  // converged / the fused scalar step's test fired
   using T = EpiTraits<EPI>;
@@ -2225,7 +2242,7 @@ __global__ __launch_bounds__(kBlock, NH > 15 ? 2 : 1) void spmv_diawalk_kernel(S
       pin.x2 = own2;
       pin.e = own3;
     }
-    if (active) epi_row_in<EPI>(a, row, sum1, sum2, a.x1, a.x2, pin, acc);
+    if (active) epi_row_in<EPI, PO ? 1 : 0>(a, row, sum1, sum2, a.x1, a.x2, pin, acc);
     __syncthreads();
   }
   __syncthreads();
@@ -2238,7 +2255,17 @@ template <int E, int NH>
 void spmv_diawalk_launch_t(const SpmvArgs& a, int nblocks, hipStream_t s) {
   constexpr int nv = EpiTraits<E>::NV;
   const size_t lds = sizeof(double) * ((size_t)(NH + 1) * kBlock + (size_t)nv * kWalkWin);
-  static std::atomic<uint64_t> opted{0};  // per device (opt_in_lds)
+  // products-only duals: their own kernel (the storing one never tests
+  // SpmvArgs::products_only)
+  constexpr bool kPo = EpiTraits<E>::NV == 2 && !is_step<E>();
+  if (kPo && a.products_only) {
+    static std::atomic<uint64_t> opted{0};  // per device (opt_in_lds)
+    if (lds > 64 * 1024)
+      opt_in_lds(opted, reinterpret_cast<const void*>(spmv_diawalk_kernel<E, NH, kPo>), lds);
+    spmv_diawalk_kernel<E, NH, kPo><<<nblocks, kBlock, lds, s>>>(a);
+    return;
+  }
+  static std::atomic<uint64_t> opted{0};
   if (lds > 64 * 1024)
     opt_in_lds(opted, reinterpret_cast<const void*>(spmv_diawalk_kernel<E, NH>), lds);
   spmv_diawalk_kernel<E, NH><<<nblocks, kBlock, lds, s>>>(a);

@@ -38,9 +38,9 @@ def short(name):
     m = re.search(r"spmv_stencil_kernel(?:_w4|_po)?<(\d+)\b", name)
     if m:
         return EPI[int(m.group(1))] + "_stencil"
-    m = re.search(r"spmv_diawalk_kernel<(\d+), \d+>", name)
-    if m:  # the symmetric DIA walk (products-only duals share its name)
-        return EPI[int(m.group(1))] + "_dia"
+    m = re.search(r"spmv_diawalk_kernel<(\d+), \d+(?:, (\w+))?>", name)
+    if m:  # the symmetric DIA walk (PO = true: the products-only dual, ..._last)
+        return EPI[int(m.group(1))] + ("_last" if m.group(2) == "true" else "") + "_dia"
     m = re.search(r"(spmv_dia|gemv)_kernel<(\d+)\b", name)
     if m:
         return EPI[int(m.group(2))] + ("_dia" if m.group(1) == "spmv_dia" else "_dense")
