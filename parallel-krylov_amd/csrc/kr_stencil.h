@@ -757,20 +757,25 @@ inline bool st_dpp(const SpmvArgs& a, bool products_only) {
 // KR_STENCIL_PAIR (bit mask, A/B): 1 products-only duals, 2 storing duals,
 // 4 the single-vector fused steps (is_step), 8 the fused first two steps,
 // 16 every other 7-point launch, 32 the inner +-n line from LDS (n = 512);
-// unset: 2 | 8 | 32 where bit 32 applies, else no pairs.
+// unset: 2 | 4 | 8 | 32 where bit 32 applies, else no pairs.
 template <int E>
 inline bool st_pair(const SpmvArgs& a, int nblocks) {
   if constexpr (E == EPI_XY_VP || E == EPI_MRR_V) {
     return false;
   } else {
-    // Default (unset): the storing duals and the fused first steps, and only
-    // where the inner +-n line can come from LDS (bit 32: n = 512) -- measured
-    // on C4 (one box, three rounds, profiles/r04h): dual 0.838 -> 0.813-0.823
-    // ms, first steps 1.71 -> 1.65 ms, 560.7 -> 563-567 it/s; plain pairs
-    // (the ±n lines loaded by both halves) made the dual 7 % slower instead.
+    // Default (unset): the storing duals, the fused steps and the fused first
+    // steps, and only where the inner +-n line can come from LDS (bit 32: n =
+    // 512) -- measured on C4 (one box, three rounds, profiles/r04h): dual
+    // 0.838 -> 0.813-0.823 ms, first steps 1.71 -> 1.65 ms, 560.7 -> 563-567
+    // it/s; plain pairs (the ±n lines loaded by both halves) made the dual 7 %
+    // slower instead. Round 5 (profiles/r05e/pair_ab.txt, one box, A/B twice):
+    // the steps too (bit 4), spmv_step_mrr_nox 1.049-1.077 -> 1.032 ms, the x2
+    // step 1.40-1.69 (bimodal) -> 1.42-1.43 ms, C4 554.3 -> 558.4-559.0 it/s;
+    // the head (bit 16) 0.58-0.60 -> 0.60 ms and the products-only dual (bit
+    // 1, with or without DPP) 0.59 -> 0.65-0.72 ms stay unpaired.
     const int env = KR_ENV("KR_STENCIL_PAIR", -1);
     const bool lfar = a.st_far[0] == -kSBlock && a.st_far[1] == kSBlock;
-    const int m = env >= 0 ? env : (lfar ? 2 | 8 | 32 : 0);
+    const int m = env >= 0 ? env : (lfar ? 2 | 4 | 8 | 32 : 0);
     constexpr bool dual = E == EPI_DUAL_MRR || E == EPI_DUAL_KCG || E == EPI_DUAL_NONE;
     const int bit = (dual && a.products_only) ? 1
                     : dual                        ? 2
@@ -866,7 +871,9 @@ void spmv_stencil_launch_r(const SpmvArgs& a, int nblocks, hipStream_t s) {
       }
     }
     constexpr bool w4 = !RELOAD && (E == EPI_DUAL_MRR || E == EPI_DUAL_KCG || E == EPI_DUAL_NONE);
-    if (w4 && st_depth() == 2)
+    // KR_STENCIL_DEPTH=2: the duals; 3: every carried 7-point launch (A/B)
+    const int depth = st_depth();
+    if (!RELOAD && (depth == 3 || (w4 && depth == 2)))
       st_launch_pat7<E, RELOAD, 11, false>(a, nblocks, lds, s);
     else if (st_dpp(a, false))
       st_launch_pat7<E, RELOAD, 35, w4>(a, nblocks, lds, s);
