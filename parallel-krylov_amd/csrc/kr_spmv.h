@@ -2009,7 +2009,14 @@ void spmv_dia_launch(const SpmvArgs& a, int nblocks, hipStream_t s) {
 // ---------------------------------------------------------------------------
 constexpr int kWalkWin = 768;  // x window, rows per vector (band <= 256)
 #ifndef KR_DIAW_MODE
-#define KR_DIAW_MODE 1
+#define KR_DIAW_MODE 3
+#endif
+// Ablations for tools/micro/walk_micro (timing only, wrong sums; never in the
+// library build): bit 0 no epilogue products / stores (the sums kept live),
+// 1 no mirror stores, 2 no lower sums, 3 no window reads in the sums, 4 no
+// full-block ballot, 5 no window shift.
+#ifndef KR_DIAW_AB
+#define KR_DIAW_AB 0
 #endif
 
 // NH = h, the number of upper (= lower) offsets, is a template parameter:
@@ -2083,9 +2090,15 @@ __global__ __launch_bounds__(kBlock, NH > 15 ? 2 : 1) void spmv_diawalk_kernel(S
   // head and the tail store of every offset; 1 = junk slot, but a wave whose
   // rows all store the head (or all the tail) of an offset skips the other
   // store (rows wv0 .. wv0+63, wave-uniform tests); 2 = as 1 with
-  // exec-masked stores instead of the junk slot.
+  // exec-masked stores instead of the junk slot; 3 (default) = ONE store per
+  // offset and lane at the top of the block: position (p + o) & 255 takes the
+  // previous block's value when p + o >= 256 (its tail, read by this block)
+  // and this block's value otherwise (its head) -- the same position, so no
+  // select of addresses, no junk slot, no branch (the walk micro put modes
+  // 1's stores at 0.52 of the products-only dual's 2.72 ms: per offset a
+  // readlane, a scalar test and branch and a generic-pointer select).
   auto low_put = [&](bool ok, int slot, int pos, double v) {
-    if constexpr (KR_DIAW_MODE == 2) {
+    if constexpr (KR_DIAW_MODE >= 2) {
       if (ok) s_low[slot * kBlock + pos] = v;
     } else {
       double* d = ok ? s_low + slot * kBlock + pos : s_junk + tid;
@@ -2131,8 +2144,19 @@ __global__ __launch_bounds__(kBlock, NH > 15 ? 2 : 1) void spmv_diawalk_kernel(S
   for (int64_t v = v0; v < v1; ++v) {
     const int64_t b = phys(v);
     const bool start = b != prev + 1;  // uniform
-    // --- the previous block's tails (its rows p + o >= 256 feed this block)
-    if (!start) {
+    if constexpr (KR_DIAW_MODE == 3) {
+      // the previous block's tails and this block's heads, one store each
+      // (this block's values: the loads issued one block ago)
+      if (!start && !(KR_DIAW_AB & 2)) {
+#pragma unroll
+        for (int u = 1; u <= NH; ++u) {
+          const int pos = tid + moff(NH + u);
+          const double val = pos >= kBlock ? up[u] : upn[u];
+          s_low[(NH - u) * kBlock + (pos & (kBlock - 1))] = val;
+        }
+      }
+    } else if (!start && !(KR_DIAW_AB & 2)) {
+      // --- the previous block's tails (its rows p + o >= 256 feed this block)
 #pragma unroll
       for (int u = 1; u <= NH; ++u) {
         const int o = moff(NH + u);
@@ -2175,7 +2199,7 @@ __global__ __launch_bounds__(kBlock, NH > 15 ? 2 : 1) void spmv_diawalk_kernel(S
       for (int k = 0; k < NH; ++k) lw[k] = blk[(int64_t)k * a.dia_ks];
 #pragma unroll
       for (int k = 0; k < NH; ++k) low_put(tid < -moff(k), k, tid, lw[k]);
-    } else {  // shift by one block inside the lane's own slots, append the new row
+    } else if (!(KR_DIAW_AB & 32)) {  // shift by one block inside the lane's own slots, append the new row
 #pragma unroll
       for (int vv = 0; vv < NV; ++vv) {
         double* w = s_win + vv * kWalkWin + tid;
@@ -2190,33 +2214,52 @@ __global__ __launch_bounds__(kBlock, NH > 15 ? 2 : 1) void spmv_diawalk_kernel(S
         nxt1 = c1, nxt2 = c2, nxt3 = c3;
       }
     }
+    if (KR_DIAW_MODE != 3 || start) {
 #pragma unroll
-    for (int u = 1; u <= NH; ++u) {  // heads: rows p + o < 256 of this block
-      const int o = moff(NH + u);
-      if (any_head(o)) low_put(tid + o < kBlock, NH - u, tid + o, up[u]);
+      for (int u = 1; u <= NH; ++u) {  // heads: rows p + o < 256 of this block
+        const int o = moff(NH + u);
+        if (!(KR_DIAW_AB & 2) && any_head(o)) low_put(tid + o < kBlock, NH - u, tid + o, up[u]);
+      }
     }
-    const bool lane_full = active && m == kFull;
-    const uint64_t all = __ballot(lane_full);
-    if ((tid & 63) == 0) s_full[tid >> 6] = all == ~0ull ? 1 : 0;
-    __syncthreads();
-    const bool full = (s_full[0] & s_full[1] & s_full[2] & s_full[3]) != 0;  // uniform
+    bool full = true;
+    if constexpr (KR_DIAW_AB & 16) {
+      __syncthreads();
+    } else {
+      const bool lane_full = active && m == kFull;
+      const uint64_t all = __ballot(lane_full);
+      if ((tid & 63) == 0) s_full[tid >> 6] = all == ~0ull ? 1 : 0;
+      __syncthreads();
+      full = (s_full[0] & s_full[1] & s_full[2] & s_full[3]) != 0;  // uniform
+    }
     // --- the row sums: lower entries (mirrors from LDS), diagonal, upper
     double sum1 = 0.0, sum2 = 0.0;
     const double* wl = s_win + kBlock + tid;  // the row's x: wl[offset]
     const double* ll = s_low + tid;           // lower slot k: ll[k * kBlock]
     if (full) {
+      if constexpr (!(KR_DIAW_AB & 4)) {
 #pragma unroll
-      for (int k = 0; k < NH; ++k) {
-        const double* w = wl + moff(k);
-        const double v = ll[k * kBlock];
-        sum1 = sum1 + v * w[0];
-        if constexpr (NV == 2) sum2 = sum2 + v * w[kWalkWin];
+        for (int k = 0; k < NH; ++k) {
+          const double* w = wl + moff(k);
+          const double v = ll[k * kBlock];
+          if constexpr (KR_DIAW_AB & 8) {
+            sum1 = sum1 + v * 1.5;
+            if constexpr (NV == 2) sum2 = sum2 + v * 0.5;
+          } else {
+            sum1 = sum1 + v * w[0];
+            if constexpr (NV == 2) sum2 = sum2 + v * w[kWalkWin];
+          }
+        }
       }
 #pragma unroll
       for (int u = 0; u <= NH; ++u) {
         const double* w = wl + moff(NH + u);
-        sum1 = sum1 + up[u] * w[0];
-        if constexpr (NV == 2) sum2 = sum2 + up[u] * w[kWalkWin];
+        if constexpr (KR_DIAW_AB & 8) {
+          sum1 = sum1 + up[u] * 1.5;
+          if constexpr (NV == 2) sum2 = sum2 + up[u] * 0.5;
+        } else {
+          sum1 = sum1 + up[u] * w[0];
+          if constexpr (NV == 2) sum2 = sum2 + up[u] * w[kWalkWin];
+        }
       }
     } else {  // absent entries skipped by a select, as every kernel here
       auto add = [&](int k, double v) {
@@ -2242,7 +2285,10 @@ __global__ __launch_bounds__(kBlock, NH > 15 ? 2 : 1) void spmv_diawalk_kernel(S
       pin.x2 = own2;
       pin.e = own3;
     }
-    if (active) epi_row_in<EPI, PO ? 1 : 0>(a, row, sum1, sum2, a.x1, a.x2, pin, acc);
+    if constexpr (KR_DIAW_AB & 1)
+      acc[0] = acc[0] + sum1 * sum2;
+    else if (active)
+      epi_row_in<EPI, PO ? 1 : 0>(a, row, sum1, sum2, a.x1, a.x2, pin, acc);
     __syncthreads();
   }
   __syncthreads();
