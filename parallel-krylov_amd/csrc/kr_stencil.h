@@ -38,6 +38,13 @@
 #ifndef KR_ST_W4
 #define KR_ST_W4 4
 #endif
+// Ablations (timing-only library builds for same-box A/B, wrong results;
+// never in the library build): bit 0 no result stores, 1 no products, 2 no
+// value-table reads (the code itself as the value), 3 the NEAR (+-1)
+// operands from the own row (no LDS line / DPP reads).
+#ifndef KR_ST_AB
+#define KR_ST_AB 0
+#endif
 constexpr int kSBlock = kStencilBlock;  // rows per stencil row block (2 per lane)
 constexpr int kSNear = 2;            // LDS line halo (offsets 0 < |o| <= kSNear)
 constexpr int kSLine = kSBlock + 2 * kSNear;
@@ -525,8 +532,8 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
       const unsigned chi = (unsigned)(cur.chi >> (CB * k)) & kNone;
       // an absent code reads an unused table entry (s_tab has kVdMax
       // slots); its product is dropped below
-      const double vlo = s_tab[clo];
-      const double vhi = s_tab[chi];
+      const double vlo = (KR_ST_AB & 4) ? (double)clo : s_tab[clo];
+      const double vhi = (KR_ST_AB & 4) ? (double)chi : s_tab[chi];
       double xlo[NV], xhi[NV];
       if (kind == SK_CENTER) {
 #pragma unroll
@@ -534,6 +541,9 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
       } else if (kind == SK_PREV) {
 #pragma unroll
         for (int v = 0; v < NV; ++v) { xlo[v] = opp[v].x; xhi[v] = opp[v].y; }
+      } else if (kind == SK_NEAR && (KR_ST_AB & 8)) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) { xlo[v] = opc[v].y; xhi[v] = opc[v].x; }
       } else if (kind == SK_NEAR) {
         if constexpr (DPP) {  // kPat7: slot 2 is -1, slot 4 is +1
 #pragma unroll
@@ -640,9 +650,14 @@ __device__ __forceinline__ void spmv_stencil_body(const SpmvArgs& a) {
       for (int q = 0; q < (NP > 0 ? NP : 1); ++q) tmp[q] = acc[q];
       const EpiVals olo = epi_values<EPI>(a, slo[0], NV == 2 ? slo[NV - 1] : 0.0, ilo, tmp);
       const EpiVals ohi = epi_values<EPI>(a, shi[0], NV == 2 ? shi[NV - 1] : 0.0, ihi, tmp);
+      if constexpr (!(KR_ST_AB & 2)) {
 #pragma unroll
-      for (int q = 0; q < (NP > 0 ? NP : 1); ++q) acc[q] = active ? tmp[q] : acc[q];
-      if constexpr (!(NTM & 4)) epi_store_pair<EPI, (NTM & 2) != 0>(a, rl, olo, ohi, active);
+        for (int q = 0; q < (NP > 0 ? NP : 1); ++q) acc[q] = active ? tmp[q] : acc[q];
+      }
+      if constexpr (!(NTM & 4) && !(KR_ST_AB & 1))
+        epi_store_pair<EPI, (NTM & 2) != 0>(a, rl, olo, ohi, active);
+      else if constexpr (KR_ST_AB & 1)
+        acc[0] = acc[0] + olo.y1 * ohi.y2;  // keep the sums live
     }
     // (6) carry along the walk: this visit's centers are the next one's PREV
     if constexpr (!RELOAD) {
