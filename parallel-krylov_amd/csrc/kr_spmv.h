@@ -229,7 +229,11 @@ template <int EPI>
 __device__ __forceinline__ bool spmv_entry(SpmvArgs& a) {
   if (a.stop && *a.stop != 0.0) return false;  // converged (device-resident scalars)
   if constexpr (EPI == EPI_XY_VP) {
+#ifdef KR_AB_NO_PROLOGUE  // timing-only ablation builds (wrong beta)
+    a.c0 = 0.5;
+#else
     if (a.pro && !spmv_prologue_beta(a)) return false;
+#endif
   }
   if constexpr (EPI == EPI_MRR_V) {
     // SC_MRR_ZETA (v3/gpu/mrr.py:47-49) from the EW_MRR_S partials, summed in
