@@ -582,6 +582,46 @@ def test_dia_symmetric_values_read_mirrored(torch_dev, monkeypatch, spec, shards
             sysm.close()
 
 
+@pytest.mark.parametrize("grid", ["auto", "1", "3"])
+@pytest.mark.parametrize("shards", [1, 3])
+def test_dia_walk_mirror_positions_at_block_edges(torch_dev, monkeypatch, shards, grid):
+    """The walk's one-store mirrors (KR_DIAW_MODE 3): lane p of a row block
+    stores its upper value of offset o at position (p + o) & 255, the
+    previous block's value when p + o >= 256 and this block's otherwise. The
+    offsets here sit on every boundary of that rule -- 1 and 2, the wave edges
+    63 / 64 / 65, 127 / 128 / 129, 191 / 192 / 193, and 254 / 255 / 256 (the
+    largest band the walk takes) -- with random symmetric values, so a store
+    at a wrong position or from the wrong block changes some row's sum. y is
+    bitwise scipy's over 1 and 3 shards and forced walk grids (long runs)."""
+    import scipy.sparse as sp
+    from parallel_krylov_amd.system import KrylovSystem, balanced_partition
+    if grid != "auto":
+        monkeypatch.setenv("KR_DIAW_GRID", grid)
+    offs = [1, 2, 63, 64, 65, 127, 128, 129, 191, 192, 193, 200, 254, 255, 256]
+    n = 5000
+    rng = np.random.default_rng(11)
+    rows, cols, vals = [np.arange(n)], [np.arange(n)], [np.full(n, 2.0 * len(offs) + 1.0)]
+    for o in offs:
+        i = np.arange(n - o)
+        v = -rng.random(n - o)
+        rows += [i, i + o]
+        cols += [i + o, i]
+        vals += [v, v]
+    A = sp.csr_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))),
+                      shape=(n, n))
+    A.sort_indices()
+    x = rng.standard_normal(n)
+    sysm = KrylovSystem(n, balanced_partition(n, shards), [0] * shards)
+    try:
+        sysm.set_matrix(A)
+        sysm.finalize()
+        assert [sysm.shard_format(s) for s in range(shards)] == ["dia_walk"] * shards
+        y = sysm.gather(sysm.spmv(sysm.split(x)))
+        np.testing.assert_array_equal(y.cpu().numpy(), A.dot(x))
+    finally:
+        sysm.close()
+
+
 def _longest_full_run(M, lo, hi):
     """The DIA walk's run of full row blocks of shard rows [lo, hi), as
     finalize picks it (kr_engine.cpp build_masks): a 256-row block is full
