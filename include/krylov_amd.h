@@ -58,8 +58,10 @@ extern "C" {
  *        the default (CG / k-skip CG return r0, the MrR family is refused).
  *   201  kr_solve_set_precond_ilu added (no struct or behaviour change).
  *   202  kr_system_shard_code_patterns added (no struct or behaviour change).
- *   203  kr_system_shard_dia_full_blocks added (no struct or behaviour change). */
-#define KR_ABI_VERSION 204
+ *   203  kr_system_shard_dia_full_blocks added (no struct or behaviour change).
+ *   204  kr_solve_kernel_stats reports device windows over a device's shards.
+ *   205  kr_system_shard_box added (no struct or behaviour change). */
+#define KR_ABI_VERSION 205
 int kr_version(void);
 const char* kr_last_error(void);
 /* Number of HIP devices visible to this process (0 when none). */
@@ -264,6 +266,14 @@ int kr_system_shard_codes(kr_system* sys, int shard, int* code_bits);
  * box: 9 blocks at 512^3). Lossless, compared byte for byte at finalize;
  * KR_STENCIL_PATTERNS=0 disables. Replaces nothing in the reference. */
 int kr_system_shard_code_patterns(kr_system* sys, int shard, int* patterns);
+/* Box stencil of shard s (after finalize): 1 when the shard is a constant-
+ * coefficient 7-point stencil on an n = 512 box (offsets -W, -512, -1, 0,
+ * +1, +512, +W; every entry of an offset the same finite value; absent
+ * entries exactly the box faces -- checked on the code patterns), else 0.
+ * Such a shard's k-skip basis pairs can run matrix-free (the box pair,
+ * kr_pair.hip: the absent operands read as 0.0, bitwise the CSR rows).
+ * KR_BOX=0 disables. Replaces nothing in the reference. */
+int kr_system_shard_box(kr_system* sys, int shard, int* box);
 /* Full-block run of shard s's symmetric DIA walk (after finalize): the
  * longest run of 256-row blocks [first, first + count) that are whole and
  * whose rows hold every offset (a band matrix: all but its first and last

@@ -20,7 +20,7 @@ KR_METHOD = {"cg": 0, "mrr": 1, "kskipcg": 2, "kskipmrr": 3, "adaptivekskipmrr":
              "pcg": 5, "chronopoulos_gear": 6, "gropp": 7, "pipeline": 8}
 # include/krylov_amd.h KR_ABI_VERSION: the struct layouts below (SolveParams,
 # SolveResult) are this version's; a library of another version is refused.
-KR_ABI_VERSION = 204
+KR_ABI_VERSION = 205
 KR_FORMAT = {0: "csr", 1: "stencil", 2: "dia", 3: "dense", 4: "dia_walk"}  # kr_system_shard_sched
 
 
@@ -99,6 +99,7 @@ _SIGNATURES = {
     "kr_system_shard_values": [_P, _I, _PI],
     "kr_system_shard_codes": [_P, _I, _PI],
     "kr_system_shard_code_patterns": [_P, _I, _PI],
+    "kr_system_shard_box": [_P, _I, _PI],
     "kr_system_shard_dia_full_blocks": [_P, _I, _PI64, _PI64],
     "kr_system_shard_dia_sym": [_P, _I, _PI],
     "kr_system_shard_sched": [_P, _I, _PI, _PI, _PI, _PI],

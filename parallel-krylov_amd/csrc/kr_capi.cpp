@@ -686,6 +686,14 @@ int kr_system_shard_code_patterns(kr_system* sys, int shard, int* patterns) {
   });
 }
 
+int kr_system_shard_box(kr_system* sys, int shard, int* box) {
+  return guarded([&] {
+    KR_REQUIRE(sys && shard >= 0 && shard < (int)sys->shards.size(), "bad shard");
+    KR_REQUIRE(sys->finalized, "system not finalized");
+    if (box) *box = sys->shards[shard].st_box ? 1 : 0;
+  });
+}
+
 int kr_system_shard_dia_full_blocks(kr_system* sys, int shard, int64_t* first, int64_t* count) {
   return guarded([&] {
     KR_REQUIRE(sys && shard >= 0 && shard < (int)sys->shards.size(), "bad shard");

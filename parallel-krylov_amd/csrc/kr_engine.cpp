@@ -560,9 +560,19 @@ bool stencil_pm(int P);
 
 int System::pair_mode() const {
   if (shards.size() != 1 || comm || nglobal_shards() != 1) return 0;
-  const int mode = KR_ENV("KR_ST2", 0);  // 0 / unset: two dual launches; 1, 2: the pairs (A/B)
-  if (mode != 1 && mode != 2) return 0;
+  // KR_ST2: 0 two dual launches; 1, 2 the code-reading pairs (A/B); 3 the box
+  // pair; unset: the box pair where the shard is a box (measured on C4, one
+  // box, profiles/r06a: the storing pair 1.44-1.46 ms against two duals'
+  // 1.68, the products-only pair 1.14-1.16 against 0.84 + 0.59; 545 -> 586
+  // it/s), else the duals
+  const int env = KR_ENV("KR_ST2", -1);
+  const int mode = env < 0 ? 3 : env;
+  if (mode != 1 && mode != 2 && mode != 3) return 0;
   const Shard& s = shards[0];
+  if (mode == 3)
+    return s.st_box && s.st_P % 16 == 0 && s.spmv_grid % s.st_P == 0 &&
+                   s.spmv_grid_po % s.st_P == 0
+               ? 3 : 0;
   if (!s.scode || !stencil_pm(s.st_P) || s.nm != 7 || s.st_nfar != 2) return 0;
   if (s.st_far[0] != -kStencilBlock || s.st_far[1] != kStencilBlock) return 0;
   if (s.st_cb != 2 && s.st_cb != 4) return 0;
@@ -580,7 +590,7 @@ int System::pair_mode() const {
 void System::spmv_pair(int in1, int in2, int out1, int out2, int slot0, SpmvEpi epi) {
   const int mode = pair_mode();
   KR_REQUIRE(mode != 0, "fused basis pair: shard not eligible");
-  KR_REQUIRE(mode == 2 || epi == EPI_DUAL_MRR, "fused basis pair (KR_ST2=1): k-skip MrR only");
+  KR_REQUIRE(mode >= 2 || epi == EPI_DUAL_MRR, "fused basis pair (KR_ST2=1): k-skip MrR only");
   KR_REQUIRE(slot0 + 14 <= kMaxSlots, "reduction slots exhausted");
   Shard& s = shards[0];
   KR_HIP_CHECK(hipSetDevice(s.dev));
@@ -625,7 +635,7 @@ void System::spmv_pair(int in1, int in2, int out1, int out2, int slot0, SpmvEpi 
     // walk segments divide both: the largest such count <= KR_ST2T_Z
     const int g1 = s.spmv_grid, g2 = po ? s.spmv_grid_po : s.spmv_grid;
     const int z1 = g1 / s.st_P, z2 = g2 / s.st_P;
-    const char* ze = getenv("KR_ST2T_Z");
+    const char* ze = getenv(mode == 3 ? "KR_ST2B_Z" : "KR_ST2T_Z");
     const int zcap = ze && atoi(ze) > 0 ? atoi(ze) : 16;
     const int zg = std::gcd(z1, z2);
     int zw = 1;
@@ -633,7 +643,13 @@ void System::spmv_pair(int in1, int in2, int out1, int out2, int slot0, SpmvEpi 
       if (zg % d == 0 && d <= zcap) zw = d;
     a.st2_z1 = z1;
     a.st2_z2 = z2;
-    launch_spmv_stencil2t(epi, a, (s.st_P / 2) * zw, s.stream);
+    if (mode == 3) {
+      a.st_box = 1;
+      for (int k = 0; k < 8; ++k) a.st_v[k] = s.st_v[k];
+      launch_spmv_stencil2b(epi, a, (s.st_P / 2) * zw, s.stream);
+    } else {
+      launch_spmv_stencil2t(epi, a, (s.st_P / 2) * zw, s.stream);
+    }
     for (int p = 0; p < 7; ++p) {
       s.slot_n[slot0 + p] = g1;
       s.slot_n[slot0 + 7 + p] = g2;
@@ -967,6 +983,73 @@ void System::build_code_patterns(Shard& s) {
   s.st_pat = dtab;
   s.st_pid = dpid;
   s.st_npat = (int)first.size();
+  build_box(s, h, pid, first);
+}
+
+// Constant-coefficient 7-point box stencil with n = 512 (Shard::st_box): the
+// offsets -W, -512, -1, 0, +1, +512, +W (W = P 512-row lines per plane,
+// whole planes), every present entry of slot k the same finite value st_v[k],
+// and the absent entries exactly the box faces -- -W iff z = 0, -512 iff
+// y = 0, -1 iff x = 0, +1 iff x = 511, +512 iff y = P-1, +W iff z = last
+// (row = (z P + y) 512 + x). Checked on the code patterns: each pattern
+// against the face class of a block holding it, then every block's class
+// against its pattern's. The box pair (kr_pair.hip) reads absent operands
+// as 0.0, which leaves a row sum unchanged, so it is bitwise the CSR rows.
+// KR_BOX=0 disables.
+void System::build_box(Shard& s, const std::vector<uint8_t>& h, const std::vector<uint32_t>& pid,
+                       const std::vector<int64_t>& first) {
+  s.st_box = false;
+  if (KR_ENV("KR_BOX", 1) == 0) return;
+  static const int32_t kPat[7] = {1, 4, 3, 0, 3, 5, 2};  // kPat7
+  if (s.nm != 7 || s.st_nfar != 2 || !std::equal(kPat, kPat + 7, s.st_kind)) return;
+  if (s.st_far[0] != -kStencilBlock || s.st_far[1] != kStencilBlock) return;
+  const int64_t P = s.st_P, W = P * kStencilBlock;
+  if (P < 2 || s.n % W != 0 || s.n / W < 2 || s.ntab <= 0) return;
+  const int64_t planes = s.n / W;
+  const int32_t want[7] = {(int32_t)-W, -kStencilBlock, -1, 0, 1, kStencilBlock, (int32_t)W};
+  if (s.moff_h.size() != 7 || !std::equal(want, want + 7, s.moff_h.begin())) return;
+  const int cb = s.st_cb;
+  const uint64_t none = cb == 8 ? 0xFFull : (1ull << cb) - 1;
+  auto code = [&](int64_t b, int x, int k) {  // slot k's code of row x of block b
+    uint64_t w = 0;
+    std::memcpy(&w, h.data() + ((size_t)b * kStencilBlock + x) * cb, cb);
+    return (w >> (cb * k)) & none;
+  };
+  // face class of block b = (z, y): bits 0/1 z first/last, 2/3 y first/last
+  auto cls = [&](int64_t b) {
+    const int64_t z = b / P, y = b % P;
+    return (z == 0 ? 1 : 0) | (z == planes - 1 ? 2 : 0) | (y == 0 ? 4 : 0) | (y == P - 1 ? 8 : 0);
+  };
+  uint64_t c[7];
+  for (int k = 0; k < 7; ++k) c[k] = none;
+  std::vector<int> pcls(first.size());
+  for (size_t q = 0; q < first.size(); ++q) {
+    const int f = cls(first[q]);
+    pcls[q] = f;
+    for (int x = 0; x < kStencilBlock; ++x) {
+      const bool absent[7] = {(f & 1) != 0, (f & 4) != 0, x == 0, false, x == kStencilBlock - 1,
+                              (f & 8) != 0, (f & 2) != 0};
+      for (int k = 0; k < 7; ++k) {
+        const uint64_t v = code(first[q], x, k);
+        if (absent[k]) {
+          if (v != none) return;
+        } else {
+          if (v == none) return;
+          if (c[k] == none) c[k] = v;
+          if (v != c[k]) return;
+        }
+      }
+    }
+  }
+  for (int64_t b = 0; b < (int64_t)pid.size(); ++b)
+    if (cls(b) != pcls[pid[(size_t)b]]) return;
+  std::vector<double> tab((size_t)s.ntab);
+  KR_HIP_CHECK(hipMemcpy(tab.data(), s.vtab, sizeof(double) * tab.size(), hipMemcpyDeviceToHost));
+  for (int k = 0; k < 7; ++k) {
+    if (c[k] == none || c[k] >= (uint64_t)s.ntab || !std::isfinite(tab[(size_t)c[k]])) return;
+    s.st_v[k] = tab[(size_t)c[k]];
+  }
+  s.st_box = true;
 }
 
 // Stencil SpMV grid. Position-major (P % 8 == 0, the 3-D stencils): P
@@ -3185,7 +3268,7 @@ class KskipCgSession : public Base {
     }
     // the tiled fused pair (KR_ST2=2) chains two duals per launch where the
     // shard allows; an odd count ends with a single dual
-    const bool pairs = sys->pair_mode() == 2;
+    const bool pairs = sys->pair_mode() >= 2;
     for (int j = 1; j <= k;) {
       if (pairs && j + 1 <= k) {
         sys->products_only = j + 1 == k;  // Ar[k], Ap[k+1] feed only the Gram products

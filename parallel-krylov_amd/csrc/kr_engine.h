@@ -115,6 +115,11 @@ struct Shard {
   uint32_t* st_pid = nullptr;
   void* st_pat = nullptr;
   int st_npat = 0;
+  // constant-coefficient 7-point box stencil with n = 512 (System::build_box):
+  // every entry of slot k is st_v[k], absent entries exactly the box faces;
+  // the box pair (kr_pair.hip) then runs without reading the matrix
+  bool st_box = false;
+  double st_v[8] = {};
   hipStream_t comm_stream = nullptr;  // halo exchange, overlapped with interior rows
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   int grid = 1;                 // workgroups of the vector kernels
@@ -298,10 +303,17 @@ struct System {
   // 512 and whole planes, narrow codes; KR_ST2=1: one position per workgroup
   // (spmv_stencil2_kernel, measured slower than two duals),
   // KR_ST2=2: two positions per workgroup (spmv_stencil2t_kernel, P % 16 == 0;
-  // bitwise the dual launches, products included).
+  // bitwise the dual launches, products included), both measured slower;
+  // KR_ST2=3 or unset: the box pair (kr_pair.hip) on a Shard::st_box shard
+  // with P % 16 == 0 -- the tiled pair's grids and products, the matrix not
+  // read; faster than the duals, so the default there.
   int pair_mode() const;
   bool pair_ok() const { return pair_mode() != 0; }
   void spmv_pair(int in1, int in2, int out1, int out2, int slot0, SpmvEpi epi = EPI_DUAL_MRR);
+  // Shard::st_box from the code patterns (host copies h: the codes of every
+  // row block, pid / first: the pattern ids and a block holding each)
+  void build_box(Shard& s, const std::vector<uint8_t>& h, const std::vector<uint32_t>& pid,
+                 const std::vector<int64_t>& first);
   void ew(EwOp op, double c0, double c1, std::array<int, 6> ids, int slot0);
   // The same for ops with more than 6 operands (-1: unused slot).
   void ew_n(EwOp op, double c0, double c1, const std::array<int, kEwOps>& ids, int slot0);

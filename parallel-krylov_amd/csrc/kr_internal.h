@@ -267,6 +267,11 @@ struct SpmvArgs {
   // two dual grids whose partials it writes (level 1 = dual m, level 2 = dual
   // m+1: general grid, or the products-only grid), the walk runs on their gcd
   int st2_z1 = 0, st2_z2 = 0;
+  // The box pair (kr_pair.hip, spmv_stencil2b_kernel): 1 when the shard is a
+  // constant-coefficient 7-point box stencil with n = 512 (Shard::st_box);
+  // st_v[k] = the value of every entry of slot k (offset st_off[k]).
+  int st_box = 0;
+  double st_v[8] = {};
   int32_t st_off[8] = {};
   int32_t st_kind[8] = {};
   int32_t st_far[4] = {};
@@ -314,6 +319,10 @@ void launch_spmv_stencil2(const SpmvArgs& a, int nblocks, hipStream_t s);
 void launch_spmv_stencil2t(SpmvEpi epi, const SpmvArgs& a, int nblocks, hipStream_t s);
 void launch_spmv_stencil2t_mrr(const SpmvArgs& a, int nblocks, hipStream_t s);
 void launch_spmv_stencil2t_kcg(const SpmvArgs& a, int nblocks, hipStream_t s);
+// The box pair (kr_pair.hip): the tiled pair's job and products for a
+// constant-coefficient 7-point box stencil (SpmvArgs::st_box), the matrix not
+// read; same grids (nblocks = P/2 x walk segments), bitwise the dual launches.
+void launch_spmv_stencil2b(SpmvEpi epi, const SpmvArgs& a, int nblocks, hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // Elementwise vector steps with fused reductions (all own-row pointers).

@@ -302,12 +302,16 @@ class KrylovSystem:
         table instead of the per-row stream; 0 = per-row stream), dia_sym
         (1: symmetric diagonal-offset values, lower entries read as the
         mirrored upper ones), dia_full_blocks / dia_full_first (DIA walk: the
-        run of 256-row blocks whose all-ones offset masks are not loaded)."""
+        run of 256-row blocks whose all-ones offset masks are not loaded),
+        box (1: constant-coefficient 7-point box stencil with n = 512, the
+        k-skip basis pairs can run matrix-free)."""
         mb, no = ctypes.c_int(), ctypes.c_int()
         lo, hi = ctypes.c_int64(), ctypes.c_int64()
         call("kr_system_shard_layout", self.handle, s, ctypes.byref(mb), ctypes.byref(no),
              ctypes.byref(lo), ctypes.byref(hi))
         dv, cb, ds, cp = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        bx = ctypes.c_int()
+        call("kr_system_shard_box", self.handle, s, ctypes.byref(bx))
         call("kr_system_shard_values", self.handle, s, ctypes.byref(dv))
         call("kr_system_shard_codes", self.handle, s, ctypes.byref(cb))
         call("kr_system_shard_code_patterns", self.handle, s, ctypes.byref(cp))
@@ -317,7 +321,7 @@ class KrylovSystem:
         return dict(mask_bits=mb.value, n_offsets=no.value, interior_lo=lo.value,
                     interior_hi=hi.value, dict_values=dv.value, code_bits=cb.value,
                     code_patterns=cp.value, dia_sym=ds.value, dia_full_blocks=fbn.value,
-                    dia_full_first=fb0.value)
+                    dia_full_first=fb0.value, box=bx.value)
 
     def shard_sched(self, s: int) -> dict:
         """Launch geometry of shard s: elementwise and SpMV grids plus the

@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol():
 def test_version_and_device_count_without_gpu():
     lib = _lib()
     import parallel_krylov_amd._lib as L
-    assert lib.kr_version() == L.KR_ABI_VERSION == 204
+    assert lib.kr_version() == L.KR_ABI_VERSION == 205
     c = ctypes.c_int(-1)
     assert lib.kr_device_count(ctypes.byref(c)) == 0
     assert c.value >= 0

@@ -1,0 +1,160 @@
+"""The box fused basis pair (kr_pair.hip, spmv_stencil2b_kernel; KR_ST2=3).
+
+A constant-coefficient 7-point stencil on an n = 512 box (every entry of an
+offset the same value, absent entries exactly the box faces) is recognised
+at finalize (System::build_box, ``shard_layout()["box"]``); its k-skip basis
+pairs then run without reading the matrix: the absent operands are read as
+0.0 (zero LDS pads, out-of-range loads, zeroed level-1 planes), which leaves
+every row sum bit for bit scipy's, and both duals' products are accumulated
+in the dual launches' order into their partials. So the histories and x
+must equal the two-dual path (KR_ST2=0) BITWISE -- which the GPU-order
+oracle already pins to the reference's statements (test_gpu_stencil.py).
+"""
+import contextlib
+import importlib
+import io
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from test_gpu_stencil import MATRICES, _system, aniso, box
+
+
+def _solver(method):
+    mod = importlib.import_module(f"parallel_krylov_amd.v3.gpu.{method}")
+    return getattr(mod, method)
+
+
+def perturbed_value(A, row=5 * 512 * 16 + 3 * 512 + 100):
+    """One interior off-diagonal entry changed: no longer constant-coefficient."""
+    A = A.tolil(copy=True)
+    A[row, row + 1] = A[row, row + 1] * 1.5
+    A = sp.csr_matrix(A)
+    A.sort_indices()
+    return A
+
+
+def dropped_entry(A, row=5 * 512 * 16 + 3 * 512 + 100):
+    """One interior +1 entry removed (stored structure off the box faces)."""
+    A = A.tolil(copy=True)
+    A[row, row + 1] = 0.0
+    A = sp.csr_matrix(A)
+    A.eliminate_zeros()
+    A.sort_indices()
+    return A
+
+
+BOX = {
+    "box512x16x12": 1, "box512x32x10": 1, "aniso512x16x12": 1, "box512x16x64": 1,
+    "box512x8x16": 1, "p3d64": 0, "box128x64x20": 0, "vals40_128x64x10": 0,
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(BOX))
+def test_box_flag(name):
+    sysm = _system(MATRICES[name](), 1)
+    try:
+        assert sysm.shard_layout(0)["box"] == BOX[name]
+    finally:
+        sysm.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("make", [perturbed_value, dropped_entry])
+def test_box_flag_rejects_irregular(make):
+    sysm = _system(make(box(512, 16, 12)), 1)
+    try:
+        assert sysm.shard_layout(0)["box"] == 0
+    finally:
+        sysm.close()
+
+
+@pytest.mark.gpu
+def test_box_flag_anisotropic_and_negative_values():
+    """Per-offset constants (not one global value), a negative diagonal."""
+    A = -aniso(512, 16, 10, 2.0, 0.75, 0.3)
+    sysm = _system(sp.csr_matrix(A), 1)
+    try:
+        assert sysm.shard_layout(0)["box"] == 1
+    finally:
+        sysm.close()
+
+
+# KR_PO_ZMAX=1 gives the products-only dual a 1-segment grid against the
+# general grid's (the pair then flushes level 1 inside one walk), KR_ST2B_Z=1
+# makes every pair walk the whole box (both levels flush); KR_ST2B_Z=2 two
+# walk segments
+BOX_CASES = [("kskipmrr", "box512x16x12", 4, {}), ("kskipmrr", "box512x16x12", 5, {}),
+             ("adaptivekskipmrr", "box512x16x12", 8, {}), ("kskipmrr", "aniso512x16x12", 4, {}),
+             ("kskipmrr", "box512x32x10", 3, {}), ("kskipmrr", "box512x32x10", 2, {}),
+             ("kskipcg", "box512x16x12", 4, {}), ("kskipcg", "box512x32x10", 5, {}),
+             ("kskipmrr", "box512x16x64", 4, {"KR_PO_ZMAX": "1"}),
+             ("kskipmrr", "box512x16x64", 4, {"KR_PO_ZMAX": "1", "KR_ST2B_Z": "1"}),
+             ("kskipmrr", "box512x16x64", 6, {"KR_ST2B_Z": "2"}),
+             ("kskipcg", "box512x16x64", 4, {"KR_PO_ZMAX": "2", "KR_ST2B_Z": "1"}),
+             ("adaptivekskipmrr", "box512x16x64", 6, {})]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method,name,k,env", BOX_CASES,
+                         ids=[f"{m}-{n}-k{k}-{len(e)}" for m, n, k, e in BOX_CASES])
+def test_box_pair_bitwise_equal_duals(monkeypatch, method, name, k, env):
+    """Histories and x bit for bit against the dual launches (KR_ST2=0):
+    k-skip MrR, adaptive k-skip MrR, k-skip CG; odd k ends with a single dual;
+    flushes at either grid's segment boundaries inside one walk."""
+    A = MATRICES[name]()
+    b = np.random.default_rng(5).standard_normal(A.shape[0])
+    kw = dict(tol=1e-10, maxiter=400, k=k)
+    monkeypatch.setenv("KRYLOV_AMD_SHARDS", "0")
+    for key, val in env.items():
+        monkeypatch.setenv(key, val)
+    out = []
+    for st2 in ("0", "3"):
+        monkeypatch.setenv("KR_ST2", st2)
+        with contextlib.redirect_stdout(io.StringIO()):
+            x, info = _solver(method)(A, b, **kw)
+        out.append((x.cpu().numpy(), info))
+    (x0, i0), (x1, i1) = out
+    np.testing.assert_array_equal(i1["nosl"], i0["nosl"])
+    if "khistory" in i0:
+        np.testing.assert_array_equal(i1["khistory"], i0["khistory"])
+    np.testing.assert_array_equal(i1["residual"], i0["residual"])
+    np.testing.assert_array_equal(x1, x0)
+
+
+def _launches(A, method, k, st2, monkeypatch):
+    monkeypatch.setenv("KR_ST2", st2)
+    sysm = _system(A, 1)
+    try:
+        b = sysm.split(np.random.default_rng(1).standard_normal(A.shape[0]))
+        sysm.begin(method, b, None, tol=0.0, maxiter=8 * (k + 1) + 2, k=k, profile=1)
+        sysm.step(4)
+        st = {r["name"]: r["launches"] for r in sysm.kernel_stats()}
+        sysm.finish(method)
+    finally:
+        sysm.close()
+    return st
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method,k", [("kskipmrr", 4), ("kskipmrr", 3), ("kskipcg", 4)])
+def test_box_pair_is_used(monkeypatch, method, k):
+    """KR_ST2=3 runs k // 2 box-pair launches per outer iteration (the last
+    products-only for even k) and k % 2 single duals on a box shard."""
+    st = _launches(MATRICES["box512x16x12"](), method, k, "3", monkeypatch)
+    tag = "mrr" if method == "kskipmrr" else "kcg"
+    npair = st.get(f"spmv2x2_gram_{tag}", 0) + st.get(f"spmv2x2_gram_{tag}_last", 0)
+    ndual = st.get(f"spmv2_gram_{tag}", 0) + st.get(f"spmv2_gram_{tag}_last", 0)
+    assert npair == 4 * (k // 2) and ndual == 4 * (k % 2), st
+    assert st.get(f"spmv2x2_gram_{tag}_last", 0) == (4 if k % 2 == 0 else 0), st
+
+
+@pytest.mark.gpu
+def test_box_pair_not_used_off_the_box(monkeypatch):
+    """An irregular matrix (one interior entry dropped) keeps the dual launches
+    under KR_ST2=3, and its history still equals the KR_ST2=0 run."""
+    A = dropped_entry(box(512, 16, 12))
+    st = _launches(A, "kskipmrr", 4, "3", monkeypatch)
+    assert st.get("spmv2x2_gram_mrr", 0) == 0 and st.get("spmv2_gram_mrr", 0) > 0, st
