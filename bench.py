@@ -418,8 +418,13 @@ def kernel_table(stats, deltas):
             avg = s_["total_ms"] / s_["launches"]
             nsh = max(1, int(s_.get("shards", 1)))
             csr = s_["bytes_per_launch"]
-            # shards past the listed ones: the last listed shard's delta
-            d = sum(deltas[:nsh]) + max(0, nsh - len(deltas)) * deltas[-1]
+            # the launch covers the first nsh shards of this process, each of
+            # which has its delta: more shards than deltas is a bookkeeping
+            # error of the caller, never padded over
+            if nsh > len(deltas):
+                raise ValueError(f"{s_['name']}: a launch covers {nsh} shards but only "
+                                 f"{len(deltas)} stored-format deltas were given")
+            d = sum(deltas[:nsh])
             st = csr - (d if s_["name"].startswith("spmv") else 0.0)
             stored[s_["name"]] = (st, csr)
             kernels[s_["name"]] = dict(launches=s_["launches"], avg_ms=round(avg, 5),
@@ -438,6 +443,19 @@ def checked_frac(achieved_gbs, peak=None):
     peak = HBM_PEAK_GBS if peak is None else peak
     f = achieved_gbs / peak
     return round(f, 4) if f <= 1.0 else None
+
+
+def frac_fields(achieved_gbs, peak=None):
+    """{"frac": ...}, plus "frac_error" saying why when checked_frac refuses
+    the value (above the peak): the record shows the mismatch instead of a
+    silent null."""
+    peak = HBM_PEAK_GBS if peak is None else peak
+    f = checked_frac(achieved_gbs, peak)
+    out = dict(frac=f)
+    if f is None:
+        out["frac_error"] = (f"achieved {achieved_gbs} GB/s exceeds the {peak} GB/s peak: "
+                             f"bytes and time of different shard sets")
+    return out
 
 
 def host_table(stats):
@@ -486,7 +504,7 @@ def step_roofline(kernels, stored, run, args, per_step, n, nnz_total, method, k)
     byts = sum(stored[n_][0] * v["launches"] for n_, v in kernels.items()) / sampled
     step_s = run["elapsed"] / args.steps
     out = dict(stored_bytes_per_step=round(byts), achieved=round(byts / step_s / 1e9, 1),
-               peak=HBM_PEAK_GBS, unit="GB/s", frac=checked_frac(byts / step_s / 1e9))
+               peak=HBM_PEAK_GBS, unit="GB/s", **frac_fields(round(byts / step_s / 1e9, 1)))
     if method in ("kskipmrr", "adaptivekskipmrr") and k > 0 and nnz_total > 0:
         b_spmv = 12.0 * nnz_total + 4.0 * (n + 1) + 16.0 * n
         per_iter = ((3 * k + 1) * b_spmv + (2 * k + 3) * 8.0 * n + 9 * (k + 1) * 8.0 * n) / (k + 1)
@@ -542,7 +560,7 @@ def main():
         # masks instead of columns, 1-byte dictionary codes instead of values:
         # DESIGN.md 9); the CSR figure of SURVEY.md 8(d) is csr_equiv_gbs
         roofline = dict(bound="hbm", kernel=dom, achieved=ach, peak=HBM_PEAK_GBS, unit="GB/s",
-                        frac=checked_frac(ach),
+                        **frac_fields(ach),
                         copy_peak=HBM_COPY_GBS, frac_of_copy=round(ach / HBM_COPY_GBS, 4),
                         traffic=pmc_traffic(args.config, dom),
                         traffic_source=f"profiles/pmc/{args.config}.json",
@@ -564,7 +582,7 @@ def main():
         if kc:
             dc = dominant(kc)
             csr_rec.update(kernel=dc, avg_ms=kc[dc]["avg_ms"], achieved=kc[dc]["gbs"],
-                           frac=checked_frac(kc[dc]["gbs"]),
+                           **frac_fields(kc[dc]["gbs"]),
                            traffic=pmc_traffic(args.config + "_csr", dc),
                            traffic_source=f"profiles/pmc/{args.config}_csr.json",
                            kernels=kc)

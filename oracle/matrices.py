@@ -209,13 +209,24 @@ class ParCSR:
 
     _lib = None
 
+    @staticmethod
+    def lib_path():
+        import os
+        return os.path.join(os.path.dirname(os.path.abspath(__file__)), "liboracle_csrmv.so")
+
+    @staticmethod
+    def available():
+        """True when oracle/build.sh has built the helper (build() runs it;
+        its failure does not fail the product build)."""
+        import os
+        return os.path.exists(ParCSR.lib_path())
+
     def __init__(self, indptr, indices, data, shape):
         import ctypes
-        import os
         if ParCSR._lib is None:
-            path = os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                                "liboracle_csrmv.so")
-            lib = ctypes.CDLL(path)
+            if not ParCSR.available():
+                raise FileNotFoundError(f"{ParCSR.lib_path()} is missing: run oracle/build.sh")
+            lib = ctypes.CDLL(ParCSR.lib_path())
             P = ctypes.c_void_p
             lib.oracle_csrmv.argtypes = [ctypes.c_int64, P, P, P, P, P]
             lib.oracle_csrmv.restype = None

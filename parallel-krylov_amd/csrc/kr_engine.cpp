@@ -636,7 +636,9 @@ void System::spmv_pair(int in1, int in2, int out1, int out2, int slot0, SpmvEpi 
     const int g1 = s.spmv_grid, g2 = po ? s.spmv_grid_po : s.spmv_grid;
     const int z1 = g1 / s.st_P, z2 = g2 / s.st_P;
     const char* ze = getenv(mode == 3 ? "KR_ST2B_Z" : "KR_ST2T_Z");
-    const int zcap = ze && atoi(ze) > 0 ? atoi(ze) : 16;
+    // the box pair: 64-plane walks at 512^3 (3 of every 64 planes re-walked;
+    // KR_ST2B_Z 4 / 8 / 16 / 32: 1.385 / 1.395 / 1.444 / 1.542 ms, profiles/r06a)
+    const int zcap = ze && atoi(ze) > 0 ? atoi(ze) : (mode == 3 ? 8 : 16);
     const int zg = std::gcd(z1, z2);
     int zw = 1;
     for (int d = 1; d <= zg; ++d)
@@ -646,7 +648,15 @@ void System::spmv_pair(int in1, int in2, int out1, int out2, int slot0, SpmvEpi 
     if (mode == 3) {
       a.st_box = 1;
       for (int k = 0; k < 8; ++k) a.st_v[k] = s.st_v[k];
-      launch_spmv_stencil2b(epi, a, (s.st_P / 2) * zw, s.stream);
+      if (!s.pairq) {
+        const size_t bytes = sizeof(double) * 14 * 4 * (size_t)s.pstride;
+        KR_HIP_CHECK(hipMalloc(&s.pairq, bytes));
+        s.owned.push_back(s.pairq);
+        fresh_fill(s.pairq, bytes, s.stream);
+      }
+      a.partq = s.pairq;
+      const int xs = st2b_xsegments(po);
+      launch_spmv_stencil2b(epi, a, (s.st_P / 2) * xs * zw, xs, g1, g2, s.stream);
     } else {
       launch_spmv_stencil2t(epi, a, (s.st_P / 2) * zw, s.stream);
     }
@@ -660,6 +670,57 @@ void System::spmv_pair(int in1, int in2, int out1, int out2, int slot0, SpmvEpi 
   // level-2 outputs (none products-only) -- one dual SpMV's; level 1 never
   // leaves the chip
   const double bytes = 12.0 * s.nnz + 4.0 * (s.n + 1) + 16.0 * s.n + (po ? 0.0 : 16.0 * s.n);
+  prof_end(s, nm, t0, bytes);
+}
+
+bool System::step2_ok() const {
+  if (shards.size() != 1 || comm || nglobal_shards() != 1) return false;
+  if (KR_ENV("KR_STEP2", 1) == 0) return false;
+  const Shard& s = shards[0];
+  return s.st_box && s.st_P % 16 == 0;
+}
+
+void System::spmv_step2(int r_in, int r_out, int y_in, int y_out, int z, int xs, int xd,
+                        double eta0, double zeta0, double eta1, double zeta1) {
+  KR_REQUIRE(step2_ok(), "box step pair: shard not eligible");
+  KR_REQUIRE(r_out != r_in && y_out != y_in && y_out != r_in && r_out != y_in,
+             "box step pair: r / y outputs alias their gathered inputs");
+  Shard& s = shards[0];
+  KR_HIP_CHECK(hipSetDevice(s.dev));
+  const char* nm = "spmv_step2_mrr_stencil";
+  hipEvent_t t0 = nullptr;
+  prof_begin(s, nm, t0);
+  SpmvArgs a;
+  a.n = s.n;
+  a.x1 = s.vec[r_in];
+  a.x2 = s.vec[y_in];
+  a.xoff = s.pad;
+  a.xlen = s.ld;
+  a.y1 = s.own(r_out);
+  a.u1 = s.own(y_out);
+  a.u2 = s.own(z);
+  a.us = s.own(xs);
+  a.ud = s.own(xd);
+  a.c0 = eta0;
+  a.c1 = zeta0;
+  a.c2 = eta1;
+  a.c3 = zeta1;
+  a.st_P = s.st_P;
+  a.st_box = 1;
+  for (int k = 0; k < 8; ++k) a.st_v[k] = s.st_v[k];
+  a.stop = dev_stop ? s.st + ST_STOP : nullptr;
+  // walk segments: 16 per plane column at 512 planes (32-plane walks), fewer
+  // on thinner boxes (>= 8 planes per walk); KR_STEP2_Z overrides
+  const int64_t planes = s.n / ((int64_t)s.st_P * kStencilBlock);
+  int zw = KR_ENV("KR_STEP2_Z", 0);
+  if (zw <= 0) {
+    zw = 1;
+    while (zw < 16 && planes / (2 * zw) >= 8) zw *= 2;
+  }
+  zw = (int)std::min<int64_t>(zw, planes);
+  launch_spmv_step2b(a, (s.st_P / 2) * zw, s.stream);
+  // algorithmic bytes in CSR terms: A once, r, y, z, x in and r, y, z, x out
+  const double bytes = 12.0 * s.nnz + 4.0 * (s.n + 1) + 64.0 * s.n;
   prof_end(s, nm, t0, bytes);
 }
 
@@ -2013,14 +2074,16 @@ void System::spmv(SpmvEpi epi, int in1, int in2, int out1, int out2, int e, int 
     a.products_only = po_shard(s) ? 1 : 0;
     a.stop = dev_stop ? s.st + ST_STOP : nullptr;
     a.nnz_total = s.nnz;
-    // Non-temporal result stores: the row walks of large shards (a plain-CSR
-    // dual at 512^3 -5 %; C1's 64k rows, whose vectors stay in L2/MALL for
-    // the next kernel, lost 8 % with them); not the DIA kernels (C3 / C5
-    // neutral as an A/B build, profiles/r05b/dia_nts). KR_NT_STORES=0/1
-    // forces either.
+    // Non-temporal matrix stream and result stores: the row walks of large
+    // shards (variant 13: a plain-CSR dual at 512^3 -5 %; C1's 64k rows,
+    // whose vectors stay in L2/MALL for the next kernel, lost 8 % with them).
+    // Only the row walk reads the flag -- the DIA kernels keep plain stores
+    // (C3 / C5 neutral as an A/B build, profiles/r05b/dia_nts) -- so a DIA
+    // shard's short-row launches that fall back to the row walk (no x window)
+    // get variant 13 like any large shard. KR_NT_STORES=0/1 forces either.
     {
       const int e = KR_ENV("KR_NT_STORES", -1);
-      a.nt_stores = e >= 0 ? e : (!s.dia && s.n >= ((int64_t)1 << 22)) ? 1 : 0;
+      a.nt_stores = e >= 0 ? e : s.n >= ((int64_t)1 << 22) ? 1 : 0;
     }
     if (s.dense) {
       a.dense = 1;
@@ -3197,7 +3260,20 @@ class KskipMrrSession : public Base {
     } else {
       ew_step(0);
     }
+    const bool step2 = sys->fuse_steps && sys->step2_ok();
     for (int j = j1; j <= k; ++j) {
+      if (step2 && step_kind(j) == 0 && j + 1 <= k && step_kind(j + 1) == 1) {
+        // steps j (x deferred) and j+1 (x = (x - z_j) - z_{j+1}) in one walk
+        // on a box shard: r and y into their other buffers, z and x as the
+        // two step kernels write them (System::spmv_step2; bitwise those)
+        sys->spmv_step2(r0, r_alt, y0, y_alt, Z, xsrc, cur, eta[j], zeta[j], eta[j + 1],
+                        zeta[j + 1]);
+        xsrc = cur;
+        std::swap(r0, r_alt);
+        std::swap(y0, y_alt);
+        ++j;
+        continue;
+      }
       if (sys->fuse_steps) {
         const int kind = step_kind(j);
         StepOps st;

@@ -120,6 +120,7 @@ struct Shard {
   // the box pair (kr_pair.hip) then runs without reading the matrix
   bool st_box = false;
   double st_v[8] = {};
+  double* pairq = nullptr;  // SpmvArgs::partq of the box pair, 14 x pstride x 4, owned
   hipStream_t comm_stream = nullptr;  // halo exchange, overlapped with interior rows
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   int grid = 1;                 // workgroups of the vector kernels
@@ -310,6 +311,13 @@ struct System {
   int pair_mode() const;
   bool pair_ok() const { return pair_mode() != 0; }
   void spmv_pair(int in1, int in2, int out1, int out2, int slot0, SpmvEpi epi = EPI_DUAL_MRR);
+  // The box step pair (kr_pair.hip, launch_spmv_step2b): k-skip MrR steps j
+  // and j+1 (EPI_STEP_MRR_NOX + EPI_STEP_MRR_X2) in one walk on a box shard
+  // (one shard, no communicator, P % 16 == 0). KR_STEP2=0 disables.
+  bool step2_ok() const;
+  // r: r_in -> r_out, y: y_in -> y_out (other buffers), z in place, x: xs -> xd
+  void spmv_step2(int r_in, int r_out, int y_in, int y_out, int z, int xs, int xd, double eta0,
+                  double zeta0, double eta1, double zeta1);
   // Shard::st_box from the code patterns (host copies h: the codes of every
   // row block, pid / first: the pattern ids and a block holding each)
   void build_box(Shard& s, const std::vector<uint8_t>& h, const std::vector<uint32_t>& pid,

@@ -272,6 +272,9 @@ struct SpmvArgs {
   // st_v[k] = the value of every entry of slot k (offset st_off[k]).
   int st_box = 0;
   double st_v[8] = {};
+  // ... its products: [14 slots][grid][4 x quarters], combined into partials
+  // (slot kk at partials + kk * grid) by st2b_combine_kernel
+  double* partq = nullptr;
   int32_t st_off[8] = {};
   int32_t st_kind[8] = {};
   int32_t st_far[4] = {};
@@ -321,8 +324,19 @@ void launch_spmv_stencil2t_mrr(const SpmvArgs& a, int nblocks, hipStream_t s);
 void launch_spmv_stencil2t_kcg(const SpmvArgs& a, int nblocks, hipStream_t s);
 // The box pair (kr_pair.hip): the tiled pair's job and products for a
 // constant-coefficient 7-point box stencil (SpmvArgs::st_box), the matrix not
-// read; same grids (nblocks = P/2 x walk segments), bitwise the dual launches.
-void launch_spmv_stencil2b(SpmvEpi epi, const SpmvArgs& a, int nblocks, hipStream_t s);
+// read; nblocks = P/2 tiles x xs x-segments x walk segments; its products
+// go through SpmvArgs::partq into the n1 / n2 partials of the two dual grids,
+// bitwise the dual launches'.
+void launch_spmv_stencil2b(SpmvEpi epi, const SpmvArgs& a, int nblocks, int xs, int n1, int n2,
+                           hipStream_t s);
+// The box step pair (kr_pair.hip): k-skip MrR steps j (EPI_STEP_MRR_NOX) and
+// j+1 (EPI_STEP_MRR_X2) in one walk on a box shard: x1 = r_a (gathered), x2
+// = y_a (gathered), y1 = r_c, u1 = y_c (other buffers), u2 = z (in place),
+// us / ud = x source / destination, c0 c1 / c2 c3 = the steps' (eta, zeta);
+// nblocks = P/2 x walk segments. Bitwise the two step launches.
+void launch_spmv_step2b(const SpmvArgs& a, int nblocks, hipStream_t s);
+// x segments per line of the box pair (1, 2 or 4; kr_pair.hip)
+int st2b_xsegments(bool products_only);
 
 // ---------------------------------------------------------------------------
 // Elementwise vector steps with fused reductions (all own-row pointers).

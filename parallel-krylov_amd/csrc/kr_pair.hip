@@ -14,27 +14,36 @@
 //  * Values: every entry of slot k (offset -W, -n, -1, 0, +1, +n, +W) is the
 //    same double V[k] (SpmvArgs::st_v, scalar registers).
 //  * Absent entries are exactly the box faces (x = 0 / 511, y = 0 / P-1,
-//    z = 0 / planes-1). Their operand is read as 0.0 -- zero pads at both ends
-//    of every LDS line (x faces), zero lines for positions outside [0, P)
-//    (y faces: the loads go out of the buffer's range and return 0), zero
-//    planes outside [0, planes) (z faces: the same, and level 1 is set to 0
-//    there) -- and V[k] * 0.0 = +-0 added to a running sum leaves it
-//    unchanged: a row sum starts at +0.0 and IEEE round-to-nearest addition
-//    gives -0 only for (-0) + (-0), so the sum is never -0, and s + (+-0) = s.
-//    V[k] is finite (the host checks), so every row equals scipy's
-//    csr_matvec bit for bit: its entries in stored order from 0.0, each
-//    product rounded, no FMA.
+//    z = 0 / planes-1). Their operand is read as 0.0 -- zero halo rows on the
+//    x faces, zero lines for positions outside [0, P) (y faces), zero planes
+//    outside [0, planes) (z faces; the loads go out of the buffer's range and
+//    return 0, level 1 is set to 0 there) -- and V[k] * 0.0 = +-0 added to a
+//    running sum leaves it unchanged: a row sum starts at +0.0 and IEEE
+//    round-to-nearest addition gives -0 only for (-0) + (-0), so the sum is
+//    never -0, and s + (+-0) = s. V[k] is finite (the host checks), so every
+//    row equals scipy's csr_matvec bit for bit: its entries in stored order
+//    from 0.0, each product rounded, no FMA.
 //  * The walk's bookkeeping is 32-bit and incremental; nothing in the loop
-//    divides. One plane step is ~20 scalar instructions per wave.
+//    divides. One plane step is ~30 scalar instructions per wave.
 //
-// Layout: a 1024-thread workgroup walks the adjacent positions p0, p0 + 1
-// (p0 even) over one plane segment; four 256-lane groups g = (H, C): line
-// half H, chain C (0: x1 = Ar[m+1], 1: x2 = Ay[m]); lane t owns rows 2t,
-// 2t + 1 of a line (the dual kernel's lane mapping):
+// Layout: a workgroup walks x-segment xs (SL = 512 / XS rows) of the adjacent
+// positions p0, p0 + 1 (p0 even) over one plane segment; four groups g = (H,
+// C) of SL / 2 lanes: line half H, chain C (0: x1 = Ar[m+1], 1: x2 = Ay[m]);
+// lane t owns rows 2t, 2t + 1 of the segment (the dual kernel's lane mapping
+// within its wave xs * SL / 128 + ...):
 //
 //   level 0 (loaded)  : positions p0-2 .. p0+3, group (H, C) loads 3H .. 3H+2
 //   level 1 (computed): positions p0-1 .. p0+2, group (H, C) computes 2H+1, 2H+2
 //   level 2 (stored)  : positions p0, p0+1, group (H, C) owns p0 + H
+//
+// An LDS line holds the segment's rows and two halo rows on each side (the
+// x neighbours of the segment's end rows, loaded with it; 0.0 on an x face).
+// The level-1 value of the own line's two halo rows (rows -1 and SL, the +-1
+// operands of level 2's end rows) is computed by two lanes of the group.
+// XS = 4: 256-thread workgroups, ~29 KB of LDS, four per CU, so one
+// workgroup's barriers overlap the others' work; XS = 1: one 1024-thread
+// workgroup per CU, halo rows always x faces. Measured (st2b_xsegments):
+// XS = 4 for the storing pair, XS = 1 for the products-only one.
 //
 // Step s (level 0 of plane s arrives, loaded one step ahead): level 1 of
 // plane s-1 is completed by its +W term and plane s's sum started (-W .. +n);
@@ -46,14 +55,16 @@
 // position p0 + H are accumulated by group (H, 0), dual m+1's (level 1 x
 // level 2) by group (H, 1) -- each lane plane by plane, row 2t then 2t+1,
 // the other chain's operands read from LDS -- exactly as the dual launch's
-// workgroup of that (position, segment) accumulates them; at each segment
-// boundary of a level's dual grid the group's accumulators go to that grid's
-// partial of the virtual workgroup (block_reduce_store's order).
+// wave of that (position, segment, x quarter) accumulates them; at each
+// segment boundary of a level's dual grid each wave's shuffle-reduced value
+// goes to its x quarter's slot of SpmvArgs::partq, and st2b_combine_kernel
+// sums the four quarters in block_reduce_store's order into the partial of
+// the virtual workgroup.
 #include "kr_spmv.h"
 
 // Ablations (timing-only library builds, wrong results; same-box A/B, never
 // the library build): bit 0 no level-2 sums or stores, 1 no products, 2 the
-// +-1 operands from the own rows (no ds_read2), 3 no second barrier.
+// +-1 operands from the own rows (no LDS reads for them), 3 no second barrier.
 #ifndef KR_ST2B_AB
 #define KR_ST2B_AB 0
 #endif
@@ -64,16 +75,15 @@
 namespace kr {
 namespace {
 
-constexpr int kBL = kSBlock + 4;  // an LDS line: 2 zero pads, 512 rows, 2 zero pads
-
+template <int XS>
 struct St2bLds {
-  double x0[2][6][kBL];        // level 0 of plane s: [chain][position p0-2+j]
-  double x1[2][4][kBL];        // level 1 of plane s-1: [chain][position p0-1+j]
-  double xa[2][2][kSBlock];    // [step parity][H]: chain 1's level 0 of plane s-1, own line
-  double xb[2][2][kSBlock];    // [H][level 1, 2]: chain 0's values of plane s-2, own line
-  double red[4][7 * 4];        // [group] flush reduction
+  static constexpr int SL = kSBlock / XS;  // rows per segment
+  static constexpr int LL = SL + 4;        // an LDS line: halo rows -2, -1, the segment, SL, SL+1
+  double x0[2][6][LL];  // level 0 of plane s: [chain][position p0-2+j][row + 2]
+  double x1[2][4][LL];  // level 1 of plane s-1: [chain][position p0-1+j][row + 2]
+  double xa[2][2][SL];  // [step parity][H]: chain 1's level 0 of plane s-1, own line
+  double xb[2][2][SL];  // [H][level 1, 2]: chain 0's values of plane s-2, own line
 };
-constexpr size_t kSt2bLds = sizeof(St2bLds);
 
 __device__ __forceinline__ dbl2v lds2(const double* p) { return *reinterpret_cast<const dbl2v*>(p); }
 __device__ __forceinline__ void lds2_st(double* p, dbl2v v) { *reinterpret_cast<dbl2v*>(p) = v; }
@@ -92,13 +102,31 @@ __device__ __forceinline__ dbl2v st2b_part(const double (&v)[7], dbl2v xw, dbl2v
   sl = sl + v[5] * pn.x;   sh = sh + v[5] * pn.y;
   return dbl2v{sl, sh};
 }
+// The same sum for one row.
+__device__ __forceinline__ double st2b_part1(const double (&v)[7], double xw, double mn, double m1,
+                                             double own, double p1, double pn) {
+  double s = 0.0;
+  s = s + v[0] * xw;
+  s = s + v[1] * mn;
+  s = s + v[2] * m1;
+  s = s + v[3] * own;
+  s = s + v[4] * p1;
+  s = s + v[5] * pn;
+  return s;
+}
 
-template <int EPI, bool PO, int H, int C>
-__device__ __forceinline__ void st2b_walk(const SpmvArgs& a, St2bLds& L, int t, int p0, int q,
-                                          int zs, int Zw) {
+template <int EPI, bool PO, int XS, int H, int C>
+__device__ __forceinline__ void st2b_walk(const SpmvArgs& a, St2bLds<XS>& L, int t, int p0, int xs,
+                                          int q, int zs, int Zw) {
+  using Lds = St2bLds<XS>;
+  constexpr int SL = Lds::SL;
+  constexpr int G = SL / 2;      // lanes per group
+  constexpr int NWG = G / 64;    // waves per group
   constexpr int NP = 7;
   constexpr int IO = H == 0 ? 1 : 0;  // own line among the group's two level-1 lines
-  constexpr int g = 2 * H + C;
+  constexpr int J2 = 2 + H;           // own line's level-0 index (x0), x1 index 1 + H
+  const int lane = t & 63, wig = t >> 6;
+  const int quarter = xs * NWG + wig;  // the dual workgroup's wave this wave stands for
   const int P = a.st_P, PP = P >> 3;
   const int W = P * kSBlock;
   const int planes = (int)(a.n / W);
@@ -108,34 +136,39 @@ __device__ __forceinline__ void st2b_walk(const SpmvArgs& a, St2bLds& L, int t, 
 #pragma unroll
   for (int k = 0; k < 7; ++k) v[k] = a.st_v[k];
 
-  // level-0 loads: line jj (position p0 - 2 + 3H + jj) of chain C at plane z;
-  // positions outside [0, P) and planes outside [0, planes) read 0 (offset
-  // past the buffer: the range check returns zeros)
+  // level-0 loads: segment xs of line jj (position p0 - 2 + 3H + jj) of
+  // chain C at plane z, and its halo chunk (even lanes rows -2, -1; odd lanes
+  // rows SL, SL+1); positions outside [0, P), planes outside [0, planes) and
+  // halo rows past an x face read 0 (offset past the buffer: the range check
+  // returns zeros)
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<double*>(C == 0 ? a.x1 : a.x2), 0, (int)(a.xlen * 8), 0x00020000);
   const uint32_t lb = (uint32_t)t * 16u;
+  const uint32_t hb = (lane & 1) ? (uint32_t)SL * 8u : (uint32_t)-16;
+  const uint32_t hm = -(uint32_t)((lane & 1) ? xs < XS - 1 : xs > 0);  // all ones: halo not a face
   uint32_t lbase[3], lok[3];
 #pragma unroll
   for (int jj = 0; jj < 3; ++jj) {
     const int pos = p0 - 2 + 3 * H + jj;
     lok[jj] = -(uint32_t)(pos >= 0 && pos < P);
-    lbase[jj] = (uint32_t)((a.xoff + (int64_t)pos * kSBlock) * 8);
+    lbase[jj] = (uint32_t)((a.xoff + (int64_t)pos * kSBlock + (int64_t)xs * SL) * 8);
   }
   const uint32_t wbytes = (uint32_t)W * 8u;
   constexpr uint32_t kOut = 0x80000000u;
   // the stage registers: written to LDS as soon as they arrive and reloaded
   // at once with the next plane (the own rows are read back from LDS), so
   // nothing copies a register a load is still writing
-  dbl2v st[3];
+  dbl2v st[3], sth[3];
   auto issue = [&](int z) {
     const uint32_t zm = -(uint32_t)((unsigned)z < (unsigned)planes);  // all ones: plane in range
     const uint32_t zo = (uint32_t)z * wbytes;
 #pragma unroll
     for (int jj = 0; jj < 3; ++jj) {
-      // branch-free select (a load under a branch costs the compiler's wait counts)
-      const uint32_t m = zm & lok[jj];
-      const uint32_t u = ((lbase[jj] + zo) & m) | (kOut & ~m);
-      st[jj] = st_bld2(rx, u + lb);
+      // branch-free selects (a load under a branch costs the compiler's wait counts)
+      const uint32_t m = zm & lok[jj], mh = m & hm;
+      const uint32_t u = lbase[jj] + zo;
+      st[jj] = st_bld2(rx, ((u & m) | (kOut & ~m)) + lb);
+      sth[jj] = st_bld2(rx, ((u + hb) & mh) | (kOut & ~mh));
     }
   };
   // level-1 lines outside [0, P) are 0 (the -n / +n of the y faces)
@@ -145,55 +178,42 @@ __device__ __forceinline__ void st2b_walk(const SpmvArgs& a, St2bLds& L, int t, 
     const int pos = p0 - 1 + 2 * H + i;
     l1ok[i] = pos >= 0 && pos < P;
   }
-  double* const ydst = (C == 0 ? a.y1 : a.y2) + (int64_t)pown * kSBlock + 2 * t;
+  double* const ydst =
+      (C == 0 ? a.y1 : a.y2) + (int64_t)pown * kSBlock + (int64_t)xs * SL + 2 * t;
 
-  // ---- products and their flushes (every group joins every flush: it holds a barrier)
-  double* const part = C == 0 ? a.partials : a.partials2;
+  // ---- products: each wave's shuffle-reduced value to its x quarter of the
+  // virtual workgroup (position, grid segment); st2b_combine_kernel sums them
   const int Z1 = a.st2_z1, Z2 = a.st2_z2;
   int seg = zs * ((C == 0 ? Z1 : Z2) / Zw);  // this group's level's current grid segment
   double acc[NP];
 #pragma unroll
   for (int k = 0; k < NP; ++k) acc[k] = 0.0;
-  auto flush = [&](bool mine) {
-    const int lane = t & 63, wave = t >> 6;
-    if (mine) {
+  auto flush = [&]() {
+    const int64_t vwg = 8 * ((int64_t)seg * PP + (pown - q * PP)) + q;
+    double* const dst = a.partq + ((int64_t)(C == 0 ? 0 : NP) * a.grid + vwg) * 4 + quarter;
 #pragma unroll
-      for (int k = 0; k < NP; ++k) {
-        double r = acc[k];
+    for (int k = 0; k < NP; ++k) {
+      double r = acc[k];
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) r += __shfl_down(r, off, 64);
-        if (lane == 0) L.red[g][k * 4 + wave] = r;
-      }
+      for (int off = 32; off > 0; off >>= 1) r += __shfl_down(r, off, 64);
+      if (lane == 0) dst[(int64_t)k * a.grid * 4] = r;
+      acc[k] = 0.0;
     }
-    __syncthreads();
-    if (mine) {
-      if (t < NP) {
-        const double* r = L.red[g] + t * 4;
-        double s = r[0];
-        s = s + r[1];
-        s = s + r[2];
-        s = s + r[3];
-        part[(int64_t)t * a.grid + 8 * ((int64_t)seg * PP + (pown - q * PP)) + q] = s;
-      }
-#pragma unroll
-      for (int k = 0; k < NP; ++k) acc[k] = 0.0;
-      ++seg;
-    }
-    __syncthreads();  // red[] is reused by the next flush
+    ++seg;
   };
   int sg1 = zs * (Z1 / Zw), sg2 = zs * (Z2 / Zw);
   int nb1 = (int)((int64_t)planes * (sg1 + 1) / Z1);  // level 1's next grid boundary
   int nb2 = (int)((int64_t)planes * (sg2 + 1) / Z2);
   auto cross1 = [&](int z) {
     if (z >= nb1) {
-      flush(C == 0);
+      if constexpr (C == 0) flush();
       ++sg1;
       nb1 = (int)((int64_t)planes * (sg1 + 1) / Z1);
     }
   };
   auto cross2 = [&](int z) {
     if (z >= nb2) {
-      flush(C == 1);
+      if constexpr (C == 1) flush();
       ++sg2;
       nb2 = (int)((int64_t)planes * (sg2 + 1) / Z2);
     }
@@ -206,6 +226,12 @@ __device__ __forceinline__ void st2b_walk(const SpmvArgs& a, St2bLds& L, int t, 
   dbl2v p2 = dbl2v{0.0, 0.0};     // partial level-2 sums of plane s-2
   dbl2v k1 = dbl2v{0.0, 0.0}, k2 = dbl2v{0.0, 0.0};  // C = 1: own level 1, 2 of plane s-3
   p1[0] = p1[1] = dbl2v{0.0, 0.0};
+  // the own line's level-1 halo rows (lanes 0 / 1 of the group's first wave:
+  // row -1 / SL): level 0 of plane s-1 there, partial sum of plane s-1
+  double hl0p = 0.0, hp1 = 0.0;
+  const bool hlane = wig == 0 && lane < 2;
+  const int hr = (lane & 1) ? SL : -1;
+  const bool hface = (lane & 1) ? xs == XS - 1 : xs == 0;
   const int tl = 2 + 2 * t;       // the lane's first row in an LDS line
 
   // C = 1: dual m+1's products at plane z (level 1, 2 of chain 0 from LDS)
@@ -229,7 +255,10 @@ __device__ __forceinline__ void st2b_walk(const SpmvArgs& a, St2bLds& L, int t, 
     // (1) plane s to LDS (chain 1 also hands its own line's level 0 of plane
     // s-1 to chain 0), then the next plane's loads into the stage registers
 #pragma unroll
-    for (int jj = 0; jj < 3; ++jj) lds2_st(&L.x0[C][3 * H + jj][tl], st[jj]);
+    for (int jj = 0; jj < 3; ++jj) {
+      lds2_st(&L.x0[C][3 * H + jj][tl], st[jj]);
+      if (wig == 0 && lane < 2) lds2_st(&L.x0[C][3 * H + jj][(lane & 1) ? SL + 2 : 0], sth[jj]);
+    }
     if constexpr (C == 1) lds2_st(&L.xa[s & 1][H][2 * t], l0p[IO]);
     issue(s + 1);
     __syncthreads();
@@ -250,9 +279,17 @@ __device__ __forceinline__ void st2b_walk(const SpmvArgs& a, St2bLds& L, int t, 
                         own, (KR_ST2B_AB & 4) ? own.x : line[2], lds2(&L.x0[C][j + 1][tl]));
       l0p[i] = own;
     }
-    // (4) level 1 of plane s-1 to LDS
+    // (4) level 1 of plane s-1 to LDS, with the own line's halo rows
 #pragma unroll
     for (int i = 0; i < 2; ++i) lds2_st(&L.x1[C][2 * H + i][tl], l1[i]);
+    if (hlane) {
+      const double* ln = &L.x0[C][J2][hr + 2];
+      const double own = ln[0];
+      const double c = hp1 + v[6] * own;
+      L.x1[C][1 + H][hr + 2] = (pok && l1ok[IO] && !hface) ? c : 0.0;
+      hp1 = st2b_part1(v, hl0p, L.x0[C][J2 - 1][hr + 2], ln[-1], own, ln[1], L.x0[C][J2 + 1][hr + 2]);
+      hl0p = own;
+    }
     if constexpr (!(KR_ST2B_AB & 8)) __syncthreads();
     // (5) dual m's products of plane s-1
     if (s - 1 >= z0 && s - 1 < z1) {
@@ -292,74 +329,328 @@ __device__ __forceinline__ void st2b_walk(const SpmvArgs& a, St2bLds& L, int t, 
   };
 
   // prologue: level 0 of plane z0-2 (the -W operand of plane z0-1's level
-  // 1), plane z0-1 in flight; the LDS lines' zero pads
+  // 1), plane z0-1 in flight
   issue(z0 - 2);
 #pragma unroll
   for (int i = 0; i < 2; ++i) l0p[i] = st[1 - H + i];
+  // the own line's halo rows of plane z0-2 (lane 0: row -1, lane 1: row SL):
+  // from the halo chunk (rows -2, -1 / SL, SL+1)
+  hl0p = (lane & 1) ? sth[1 - H + IO].x : sth[1 - H + IO].y;
   issue(z0 - 1);
   for (int s = z0 - 1; s <= z1 + 1; ++s) step(s);
   __syncthreads();
   level2_products(z1 - 1);  // the last plane's, written by the last step
-  flush(C == 0);            // level 1's last segment (groups (H, 0))
-  flush(C == 1);            // level 2's (groups (H, 1))
+  if constexpr (C == 0) flush();  // level 1's last segment (groups (H, 0))
+  if constexpr (C == 1) flush();  // level 2's (groups (H, 1))
 }
 
-template <int EPI, bool PO>
-__global__ __launch_bounds__(4 * kBlock) void spmv_stencil2b_kernel(SpmvArgs a) {
+// Waves per SIMD: XS = 4 four 256-thread workgroups per CU (16 waves), XS = 2
+// two of 512, XS = 1 one of 1024; <= 128 VGPRs in every case.
+template <int EPI, bool PO, int XS>
+__global__ __launch_bounds__(4 * kBlock / XS) __attribute__((amdgpu_waves_per_eu(4)))
+void spmv_stencil2b_kernel(SpmvArgs a) {
   if (a.stop && *a.stop != 0.0) return;
   extern __shared__ __attribute__((aligned(16))) double s2b_dyn[];
-  St2bLds& L = *reinterpret_cast<St2bLds*>(s2b_dyn);
-  // position-major tiles: XCD q = B & 7 walks the position pairs of
-  // [q P/8, (q+1) P/8) over the plane segments of the walk grid
+  St2bLds<XS>& L = *reinterpret_cast<St2bLds<XS>*>(s2b_dyn);
+  // XCD q = B & 7 walks the position pairs of [q P/8, (q+1) P/8): the x
+  // segments of a tile, then the tiles, then the plane segments
+  const int P = a.st_P, PP = P >> 3;
+  const int B = blockIdx.x, q = B & 7, w2 = B >> 3;
+  const int half = PP >> 1, Zw = gridDim.x / ((P >> 1) * XS);
+  const int xs = w2 % XS, w3 = w2 / XS;
+  const int p0 = q * PP + 2 * (w3 % half);
+  const int zs = w3 / half;
+  constexpr int G = kBlock / XS;  // lanes per group
+  const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / G));
+  const int t = (int)(threadIdx.x % G);
+  switch (g) {
+    case 0: st2b_walk<EPI, PO, XS, 0, 0>(a, L, t, p0, xs, q, zs, Zw); break;
+    case 1: st2b_walk<EPI, PO, XS, 0, 1>(a, L, t, p0, xs, q, zs, Zw); break;
+    case 2: st2b_walk<EPI, PO, XS, 1, 0>(a, L, t, p0, xs, q, zs, Zw); break;
+    default: st2b_walk<EPI, PO, XS, 1, 1>(a, L, t, p0, xs, q, zs, Zw); break;
+  }
+}
+
+// partials[kk * grid + v] = ((q0 + q1) + q2) + q3 of the four x quarters of
+// virtual workgroup v (block_reduce_store's order): kk < 7 over the n1
+// workgroups of dual m's grid, kk >= 7 over dual m+1's n2.
+__global__ __launch_bounds__(kBlock) void st2b_combine_kernel(const double* __restrict__ partq,
+                                                               double* __restrict__ partials,
+                                                               int grid, int n1, int n2) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int kk = (int)(i / grid), v = (int)(i % grid);
+  if (kk >= 14 || v >= (kk < 7 ? n1 : n2)) return;
+  const dbl2v lo = *reinterpret_cast<const dbl2v*>(partq + ((int64_t)kk * grid + v) * 4);
+  const dbl2v hi = *reinterpret_cast<const dbl2v*>(partq + ((int64_t)kk * grid + v) * 4 + 2);
+  double s = lo.x;
+  s = s + lo.y;
+  s = s + hi.x;
+  s = s + hi.y;
+  partials[(int64_t)kk * grid + v] = s;
+}
+
+template <int EPI, bool PO, int XS>
+void st2b_launch_t(const SpmvArgs& a, int nblocks, hipStream_t s) {
+  static std::atomic<uint64_t> opted{0};  // per device (opt_in_lds)
+  opt_in_lds(opted, reinterpret_cast<const void*>(spmv_stencil2b_kernel<EPI, PO, XS>),
+             sizeof(St2bLds<XS>));
+  spmv_stencil2b_kernel<EPI, PO, XS><<<nblocks, 4 * kBlock / XS, sizeof(St2bLds<XS>), s>>>(a);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
+template <int EPI, int XS>
+void st2b_launch_x(const SpmvArgs& a, int nblocks, hipStream_t s) {
+  if (a.products_only)
+    st2b_launch_t<EPI, true, XS>(a, nblocks, s);
+  else
+    st2b_launch_t<EPI, false, XS>(a, nblocks, s);
+}
+
+template <int EPI>
+void st2b_launch_e(const SpmvArgs& a, int nblocks, int xs, hipStream_t s) {
+  switch (xs) {
+    case 1: st2b_launch_x<EPI, 1>(a, nblocks, s); return;
+    case 2: st2b_launch_x<EPI, 2>(a, nblocks, s); return;
+    default: st2b_launch_x<EPI, 4>(a, nblocks, s); return;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// The box step pair: two consecutive fused k-skip MrR steps in ONE walk
+// (v3/gpu/kskipmrr.py:88-95, steps j and j+1 of an outer iteration; the
+// unfused kernels are EPI_STEP_MRR_NOX then EPI_STEP_MRR_X2, kr_spmv.h
+// epi_values). Step j: Ar1 = A r_a; y_b = eta_j y_a + zeta_j Ar1; z_b =
+// eta_j z_a - zeta_j r_a; r_b = r_a - y_b. Step j+1: Ar1' = A r_b; y_c =
+// eta' y_b + zeta' Ar1'; z_c = eta' z_b - zeta' r_b; r_c = r_b - y_c; x =
+// (x - z_b) - z_c. r_b (level 1) and y_b never leave the chip: 8 vectors of
+// HBM traffic (r, y, z, x in and out) instead of the two kernels' 14.
+//
+// The box pair's walk with one chain: a 1024-thread workgroup walks the
+// positions p0, p0 + 1 of a plane segment; group g (256 lanes, rows 2t, 2t+1)
+// owns level-1 line g (position p0-1+g): level 0 of r for lines 0 .. 5
+// (group 0 also loads line 0, group 3 line 5), y_a of its line; groups 1 and
+// 2 (positions p0, p0+1) also run level 2 and the stores. Every statement is
+// the unfused kernels', in their order, so the results are bitwise theirs.
+// y_c goes to another buffer than y_a (other workgroups still read y_a on
+// their halo lines), r_c to another than r_a; z and x in place (own rows).
+// ---------------------------------------------------------------------------
+struct Sp2bLds {
+  double x0[6][kSBlock + 4];  // r_a of plane s: [position p0-2+j][row + 2], zero pads
+  double x1[4][kSBlock + 4];  // r_b of plane s-1: [position p0-1+j][row + 2]
+};
+
+template <int G>
+__device__ __forceinline__ void sp2b_walk(const SpmvArgs& a, Sp2bLds& L, int t, int p0, int q,
+                                          int zs, int Zw) {
+  constexpr bool OUT = G == 1 || G == 2;  // level 2 and the stores
+  constexpr int J = G + 1;                // the group's level-1 line in x0
+  constexpr int NL = (G == 0 || G == 3) ? 2 : 1;  // r_a lines the group loads
+  constexpr int L0 = G == 0 ? 0 : G + 1;          // the first of them
+  const int P = a.st_P;
+  const int W = P * kSBlock;
+  const int planes = (int)(a.n / W);
+  const int z0 = (int)((int64_t)planes * zs / Zw), z1 = (int)((int64_t)planes * (zs + 1) / Zw);
+  (void)q;
+  double v[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) v[k] = a.st_v[k];
+  const double c0 = a.c0, c1 = a.c1, c2 = a.c2, c3 = a.c3;
+
+  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<double*>(a.x1), 0, (int)(a.xlen * 8), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<double*>(a.x2), 0, (int)(a.xlen * 8), 0x00020000);
+  const uint32_t lb = (uint32_t)t * 16u;
+  const uint32_t wbytes = (uint32_t)W * 8u;
+  constexpr uint32_t kOut = 0x80000000u;
+  uint32_t lbase[NL], lok[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int pos = p0 - 2 + L0 + i;
+    lok[i] = -(uint32_t)(pos >= 0 && pos < P);
+    lbase[i] = (uint32_t)((a.xoff + (int64_t)pos * kSBlock) * 8);
+  }
+  const int posj = p0 - 1 + G;
+  const bool jok = posj >= 0 && posj < P;
+  const uint32_t jbase = (uint32_t)((a.xoff + (int64_t)posj * kSBlock) * 8);
+  const uint32_t jm = -(uint32_t)jok;
+  // own rows of the output line (OUT groups): plane 0 row of lane t
+  const int64_t orow = (int64_t)posj * kSBlock + 2 * t;
+
+  dbl2v st[NL], sty, stz, stx;
+  auto issue = [&](int z) {  // r_a of plane z, y_a of plane z-1, z_a / x of plane z-2
+    const uint32_t zm = -(uint32_t)((unsigned)z < (unsigned)planes);
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const uint32_t m = zm & lok[i];
+      st[i] = st_bld2(rr, (((lbase[i] + (uint32_t)z * wbytes) & m) | (kOut & ~m)) + lb);
+    }
+    const uint32_t ym = -(uint32_t)((unsigned)(z - 1) < (unsigned)planes) & jm;
+    sty = st_bld2(ry, (((jbase + (uint32_t)(z - 1) * wbytes) & ym) | (kOut & ~ym)) + lb);
+    if constexpr (OUT) {
+      const int zz = (unsigned)(z - 2) < (unsigned)planes ? z - 2 : 0;  // past a face: unused
+      stz = *reinterpret_cast<const dbl2v*>(a.u2 + orow + (int64_t)zz * W);
+      stx = *reinterpret_cast<const dbl2v*>(a.us + orow + (int64_t)zz * W);
+    }
+  };
+
+  dbl2v l0p = dbl2v{0.0, 0.0};  // r_a of plane s-1, own column of line J
+  dbl2v p1 = dbl2v{0.0, 0.0};   // partial Ar1 sums of plane s-1
+  dbl2v ra2 = dbl2v{0.0, 0.0};  // OUT: r_a of plane s-2
+  dbl2v yb2 = dbl2v{0.0, 0.0};  // OUT: y_b of plane s-2
+  dbl2v l1p = dbl2v{0.0, 0.0};  // OUT: r_b of plane s-2
+  dbl2v p2 = dbl2v{0.0, 0.0};   // OUT: partial Ar1' sums of plane s-2
+  const int tl = 2 + 2 * t;
+
+  auto step = [&](int s) {
+    // (1) r_a of plane s to LDS; keep y_a (plane s-1), z_a and x (plane s-2)
+#pragma unroll
+    for (int i = 0; i < NL; ++i) lds2_st(&L.x0[L0 + i][tl], st[i]);
+    const dbl2v ya = sty;
+    dbl2v za = dbl2v{0.0, 0.0}, xa = dbl2v{0.0, 0.0};
+    if constexpr (OUT) {
+      za = stz;
+      xa = stx;
+    }
+    issue(s + 1);
+    __syncthreads();
+    // (2) step j at plane s-1 (line J): Ar1 completed by its +W term (this
+    // plane), then y_b, r_b; plane s's sum started
+    const double* line = &L.x0[J][tl];
+    const dbl2v own = lds2(line);
+    const dbl2v ar = dbl2v{p1.x + v[6] * own.x, p1.y + v[6] * own.y};
+    dbl2v yb, rb;
+    {
+      const double t1l = c0 * ya.x, t1h = c0 * ya.y;
+      const double t2l = c1 * ar.x, t2h = c1 * ar.y;
+      yb = dbl2v{t1l + t2l, t1h + t2h};
+      rb = dbl2v{l0p.x - yb.x, l0p.y - yb.y};
+    }
+    const bool pok = (unsigned)(s - 1) < (unsigned)planes;
+    if (!(pok && jok)) rb = dbl2v{0.0, 0.0};  // level 1 off the box: the absent operand
+    const dbl2v ra1 = l0p;  // r_a of plane s-1
+    p1 = st2b_part(v, l0p, lds2(&L.x0[J - 1][tl]), line[-1], own, line[2], lds2(&L.x0[J + 1][tl]));
+    l0p = own;
+    lds2_st(&L.x1[G][tl], rb);
+    __syncthreads();
+    if constexpr (OUT) {
+      // (3) step j+1 at plane s-2 (Ar1' completed by r_b of plane s-1), the
+      // stores; plane s-1's Ar1' sum started
+      const dbl2v ar2 = dbl2v{p2.x + v[6] * rb.x, p2.y + v[6] * rb.y};
+      if (s - 2 >= z0 && s - 2 < z1) {
+        // step j's z at plane s-2 (EPI_STEP_MRR_NOX: t3 = eta z; t4 = zeta r)
+        const double t3l = c0 * za.x, t3h = c0 * za.y;
+        const double t4l = c1 * ra2.x, t4h = c1 * ra2.y;
+        const dbl2v zb = dbl2v{t3l - t4l, t3h - t4h};
+        // step j+1 (EPI_STEP_MRR_X2)
+        const double s1l = c2 * yb2.x, s1h = c2 * yb2.y;
+        const double s2l = c3 * ar2.x, s2h = c3 * ar2.y;
+        const dbl2v yc = dbl2v{s1l + s2l, s1h + s2h};
+        const double s3l = c2 * zb.x, s3h = c2 * zb.y;
+        const double s4l = c3 * l1p.x, s4h = c3 * l1p.y;
+        const dbl2v zc = dbl2v{s3l - s4l, s3h - s4h};
+        const dbl2v xm = dbl2v{xa.x - zb.x, xa.y - zb.y};
+        const dbl2v xn = dbl2v{xm.x - zc.x, xm.y - zc.y};
+        const dbl2v rc = dbl2v{l1p.x - yc.x, l1p.y - yc.y};
+        const int64_t row = orow + (int64_t)(s - 2) * W;
+        __builtin_nontemporal_store(yc, reinterpret_cast<dbl2v*>(a.u1 + row));
+        __builtin_nontemporal_store(zc, reinterpret_cast<dbl2v*>(a.u2 + row));
+        __builtin_nontemporal_store(xn, reinterpret_cast<dbl2v*>(a.ud + row));
+        __builtin_nontemporal_store(rc, reinterpret_cast<dbl2v*>(a.y1 + row));
+      }
+      const double* lx = &L.x1[G][tl];
+      p2 = st2b_part(v, l1p, lds2(&L.x1[G - 1][tl]), lx[-1], rb, lx[2], lds2(&L.x1[G + 1][tl]));
+      l1p = rb;
+      yb2 = yb;
+      ra2 = ra1;
+    }
+  };
+
+  // prologue: r_a of plane z0-2 (the -W operand of plane z0-1), plane z0-1 in flight
+  issue(z0 - 2);
+  l0p = st[J - L0];
+  issue(z0 - 1);
+  for (int s = z0 - 1; s <= z1 + 1; ++s) step(s);
+}
+
+__global__ __launch_bounds__(4 * kBlock) __attribute__((amdgpu_waves_per_eu(4)))
+void spmv_step2b_kernel(SpmvArgs a) {
+  if (a.stop && *a.stop != 0.0) return;
+  extern __shared__ __attribute__((aligned(16))) double sp2b_dyn[];
+  Sp2bLds& L = *reinterpret_cast<Sp2bLds*>(sp2b_dyn);
+  // the LDS lines' zero pads (x faces), visible after the first step's barrier
+  if (threadIdx.x < 40) {
+    const int i = threadIdx.x >> 2, e = threadIdx.x & 3;  // line i of 10, pad e
+    double* line = i < 6 ? &L.x0[i][0] : &L.x1[i - 6][0];
+    line[e < 2 ? e : kSBlock + e] = 0.0;
+  }
   const int P = a.st_P, PP = P >> 3;
   const int B = blockIdx.x, q = B & 7, w2 = B >> 3;
   const int half = PP >> 1, Zw = gridDim.x / (P >> 1);
   const int p0 = q * PP + 2 * (w2 % half);
   const int zs = w2 / half;
-  // the LDS lines' zero pads (x faces), visible after the first step's barrier
-  if (threadIdx.x < 80) {
-    const int i = threadIdx.x >> 2, e = threadIdx.x & 3;  // line i of 20, pad e
-    double* line = i < 12 ? &L.x0[i / 6][i % 6][0] : &L.x1[(i - 12) / 4][(i - 12) % 4][0];
-    line[e < 2 ? e : kBL - 4 + e] = 0.0;
-  }
   const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kBlock));
   const int t = (int)(threadIdx.x % kBlock);
   switch (g) {
-    case 0: st2b_walk<EPI, PO, 0, 0>(a, L, t, p0, q, zs, Zw); break;
-    case 1: st2b_walk<EPI, PO, 0, 1>(a, L, t, p0, q, zs, Zw); break;
-    case 2: st2b_walk<EPI, PO, 1, 0>(a, L, t, p0, q, zs, Zw); break;
-    default: st2b_walk<EPI, PO, 1, 1>(a, L, t, p0, q, zs, Zw); break;
+    case 0: sp2b_walk<0>(a, L, t, p0, q, zs, Zw); break;
+    case 1: sp2b_walk<1>(a, L, t, p0, q, zs, Zw); break;
+    case 2: sp2b_walk<2>(a, L, t, p0, q, zs, Zw); break;
+    default: sp2b_walk<3>(a, L, t, p0, q, zs, Zw); break;
   }
-}
-
-template <int EPI, bool PO>
-void st2b_launch_t(const SpmvArgs& a, int nblocks, hipStream_t s) {
-  static std::atomic<uint64_t> opted{0};  // per device (opt_in_lds)
-  opt_in_lds(opted, reinterpret_cast<const void*>(spmv_stencil2b_kernel<EPI, PO>), kSt2bLds);
-  spmv_stencil2b_kernel<EPI, PO><<<nblocks, 4 * kBlock, kSt2bLds, s>>>(a);
-  KR_HIP_CHECK(hipGetLastError());
 }
 
 }  // namespace
 
-void launch_spmv_stencil2b(SpmvEpi epi, const SpmvArgs& a, int nblocks, hipStream_t s) {
+// x segments per line (KR_ST2B_XS for the storing pair, KR_ST2B_XS_PO for
+// the products-only one: 1, 2 or 4). Measured on C4 (one box, twice,
+// profiles/r06x): storing pair 1.29 / 1.28 / 1.32 ms at 4 / 2 / 1 segments,
+// products-only pair 1.26 / 1.24 / 1.13 ms (no stores to hide behind, the
+// halo loads cost more than the overlap gains).
+int st2b_xsegments(bool products_only) {
+  const int x = products_only ? KR_ENV("KR_ST2B_XS_PO", 1) : KR_ENV("KR_ST2B_XS", 4);
+  return x == 1 || x == 2 ? x : 4;
+}
+
+void launch_spmv_stencil2b(SpmvEpi epi, const SpmvArgs& a, int nblocks, int xs, int n1, int n2,
+                           hipStream_t s) {
   const int64_t W = (int64_t)a.st_P * kSBlock;
   const int64_t planes = a.st_P > 0 ? a.n / W : 0;
+  const int tiles = a.st_P / 2;
+  const int zw = tiles > 0 && xs > 0 ? nblocks / (tiles * xs) : 0;
   KR_REQUIRE(a.st_box && a.st_P % 16 == 0 && a.n == planes * W && planes >= 1 && a.rb_gap == 0 &&
-                 a.partials2 && a.st2_z1 > 0 && a.st2_z2 > 0 && nblocks % (a.st_P / 2) == 0 &&
-                 a.st2_z1 % (2 * nblocks / a.st_P) == 0 && a.st2_z2 % (2 * nblocks / a.st_P) == 0 &&
-                 planes >= a.st2_z1 && planes >= a.st2_z2 && (a.xlen + W) * 8 < (int64_t(1) << 31),
+                 a.partials && a.partq && a.st2_z1 > 0 && a.st2_z2 > 0 &&
+                 (xs == 1 || xs == 2 || xs == 4) && zw > 0 && nblocks == tiles * xs * zw &&
+                 a.st2_z1 % zw == 0 && a.st2_z2 % zw == 0 && planes >= a.st2_z1 &&
+                 planes >= a.st2_z2 && n1 == a.st_P * a.st2_z1 && n2 == a.st_P * a.st2_z2 &&
+                 n1 <= a.grid && n2 <= a.grid && (a.xlen + W) * 8 < (int64_t(1) << 31),
              "box fused basis pair: constant-coefficient 7-point box with n = 512, P % 16 == 0, "
              "whole planes, a walk grid dividing both dual grids");
-  const bool po = a.products_only != 0;
   if (epi == EPI_DUAL_MRR)
-    po ? st2b_launch_t<EPI_DUAL_MRR, true>(a, nblocks, s)
-       : st2b_launch_t<EPI_DUAL_MRR, false>(a, nblocks, s);
+    st2b_launch_e<EPI_DUAL_MRR>(a, nblocks, xs, s);
   else if (epi == EPI_DUAL_KCG)
-    po ? st2b_launch_t<EPI_DUAL_KCG, true>(a, nblocks, s)
-       : st2b_launch_t<EPI_DUAL_KCG, false>(a, nblocks, s);
+    st2b_launch_e<EPI_DUAL_KCG>(a, nblocks, xs, s);
   else
     throw Failure(KR_ERR_INVALID, "box fused basis pair: EPI_DUAL_MRR or EPI_DUAL_KCG");
+  const int64_t total = (int64_t)14 * a.grid;
+  st2b_combine_kernel<<<(int)((total + kBlock - 1) / kBlock), kBlock, 0, s>>>(a.partq, a.partials,
+                                                                               a.grid, n1, n2);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
+void launch_spmv_step2b(const SpmvArgs& a, int nblocks, hipStream_t s) {
+  const int64_t W = (int64_t)a.st_P * kSBlock;
+  const int64_t planes = a.st_P > 0 ? a.n / W : 0;
+  const int tiles = a.st_P / 2;
+  KR_REQUIRE(a.st_box && a.st_P % 16 == 0 && a.n == planes * W && planes >= 1 && a.rb_gap == 0 &&
+                 tiles > 0 && nblocks % tiles == 0 && nblocks / tiles <= planes && a.x1 &&
+                 a.x2 && a.u1 && a.u2 && a.us && a.ud && a.y1 && a.u1 != a.x2 + a.xoff &&
+                 a.y1 != a.x1 + a.xoff && (a.xlen + W) * 8 < (int64_t(1) << 31),
+             "box step pair: constant-coefficient 7-point box with n = 512, P % 16 == 0, "
+             "whole planes; y and r written to other buffers than they are read from");
+  static std::atomic<uint64_t> opted{0};
+  opt_in_lds(opted, reinterpret_cast<const void*>(spmv_step2b_kernel), sizeof(Sp2bLds));
+  spmv_step2b_kernel<<<nblocks, 4 * kBlock, sizeof(Sp2bLds), s>>>(a);
+  KR_HIP_CHECK(hipGetLastError());
 }
 
 }  // namespace kr

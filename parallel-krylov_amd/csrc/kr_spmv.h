@@ -13,6 +13,17 @@
 
 #include "kr_internal.h"
 
+// Timing-only ablation macros (KR_ST_AB, KR_DIAW_AB, KR_AB_NO_PROLOGUE,
+// KR_ST2T_TIMING; kr_pair.hip has KR_ST2B_AB) compile parts of kernels out
+// and give WRONG results: a build that sets one must also define
+// KR_ALLOW_WRONG_RESULTS, and only A/B libraries with their own file names
+// do (tools/micro/pair_ab_build.sh, tools/lib_ab.sh with EXTRA=...).
+#if ((defined(KR_ST_AB) && KR_ST_AB) || (defined(KR_DIAW_AB) && KR_DIAW_AB) || \
+     defined(KR_AB_NO_PROLOGUE) || defined(KR_ST2T_TIMING)) &&                   \
+    !defined(KR_ALLOW_WRONG_RESULTS)
+#error "ablation build (wrong results): define KR_ALLOW_WRONG_RESULTS, A/B libraries only"
+#endif
+
 namespace kr {
 
 template <int E>

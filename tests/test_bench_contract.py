@@ -6,6 +6,8 @@ kernel), and the full-size parity check compares history entries."""
 import json
 import os
 
+import pytest
+
 from conftest import REPO
 
 
@@ -184,9 +186,12 @@ def test_multi_shard_kernel_table_is_per_device():
     # have claimed more than the HBM peak: refused
     bogus = (8 * csr - d) / (0.88 * 1e6)
     assert bench.checked_frac(bogus) is None
-    # a shard count past the listed deltas reuses the last one
-    k2, s2 = bench.kernel_table([dict(eight[0], shards=2)], [d])
-    assert s2["spmv2_gram_mrr"][0] == 8 * csr - 2 * d
+    rec = bench.frac_fields(bogus)
+    assert rec["frac"] is None and "exceeds" in rec["frac_error"]  # said, not a silent null
+    assert "frac_error" not in bench.frac_fields(k1["spmv2_gram_mrr"]["gbs"])
+    # a shard count past the listed deltas is a bookkeeping error: refused
+    with pytest.raises(ValueError):
+        bench.kernel_table([dict(eight[0], shards=2)], [d])
     # non-SpMV kernels keep their bytes
     kv, sv = bench.kernel_table([dict(name="update_mrr", launches=2, total_ms=1.0,
                                       bytes_per_launch=1e9, shards=8)], [d] * 8)

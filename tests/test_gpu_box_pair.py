@@ -94,7 +94,14 @@ BOX_CASES = [("kskipmrr", "box512x16x12", 4, {}), ("kskipmrr", "box512x16x12", 5
              ("kskipmrr", "box512x16x64", 4, {"KR_PO_ZMAX": "1", "KR_ST2B_Z": "1"}),
              ("kskipmrr", "box512x16x64", 6, {"KR_ST2B_Z": "2"}),
              ("kskipcg", "box512x16x64", 4, {"KR_PO_ZMAX": "2", "KR_ST2B_Z": "1"}),
-             ("adaptivekskipmrr", "box512x16x64", 6, {})]
+             ("adaptivekskipmrr", "box512x16x64", 6, {}),
+             # x segments per line (KR_ST2B_XS, default 4): whole lines, halves
+             ("kskipmrr", "box512x16x12", 4, {"KR_ST2B_XS": "1", "KR_ST2B_XS_PO": "4"}),
+             ("kskipmrr", "box512x32x10", 5, {"KR_ST2B_XS": "2"}),
+             ("kskipcg", "box512x16x12", 4, {"KR_ST2B_XS": "2", "KR_ST2B_XS_PO": "2"}),
+             ("adaptivekskipmrr", "aniso512x16x12", 6, {"KR_ST2B_XS": "1"}),
+             ("kskipmrr", "box512x16x64", 4, {"KR_PO_ZMAX": "1", "KR_ST2B_Z": "1",
+                                              "KR_ST2B_XS": "2"})]
 
 
 @pytest.mark.gpu
@@ -158,3 +165,52 @@ def test_box_pair_not_used_off_the_box(monkeypatch):
     A = dropped_entry(box(512, 16, 12))
     st = _launches(A, "kskipmrr", 4, "3", monkeypatch)
     assert st.get("spmv2x2_gram_mrr", 0) == 0 and st.get("spmv2_gram_mrr", 0) > 0, st
+
+
+# the box step pair (KR_STEP2, default on for box shards): k-skip MrR steps j
+# (x deferred) and j+1 in one walk, against the two step launches
+STEP2_CASES = [("kskipmrr", "box512x16x12", 4, {}), ("kskipmrr", "box512x16x12", 5, {}),
+               ("kskipmrr", "box512x32x10", 3, {}), ("kskipmrr", "box512x32x10", 6, {}),
+               ("kskipmrr", "aniso512x16x12", 4, {}), ("adaptivekskipmrr", "box512x16x12", 8, {}),
+               ("adaptivekskipmrr", "box512x16x64", 6, {}),
+               ("kskipmrr", "box512x16x64", 4, {"KR_STEP2_Z": "1"}),
+               ("kskipmrr", "box512x16x64", 4, {"KR_STEP2_Z": "3"}),
+               ("kskipmrr", "box512x16x12", 4, {"KR_FUSE_FIRST": "0"}),
+               ("kskipmrr", "box512x16x12", 4, {"KR_ST2": "0"})]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method,name,k,env", STEP2_CASES,
+                         ids=[f"{m}-{n}-k{k}-{'-'.join(e)}" for m, n, k, e in STEP2_CASES])
+def test_box_step_pair_bitwise_equal_steps(monkeypatch, method, name, k, env):
+    """Histories and x bit for bit against the two step launches (KR_STEP2=0):
+    even and odd k, adaptive rollbacks, walks of 1 / 3 segments, without the
+    fused first steps, with the dual launches instead of the box pair."""
+    A = MATRICES[name]()
+    b = np.random.default_rng(7).standard_normal(A.shape[0])
+    kw = dict(tol=1e-10, maxiter=400, k=k)
+    monkeypatch.setenv("KRYLOV_AMD_SHARDS", "0")
+    for key, val in env.items():
+        monkeypatch.setenv(key, val)
+    out = []
+    for on in ("0", "1"):
+        monkeypatch.setenv("KR_STEP2", on)
+        with contextlib.redirect_stdout(io.StringIO()):
+            x, info = _solver(method)(A, b, **kw)
+        out.append((x.cpu().numpy(), info))
+    (x0, i0), (x1, i1) = out
+    np.testing.assert_array_equal(i1["nosl"], i0["nosl"])
+    if "khistory" in i0:
+        np.testing.assert_array_equal(i1["khistory"], i0["khistory"])
+    np.testing.assert_array_equal(i1["residual"], i0["residual"])
+    np.testing.assert_array_equal(x1, x0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,pairs", [(4, 1), (5, 2), (2, 0), (3, 1)])
+def test_box_step_pair_is_used(monkeypatch, k, pairs):
+    """k-skip MrR on a box shard: one step-pair launch per outer iteration
+    for each (even j >= 2, j+1 <= k) pair of steps after the fused first two."""
+    monkeypatch.delenv("KR_STEP2", raising=False)
+    st = _launches(MATRICES["box512x16x12"](), "kskipmrr", k, "3", monkeypatch)
+    assert st.get("spmv_step2_mrr_stencil", 0) == 4 * pairs, st

@@ -108,10 +108,16 @@ def test_c5_fullsize_matches_oracle():
     the N = 50M, h = 31 / W = 256 banded system) against the oracle
     (oracle.v3cpu.adaptivekskipmrr, bitwise the reference's v3/cpu) on the
     same matrix and b, two outer iterations (11 solver iterations): nosl and
-    khistory identical, every residual entry within 1e-12 relative (SURVEY.md
-    8c), x within 1e-11 relative. The host CSR needs ~760 B per row; N is 50M
-    unless the box has less than ~40 GB for it."""
+    khistory identical; every residual entry whose oracle value is >= 1e-8
+    within 1e-12 relative (the contract's regime), entries
+    below 1e-8 within max(1e-12, 10x the measured reordering envelope); x
+    within max(1e-11, 10x its envelope) -- the bound the contract leaves to
+    the k-skip x (DESIGN.md 7 records the measured envelope). The host CSR
+    needs ~760 B per row; N is 50M unless the box has less than ~40 GB for
+    it."""
     from oracle import matrices, v3cpu
+    if not matrices.ParCSR.available():
+        pytest.skip("oracle/liboracle_csrmv.so not built (oracle/build.sh failed or not run)")
     per_row = 64 * 12 + 8 + 14 * 8 * 2  # CSR + the oracle's vectors, bytes per row
     n = min(50_000_000, _host_budget_bytes() // per_row)
     assert n >= 5_000_000, f"host memory too small for the C5 parity check ({n} rows)"
@@ -138,7 +144,9 @@ def test_c5_fullsize_matches_oracle():
     np.testing.assert_array_equal(info["nosl"], ref["nosl"], err_msg=msg)
     np.testing.assert_array_equal(info["khistory"], ref["khistory"], err_msg=msg)
     rel = np.abs(info["residual"] - ref["residual"]) / np.abs(ref["residual"])
-    assert np.all(rel <= np.maximum(1e-12, 10.0 * env)), (msg, rel)
+    contract = np.abs(ref["residual"]) >= 1e-8
+    assert np.all(rel[contract] <= 1e-12), (msg, rel)
+    assert np.all(rel[~contract] <= np.maximum(1e-12, 10.0 * env[~contract])), (msg, rel)
     xrel = np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref)
     assert xrel <= max(1e-11, 10.0 * x_env), (msg, xrel)
     print(f"{msg}: residual max rel {rel.max():.2e}, x rel {xrel:.2e}, "

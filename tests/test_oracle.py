@@ -86,6 +86,8 @@ def test_parcsr_matvec_is_scipy_bitwise():
     oracle's A.dot."""
     import scipy.sparse as sp
     from oracle import matrices
+    if not matrices.ParCSR.available():
+        pytest.skip("oracle/liboracle_csrmv.so not built (oracle/build.sh failed or not run)")
     rng = np.random.default_rng(7)
     n = 4001
     rows = np.repeat(np.arange(n), rng.integers(0, 40, n))
