@@ -680,14 +680,16 @@ bool System::step2_ok() const {
   return s.st_box && s.st_P % 16 == 0;
 }
 
-void System::spmv_step2(int r_in, int r_out, int y_in, int y_out, int z, int xs, int xd,
-                        double eta0, double zeta0, double eta1, double zeta1) {
+void System::spmv_step2(int r_in, int r_out, int y_in, int y_out, int z, int xs, int xd, int xm,
+                        const double* c, int ar1, int xpend) {
   KR_REQUIRE(step2_ok(), "box step pair: shard not eligible");
-  KR_REQUIRE(r_out != r_in && y_out != y_in && y_out != r_in && r_out != y_in,
+  KR_REQUIRE(r_out != r_in && y_out != y_in && y_out != r_in && r_out != y_in &&
+                 (ar1 < 0 || (ar1 != r_out && ar1 != y_out)),
              "box step pair: r / y outputs alias their gathered inputs");
+  const bool virt = ar1 >= 0;
   Shard& s = shards[0];
   KR_HIP_CHECK(hipSetDevice(s.dev));
-  const char* nm = "spmv_step2_mrr_stencil";
+  const char* nm = virt ? "spmv_step3_mrr_stencil" : "spmv_step2_mrr_stencil";
   hipEvent_t t0 = nullptr;
   prof_begin(s, nm, t0);
   SpmvArgs a;
@@ -701,10 +703,16 @@ void System::spmv_step2(int r_in, int r_out, int y_in, int y_out, int z, int xs,
   a.u2 = s.own(z);
   a.us = s.own(xs);
   a.ud = s.own(xd);
-  a.c0 = eta0;
-  a.c1 = zeta0;
-  a.c2 = eta1;
-  a.c3 = zeta1;
+  a.c0 = c[0];
+  a.c1 = c[1];
+  a.c2 = c[2];
+  a.c3 = c[3];
+  if (virt) {
+    a.x3 = s.vec[ar1];
+    a.c4 = c[4];
+    a.c5 = c[5];
+    a.xpend = xpend;
+  }
   a.st_P = s.st_P;
   a.st_box = 1;
   for (int k = 0; k < 8; ++k) a.st_v[k] = s.st_v[k];
@@ -718,9 +726,11 @@ void System::spmv_step2(int r_in, int r_out, int y_in, int y_out, int z, int xs,
     while (zw < 16 && planes / (2 * zw) >= 8) zw *= 2;
   }
   zw = (int)std::min<int64_t>(zw, planes);
-  launch_spmv_step2b(a, (s.st_P / 2) * zw, s.stream);
-  // algorithmic bytes in CSR terms: A once, r, y, z, x in and r, y, z, x out
-  const double bytes = 12.0 * s.nnz + 4.0 * (s.n + 1) + 64.0 * s.n;
+  launch_spmv_step2b(a, (s.st_P / 2) * zw, virt ? 1 : 0, xm, s.stream);
+  // algorithmic bytes in CSR terms: A once, r, y, (Ar1,) z, x in and r, y,
+  // z, x out (x neither way when no step of the pair touches it)
+  const double vecs = (virt ? 9.0 : 8.0) - (virt || xm != 0 ? 0.0 : 2.0);
+  const double bytes = 12.0 * s.nnz + 4.0 * (s.n + 1) + 8.0 * vecs * s.n;
   prof_end(s, nm, t0, bytes);
 }
 
@@ -3237,7 +3247,20 @@ class KskipMrrSession : public Base {
       }
     };
     int j1 = 1;
-    if (sys->fuse_steps && sys->fuse_first && k >= 1) {
+    const bool step2 = sys->fuse_steps && sys->step2_ok();
+    if (step2 && sys->fuse_first && k >= 2 && KR_ENV("KR_STEP3", 1) != 0) {
+      // steps 0, 1 (FIRST2's) and 2 in one walk on a box shard: step 2 is an
+      // even step, x deferred (kind 0) or applied (kind 2, the last step)
+      const int kind2 = step_kind(2);
+      const double c[6] = {eta[0], zeta[0], eta[1], zeta[1], eta[2], zeta[2]};
+      sys->spmv_step2(r0, r_alt, y0, y_alt, Z, xsrc, cur, kind2 == 2 ? 4 : 0, c, AR(1),
+                      xpend ? 1 : 0);
+      xpend = kind2 == 0 && k == 2;  // xdefer: step 2's x -= z left to the next outer iteration
+      xsrc = cur;
+      std::swap(r0, r_alt);
+      std::swap(y0, y_alt);
+      j1 = 3;
+    } else if (sys->fuse_steps && sys->fuse_first && k >= 1) {
       // steps 0 (kind 0) and 1 (kind 1) in one SpMV: r1 is formed at every
       // gathered column from r0, y0, Ar1; new y and r go to the other buffers
       StepOps st;
@@ -3260,15 +3283,19 @@ class KskipMrrSession : public Base {
     } else {
       ew_step(0);
     }
-    const bool step2 = sys->fuse_steps && sys->step2_ok();
     for (int j = j1; j <= k; ++j) {
-      if (step2 && step_kind(j) == 0 && j + 1 <= k && step_kind(j + 1) == 1) {
-        // steps j (x deferred) and j+1 (x = (x - z_j) - z_{j+1}) in one walk
-        // on a box shard: r and y into their other buffers, z and x as the
-        // two step kernels write them (System::spmv_step2; bitwise those)
-        sys->spmv_step2(r0, r_alt, y0, y_alt, Z, xsrc, cur, eta[j], zeta[j], eta[j + 1],
-                        zeta[j + 1]);
-        xsrc = cur;
+      const int ka = step_kind(j), kb = j + 1 <= k ? step_kind(j + 1) : -1;
+      if (step2 && kb >= 0 && ka != 2) {
+        // steps j and j+1 in one walk on a box shard: r and y into their
+        // other buffers, z and x as the two step kernels write them
+        // (System::spmv_step2; bitwise those). x loses z_j's predecessor
+        // and z_j when step j is an x2 step, z_j when step j+1 is, z_{j+1}
+        // when step j+1 updates x at all
+        const int xm = (ka == 1 ? 3 : 0) | (kb == 1 ? 2 : 0) | (kb >= 1 ? 4 : 0);
+        const double c[4] = {eta[j], zeta[j], eta[j + 1], zeta[j + 1]};
+        sys->spmv_step2(r0, r_alt, y0, y_alt, Z, xsrc, cur, xm, c);
+        if (xm != 0) xsrc = cur;
+        if (kb == 0 && j + 1 == k) xpend = true;  // xdefer: left to the next outer iteration
         std::swap(r0, r_alt);
         std::swap(y0, y_alt);
         ++j;

@@ -315,9 +315,11 @@ struct System {
   // and j+1 (EPI_STEP_MRR_NOX + EPI_STEP_MRR_X2) in one walk on a box shard
   // (one shard, no communicator, P % 16 == 0). KR_STEP2=0 disables.
   bool step2_ok() const;
-  // r: r_in -> r_out, y: y_in -> y_out (other buffers), z in place, x: xs -> xd
-  void spmv_step2(int r_in, int r_out, int y_in, int y_out, int z, int xs, int xd, double eta0,
-                  double zeta0, double eta1, double zeta1);
+  // r: r_in -> r_out, y: y_in -> y_out (other buffers), z in place, x: xs ->
+  // xd; xm: which z's x loses (launch_spmv_step2b); ar1 >= 0: the step
+  // triple (steps 0-2, Ar1_0 = ar1, c[4..5] step 2's, xpend)
+  void spmv_step2(int r_in, int r_out, int y_in, int y_out, int z, int xs, int xd, int xm,
+                  const double* c, int ar1 = -1, int xpend = 0);
   // Shard::st_box from the code patterns (host copies h: the codes of every
   // row block, pid / first: the pattern ids and a block holding each)
   void build_box(Shard& s, const std::vector<uint8_t>& h, const std::vector<uint32_t>& pid,

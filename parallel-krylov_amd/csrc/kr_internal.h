@@ -204,6 +204,7 @@ struct SpmvArgs {
   const double* x3 = nullptr;  // EPI_STEP_MRR_FIRST2: Ar1 (halo-extended)
   const double* stop = nullptr;  // skip the launch when *stop != 0 (EwArgs::stop)
   double c2 = 0, c3 = 0;       // EPI_STEP_MRR_FIRST2: step-1 scalars (eta1, zeta1)
+  double c4 = 0, c5 = 0;       // the box step triple (launch_spmv_step2b virt): step 2's
   // EPI_STEP_MRR_FIRST2: the previous outer iteration's last x -= z is still
   // pending (its z is this launch's z input u2): x = ((x - z0) - z1) - z2
   int xpend = 0;
@@ -329,12 +330,14 @@ void launch_spmv_stencil2t_kcg(const SpmvArgs& a, int nblocks, hipStream_t s);
 // bitwise the dual launches'.
 void launch_spmv_stencil2b(SpmvEpi epi, const SpmvArgs& a, int nblocks, int xs, int n1, int n2,
                            hipStream_t s);
-// The box step pair (kr_pair.hip): k-skip MrR steps j (EPI_STEP_MRR_NOX) and
-// j+1 (EPI_STEP_MRR_X2) in one walk on a box shard: x1 = r_a (gathered), x2
-// = y_a (gathered), y1 = r_c, u1 = y_c (other buffers), u2 = z (in place),
-// us / ud = x source / destination, c0 c1 / c2 c3 = the steps' (eta, zeta);
-// nblocks = P/2 x walk segments. Bitwise the two step launches.
-void launch_spmv_step2b(const SpmvArgs& a, int nblocks, hipStream_t s);
+// The box step pair (kr_pair.hip): k-skip MrR steps j and j+1 in one walk on
+// a box shard: x1 = r_a (gathered), x2 = y_a (gathered), y1 = r_c, u1 = y_c
+// (other buffers), u2 = z (in place), us / ud = x source / destination, c0
+// c1 / c2 c3 = the steps' (eta, zeta); xm bits: x minus z_a (step j an x2
+// step), z_b, z_c -- 6 (nox, x2), 3 (x2, nox), 7 (x2, x). virt: steps 0, 1,
+// 2 (FIRST2 + the next): x3 = Ar1_0, c4 c5 step 2's, xpend, xm 0 or 4 (x minus
+// z_3). nblocks = P/2 x walk segments. Bitwise the step launches.
+void launch_spmv_step2b(const SpmvArgs& a, int nblocks, int virt, int xm, hipStream_t s);
 // x segments per line of the box pair (1, 2 or 4; kr_pair.hip)
 int st2b_xsegments(bool products_only);
 

@@ -417,13 +417,22 @@ void st2b_launch_e(const SpmvArgs& a, int nblocks, int xs, hipStream_t s) {
 
 // ---------------------------------------------------------------------------
 // The box step pair: two consecutive fused k-skip MrR steps in ONE walk
-// (v3/gpu/kskipmrr.py:88-95, steps j and j+1 of an outer iteration; the
-// unfused kernels are EPI_STEP_MRR_NOX then EPI_STEP_MRR_X2, kr_spmv.h
-// epi_values). Step j: Ar1 = A r_a; y_b = eta_j y_a + zeta_j Ar1; z_b =
-// eta_j z_a - zeta_j r_a; r_b = r_a - y_b. Step j+1: Ar1' = A r_b; y_c =
-// eta' y_b + zeta' Ar1'; z_c = eta' z_b - zeta' r_b; r_c = r_b - y_c; x =
-// (x - z_b) - z_c. r_b (level 1) and y_b never leave the chip: 8 vectors of
-// HBM traffic (r, y, z, x in and out) instead of the two kernels' 14.
+// (v3/gpu/kskipmrr.py:88-95; the unfused kernels are the EPI_STEP_MRR_*
+// epilogues, kr_spmv.h epi_values). Step j: Ar1 = A r_a; y_b = eta_j y_a +
+// zeta_j Ar1; z_b = eta_j z_a - zeta_j r_a; r_b = r_a - y_b. Step j+1: Ar1' =
+// A r_b; y_c = eta' y_b + zeta' Ar1'; z_c = eta' z_b - zeta' r_b; r_c = r_b -
+// y_c. x: the two steps' kinds (KskipMrrSession::step_kind) subtract z_a
+// (XM bit 0: step j is an x2 step), z_b (bit 1) and z_c (bit 2) in that
+// order, each rounded, as the two kernels do. r_b (level 1) and y_b never
+// leave the chip: 8 vectors of HBM traffic (r, y, z, x in and out) instead of
+// the two kernels' 14 (EPI_STEP_MRR_NOX 6 + EPI_STEP_MRR_X2 8).
+//
+// VIRT: steps 0, 1 and 2 of an outer iteration (EPI_STEP_MRR_FIRST2's two
+// steps, then step 2): level 0 is r_1 = r_0 - (eta_0 y_0 + zeta_0 Ar1_0),
+// formed from three gathered vectors as FIRST2 forms it (virtual_r1), level
+// 1 step 1 (c2, c3), level 2 step 2 (c4, c5); x = ((x [- z_0 if xpend]) -
+// z_1) - z_2 [- z_3: XM bit 2], FIRST2's statements. 9 vectors instead of
+// FIRST2's 9 plus the following step's 6.
 //
 // The box pair's walk with one chain: a 1024-thread workgroup walks the
 // positions p0, p0 + 1 of a plane segment; group g (256 lanes, rows 2t, 2t+1)
@@ -431,35 +440,40 @@ void st2b_launch_e(const SpmvArgs& a, int nblocks, int xs, hipStream_t s) {
 // (group 0 also loads line 0, group 3 line 5), y_a of its line; groups 1 and
 // 2 (positions p0, p0+1) also run level 2 and the stores. Every statement is
 // the unfused kernels', in their order, so the results are bitwise theirs.
-// y_c goes to another buffer than y_a (other workgroups still read y_a on
-// their halo lines), r_c to another than r_a; z and x in place (own rows).
+// y and r go to other buffers than they are read from (other workgroups
+// still read them on their halo lines); z and x in place (own rows).
 // ---------------------------------------------------------------------------
 struct Sp2bLds {
-  double x0[6][kSBlock + 4];  // r_a of plane s: [position p0-2+j][row + 2], zero pads
-  double x1[4][kSBlock + 4];  // r_b of plane s-1: [position p0-1+j][row + 2]
+  double x0[6][kSBlock + 4];  // level 0 of plane s: [position p0-2+j][row + 2], zero pads
+  double x1[4][kSBlock + 4];  // level 1 of plane s-1: [position p0-1+j][row + 2]
 };
 
-template <int G>
-__device__ __forceinline__ void sp2b_walk(const SpmvArgs& a, Sp2bLds& L, int t, int p0, int q,
-                                          int zs, int Zw) {
-  constexpr bool OUT = G == 1 || G == 2;  // level 2 and the stores
-  constexpr int J = G + 1;                // the group's level-1 line in x0
-  constexpr int NL = (G == 0 || G == 3) ? 2 : 1;  // r_a lines the group loads
+template <int G, bool VIRT, int XM>
+__device__ __forceinline__ void sp2b_walk(const SpmvArgs& a, Sp2bLds& L, int t, int p0, int zs,
+                                          int Zw) {
+  constexpr bool OUT = G == 1 || G == 2;          // level 2 and the stores
+  constexpr int J = G + 1;                        // the group's level-1 line in x0
+  constexpr int NL = (G == 0 || G == 3) ? 2 : 1;  // level-0 lines the group loads
   constexpr int L0 = G == 0 ? 0 : G + 1;          // the first of them
+  constexpr int NV = VIRT ? 3 : 1;                // gathered vectors per level-0 line
   const int P = a.st_P;
   const int W = P * kSBlock;
   const int planes = (int)(a.n / W);
   const int z0 = (int)((int64_t)planes * zs / Zw), z1 = (int)((int64_t)planes * (zs + 1) / Zw);
-  (void)q;
   double v[7];
 #pragma unroll
   for (int k = 0; k < 7; ++k) v[k] = a.st_v[k];
-  const double c0 = a.c0, c1 = a.c1, c2 = a.c2, c3 = a.c3;
+  // level 1 / level 2 scalars (VIRT: step 0's are c0, c1)
+  const double e1 = VIRT ? a.c2 : a.c0, f1 = VIRT ? a.c3 : a.c1;
+  const double e2 = VIRT ? a.c4 : a.c2, f2 = VIRT ? a.c5 : a.c3;
 
-  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<double*>(a.x1), 0, (int)(a.xlen * 8), 0x00020000);
-  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<double*>(a.x2), 0, (int)(a.xlen * 8), 0x00020000);
+  // gathered vectors: r (x1), and VIRT y_0 (x2), Ar1_0 (x3); y_a (x2) of the
+  // group's line otherwise
+  const __amdgpu_buffer_rsrc_t rv[3] = {
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(a.x1), 0, (int)(a.xlen * 8), 0x00020000),
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(a.x2), 0, (int)(a.xlen * 8), 0x00020000),
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(VIRT ? a.x3 : a.x2), 0,
+                                        (int)(a.xlen * 8), 0x00020000)};
   const uint32_t lb = (uint32_t)t * 16u;
   const uint32_t wbytes = (uint32_t)W * 8u;
   constexpr uint32_t kOut = 0x80000000u;
@@ -477,85 +491,133 @@ __device__ __forceinline__ void sp2b_walk(const SpmvArgs& a, Sp2bLds& L, int t, 
   // own rows of the output line (OUT groups): plane 0 row of lane t
   const int64_t orow = (int64_t)posj * kSBlock + 2 * t;
 
-  dbl2v st[NL], sty, stz, stx;
-  auto issue = [&](int z) {  // r_a of plane z, y_a of plane z-1, z_a / x of plane z-2
+  dbl2v st[NL][NV], sty, stz, stx;
+  auto issue = [&](int z) {  // level 0 of plane z, y_a of plane z-1, z_a / x of plane z-2
     const uint32_t zm = -(uint32_t)((unsigned)z < (unsigned)planes);
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const uint32_t m = zm & lok[i];
-      st[i] = st_bld2(rr, (((lbase[i] + (uint32_t)z * wbytes) & m) | (kOut & ~m)) + lb);
+      const uint32_t u = (((lbase[i] + (uint32_t)z * wbytes) & m) | (kOut & ~m)) + lb;
+#pragma unroll
+      for (int c = 0; c < NV; ++c) st[i][c] = st_bld2(rv[c], u);
     }
-    const uint32_t ym = -(uint32_t)((unsigned)(z - 1) < (unsigned)planes) & jm;
-    sty = st_bld2(ry, (((jbase + (uint32_t)(z - 1) * wbytes) & ym) | (kOut & ~ym)) + lb);
+    if constexpr (!VIRT) {
+      const uint32_t ym = -(uint32_t)((unsigned)(z - 1) < (unsigned)planes) & jm;
+      sty = st_bld2(rv[1], (((jbase + (uint32_t)(z - 1) * wbytes) & ym) | (kOut & ~ym)) + lb);
+    }
     if constexpr (OUT) {
       const int zz = (unsigned)(z - 2) < (unsigned)planes ? z - 2 : 0;  // past a face: unused
       stz = *reinterpret_cast<const dbl2v*>(a.u2 + orow + (int64_t)zz * W);
-      stx = *reinterpret_cast<const dbl2v*>(a.us + orow + (int64_t)zz * W);
+      if constexpr (XM != 0 || VIRT)
+        stx = *reinterpret_cast<const dbl2v*>(a.us + orow + (int64_t)zz * W);
     }
   };
 
-  dbl2v l0p = dbl2v{0.0, 0.0};  // r_a of plane s-1, own column of line J
-  dbl2v p1 = dbl2v{0.0, 0.0};   // partial Ar1 sums of plane s-1
-  dbl2v ra2 = dbl2v{0.0, 0.0};  // OUT: r_a of plane s-2
-  dbl2v yb2 = dbl2v{0.0, 0.0};  // OUT: y_b of plane s-2
-  dbl2v l1p = dbl2v{0.0, 0.0};  // OUT: r_b of plane s-2
-  dbl2v p2 = dbl2v{0.0, 0.0};   // OUT: partial Ar1' sums of plane s-2
+  dbl2v l0p = dbl2v{0.0, 0.0};  // level 0 of plane s-1, own column of line J
+  dbl2v p1 = dbl2v{0.0, 0.0};   // partial level-1 Ar1 sums of plane s-1
+  dbl2v ya1 = dbl2v{0.0, 0.0};  // VIRT: y_1 of plane s-1 (line J)
+  dbl2v ra2 = dbl2v{0.0, 0.0};  // OUT: level 0 of plane s-2 (r_a / VIRT r_1)
+  dbl2v r0h1 = dbl2v{0.0, 0.0}, r0h2 = dbl2v{0.0, 0.0};  // OUT, VIRT: r_0 of planes s-1, s-2
+  dbl2v yb2 = dbl2v{0.0, 0.0};  // OUT: level-1 y of plane s-2
+  dbl2v l1p = dbl2v{0.0, 0.0};  // OUT: level 1 of plane s-2
+  dbl2v p2 = dbl2v{0.0, 0.0};   // OUT: partial level-2 sums of plane s-2
   const int tl = 2 + 2 * t;
 
-  auto step = [&](int s) {
-    // (1) r_a of plane s to LDS; keep y_a (plane s-1), z_a and x (plane s-2)
+  // level 0 of the arriving plane into LDS (VIRT: r_1 formed from r_0, y_0,
+  // Ar1_0 exactly as virtual_r1 / FIRST2's epilogue round it); returns y_1
+  // of line J (VIRT)
+  auto arrive = [&]() {
+    dbl2v yj = dbl2v{0.0, 0.0};
 #pragma unroll
-    for (int i = 0; i < NL; ++i) lds2_st(&L.x0[L0 + i][tl], st[i]);
-    const dbl2v ya = sty;
+    for (int i = 0; i < NL; ++i) {
+      dbl2v lv = st[i][0];
+      if constexpr (VIRT) {
+        const dbl2v r0 = st[i][0], y0 = st[i][1], ar = st[i][2];
+        const double t1l = a.c0 * y0.x, t1h = a.c0 * y0.y;
+        const double t2l = a.c1 * ar.x, t2h = a.c1 * ar.y;
+        const dbl2v y1 = dbl2v{t1l + t2l, t1h + t2h};
+        lv = dbl2v{r0.x - y1.x, r0.y - y1.y};
+        if (L0 + i == J) yj = y1;
+      }
+      lds2_st(&L.x0[L0 + i][tl], lv);
+    }
+    return yj;
+  };
+
+  auto step = [&](int s) {
+    // (1) level 0 of plane s to LDS; keep y_a (plane s-1), z_a and x (plane s-2)
+    const dbl2v yj = arrive();
+    dbl2v r0own = dbl2v{0.0, 0.0};
+    if constexpr (VIRT && OUT) r0own = st[J - L0][0];
+    const dbl2v ya = VIRT ? ya1 : sty;
     dbl2v za = dbl2v{0.0, 0.0}, xa = dbl2v{0.0, 0.0};
     if constexpr (OUT) {
       za = stz;
-      xa = stx;
+      if constexpr (XM != 0 || VIRT) xa = stx;
     }
     issue(s + 1);
     __syncthreads();
-    // (2) step j at plane s-1 (line J): Ar1 completed by its +W term (this
+    // (2) level 1 at plane s-1 (line J): Ar1 completed by its +W term (this
     // plane), then y_b, r_b; plane s's sum started
     const double* line = &L.x0[J][tl];
     const dbl2v own = lds2(line);
     const dbl2v ar = dbl2v{p1.x + v[6] * own.x, p1.y + v[6] * own.y};
     dbl2v yb, rb;
     {
-      const double t1l = c0 * ya.x, t1h = c0 * ya.y;
-      const double t2l = c1 * ar.x, t2h = c1 * ar.y;
+      const double t1l = e1 * ya.x, t1h = e1 * ya.y;
+      const double t2l = f1 * ar.x, t2h = f1 * ar.y;
       yb = dbl2v{t1l + t2l, t1h + t2h};
       rb = dbl2v{l0p.x - yb.x, l0p.y - yb.y};
     }
     const bool pok = (unsigned)(s - 1) < (unsigned)planes;
     if (!(pok && jok)) rb = dbl2v{0.0, 0.0};  // level 1 off the box: the absent operand
-    const dbl2v ra1 = l0p;  // r_a of plane s-1
+    const dbl2v ra1 = l0p;  // level 0 of plane s-1
     p1 = st2b_part(v, l0p, lds2(&L.x0[J - 1][tl]), line[-1], own, line[2], lds2(&L.x0[J + 1][tl]));
     l0p = own;
+    if constexpr (VIRT) ya1 = yj;
     lds2_st(&L.x1[G][tl], rb);
     __syncthreads();
     if constexpr (OUT) {
-      // (3) step j+1 at plane s-2 (Ar1' completed by r_b of plane s-1), the
-      // stores; plane s-1's Ar1' sum started
+      // (3) level 2 at plane s-2 (Ar1' completed by level 1 of plane s-1),
+      // the stores; plane s-1's Ar1' sum started
       const dbl2v ar2 = dbl2v{p2.x + v[6] * rb.x, p2.y + v[6] * rb.y};
       if (s - 2 >= z0 && s - 2 < z1) {
-        // step j's z at plane s-2 (EPI_STEP_MRR_NOX: t3 = eta z; t4 = zeta r)
-        const double t3l = c0 * za.x, t3h = c0 * za.y;
-        const double t4l = c1 * ra2.x, t4h = c1 * ra2.y;
-        const dbl2v zb = dbl2v{t3l - t4l, t3h - t4h};
-        // step j+1 (EPI_STEP_MRR_X2)
-        const double s1l = c2 * yb2.x, s1h = c2 * yb2.y;
-        const double s2l = c3 * ar2.x, s2h = c3 * ar2.y;
+        // z and x of the steps before level 2, in the unfused kernels' order
+        dbl2v zb, xn = xa;
+        if constexpr (VIRT) {
+          // FIRST2: z_1 = eta_0 z_0 - zeta_0 r_0; z_2 = eta_1 z_1 - zeta_1 r_1;
+          // x = ((xpend ? x - z_0 : x) - z_1) - z_2
+          const double t3l = a.c0 * za.x, t3h = a.c0 * za.y;
+          const double t4l = a.c1 * r0h2.x, t4h = a.c1 * r0h2.y;
+          const dbl2v zz1 = dbl2v{t3l - t4l, t3h - t4h};
+          const double s3l = e1 * zz1.x, s3h = e1 * zz1.y;
+          const double s4l = f1 * ra2.x, s4h = f1 * ra2.y;
+          zb = dbl2v{s3l - s4l, s3h - s4h};
+          if (a.xpend) xn = dbl2v{xn.x - za.x, xn.y - za.y};
+          xn = dbl2v{xn.x - zz1.x, xn.y - zz1.y};
+          xn = dbl2v{xn.x - zb.x, xn.y - zb.y};
+        } else {
+          // step j: z_b = eta_j z_a - zeta_j r_a; x2: x - z_a, then - z_b
+          const double t3l = e1 * za.x, t3h = e1 * za.y;
+          const double t4l = f1 * ra2.x, t4h = f1 * ra2.y;
+          zb = dbl2v{t3l - t4l, t3h - t4h};
+          if constexpr (XM & 1) xn = dbl2v{xn.x - za.x, xn.y - za.y};
+          if constexpr (XM & 2) xn = dbl2v{xn.x - zb.x, xn.y - zb.y};
+        }
+        // the level-2 step (EPI_STEP_MRR_*: y, z, r; x - z_c)
+        const double s1l = e2 * yb2.x, s1h = e2 * yb2.y;
+        const double s2l = f2 * ar2.x, s2h = f2 * ar2.y;
         const dbl2v yc = dbl2v{s1l + s2l, s1h + s2h};
-        const double s3l = c2 * zb.x, s3h = c2 * zb.y;
-        const double s4l = c3 * l1p.x, s4h = c3 * l1p.y;
+        const double s3l = e2 * zb.x, s3h = e2 * zb.y;
+        const double s4l = f2 * l1p.x, s4h = f2 * l1p.y;
         const dbl2v zc = dbl2v{s3l - s4l, s3h - s4h};
-        const dbl2v xm = dbl2v{xa.x - zb.x, xa.y - zb.y};
-        const dbl2v xn = dbl2v{xm.x - zc.x, xm.y - zc.y};
+        if constexpr (XM & 4) xn = dbl2v{xn.x - zc.x, xn.y - zc.y};
         const dbl2v rc = dbl2v{l1p.x - yc.x, l1p.y - yc.y};
         const int64_t row = orow + (int64_t)(s - 2) * W;
         __builtin_nontemporal_store(yc, reinterpret_cast<dbl2v*>(a.u1 + row));
         __builtin_nontemporal_store(zc, reinterpret_cast<dbl2v*>(a.u2 + row));
-        __builtin_nontemporal_store(xn, reinterpret_cast<dbl2v*>(a.ud + row));
+        if constexpr (XM != 0 || VIRT)
+          __builtin_nontemporal_store(xn, reinterpret_cast<dbl2v*>(a.ud + row));
         __builtin_nontemporal_store(rc, reinterpret_cast<dbl2v*>(a.y1 + row));
       }
       const double* lx = &L.x1[G][tl];
@@ -563,16 +625,27 @@ __device__ __forceinline__ void sp2b_walk(const SpmvArgs& a, Sp2bLds& L, int t, 
       l1p = rb;
       yb2 = yb;
       ra2 = ra1;
+      if constexpr (VIRT) {
+        r0h2 = r0h1;
+        r0h1 = r0own;
+      }
     }
   };
 
-  // prologue: r_a of plane z0-2 (the -W operand of plane z0-1), plane z0-1 in flight
+  // prologue: level 0 of plane z0-2 (the -W operand of plane z0-1), plane
+  // z0-1 in flight
   issue(z0 - 2);
-  l0p = st[J - L0];
+  {
+    const dbl2v yj = arrive();  // LDS lines overwritten by the first step before any read
+    l0p = lds2(&L.x0[J][tl]);
+    if constexpr (VIRT) ya1 = yj;
+    if constexpr (VIRT && OUT) r0h1 = st[J - L0][0];
+  }
   issue(z0 - 1);
   for (int s = z0 - 1; s <= z1 + 1; ++s) step(s);
 }
 
+template <bool VIRT, int XM>
 __global__ __launch_bounds__(4 * kBlock) __attribute__((amdgpu_waves_per_eu(4)))
 void spmv_step2b_kernel(SpmvArgs a) {
   if (a.stop && *a.stop != 0.0) return;
@@ -592,11 +665,19 @@ void spmv_step2b_kernel(SpmvArgs a) {
   const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kBlock));
   const int t = (int)(threadIdx.x % kBlock);
   switch (g) {
-    case 0: sp2b_walk<0>(a, L, t, p0, q, zs, Zw); break;
-    case 1: sp2b_walk<1>(a, L, t, p0, q, zs, Zw); break;
-    case 2: sp2b_walk<2>(a, L, t, p0, q, zs, Zw); break;
-    default: sp2b_walk<3>(a, L, t, p0, q, zs, Zw); break;
+    case 0: sp2b_walk<0, VIRT, XM>(a, L, t, p0, zs, Zw); break;
+    case 1: sp2b_walk<1, VIRT, XM>(a, L, t, p0, zs, Zw); break;
+    case 2: sp2b_walk<2, VIRT, XM>(a, L, t, p0, zs, Zw); break;
+    default: sp2b_walk<3, VIRT, XM>(a, L, t, p0, zs, Zw); break;
   }
+}
+
+template <bool VIRT, int XM>
+void sp2b_launch_t(const SpmvArgs& a, int nblocks, hipStream_t s) {
+  static std::atomic<uint64_t> opted{0};
+  opt_in_lds(opted, reinterpret_cast<const void*>(spmv_step2b_kernel<VIRT, XM>), sizeof(Sp2bLds));
+  spmv_step2b_kernel<VIRT, XM><<<nblocks, 4 * kBlock, sizeof(Sp2bLds), s>>>(a);
+  KR_HIP_CHECK(hipGetLastError());
 }
 
 }  // namespace
@@ -637,20 +718,31 @@ void launch_spmv_stencil2b(SpmvEpi epi, const SpmvArgs& a, int nblocks, int xs, 
   KR_HIP_CHECK(hipGetLastError());
 }
 
-void launch_spmv_step2b(const SpmvArgs& a, int nblocks, hipStream_t s) {
+void launch_spmv_step2b(const SpmvArgs& a, int nblocks, int virt, int xm, hipStream_t s) {
   const int64_t W = (int64_t)a.st_P * kSBlock;
   const int64_t planes = a.st_P > 0 ? a.n / W : 0;
   const int tiles = a.st_P / 2;
   KR_REQUIRE(a.st_box && a.st_P % 16 == 0 && a.n == planes * W && planes >= 1 && a.rb_gap == 0 &&
                  tiles > 0 && nblocks % tiles == 0 && nblocks / tiles <= planes && a.x1 &&
-                 a.x2 && a.u1 && a.u2 && a.us && a.ud && a.y1 && a.u1 != a.x2 + a.xoff &&
-                 a.y1 != a.x1 + a.xoff && (a.xlen + W) * 8 < (int64_t(1) << 31),
+                 a.x2 && (!virt || a.x3) && a.u1 && a.u2 && a.y1 && (xm == 0 || (a.us && a.ud)) &&
+                 (!virt || (a.us && a.ud)) && a.u1 != a.x2 + a.xoff && a.y1 != a.x1 + a.xoff &&
+                 (a.xlen + W) * 8 < (int64_t(1) << 31),
              "box step pair: constant-coefficient 7-point box with n = 512, P % 16 == 0, "
              "whole planes; y and r written to other buffers than they are read from");
-  static std::atomic<uint64_t> opted{0};
-  opt_in_lds(opted, reinterpret_cast<const void*>(spmv_step2b_kernel), sizeof(Sp2bLds));
-  spmv_step2b_kernel<<<nblocks, 4 * kBlock, sizeof(Sp2bLds), s>>>(a);
-  KR_HIP_CHECK(hipGetLastError());
+  if (virt) {
+    KR_REQUIRE(xm == 0 || xm == 4, "box step triple: x minus z_3 or nothing more");
+    if (xm == 4)
+      sp2b_launch_t<true, 4>(a, nblocks, s);
+    else
+      sp2b_launch_t<true, 0>(a, nblocks, s);
+    return;
+  }
+  switch (xm) {
+    case 6: sp2b_launch_t<false, 6>(a, nblocks, s); return;  // (nox, x2)
+    case 3: sp2b_launch_t<false, 3>(a, nblocks, s); return;  // (x2, nox)
+    case 7: sp2b_launch_t<false, 7>(a, nblocks, s); return;  // (x2, x)
+    default: throw Failure(KR_ERR_INVALID, "box step pair: unsupported step kinds");
+  }
 }
 
 }  // namespace kr

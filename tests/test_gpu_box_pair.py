@@ -167,15 +167,22 @@ def test_box_pair_not_used_off_the_box(monkeypatch):
     assert st.get("spmv2x2_gram_mrr", 0) == 0 and st.get("spmv2_gram_mrr", 0) > 0, st
 
 
-# the box step pair (KR_STEP2, default on for box shards): k-skip MrR steps j
-# (x deferred) and j+1 in one walk, against the two step launches
+# the box step walks (KR_STEP2, default on for box shards): steps 0-2 in one
+# walk (the step triple, KR_STEP3) and pairs of the later steps in one walk
+# each (x2 / nox / x kinds), against the step launches
 STEP2_CASES = [("kskipmrr", "box512x16x12", 4, {}), ("kskipmrr", "box512x16x12", 5, {}),
                ("kskipmrr", "box512x32x10", 3, {}), ("kskipmrr", "box512x32x10", 6, {}),
+               ("kskipmrr", "box512x16x12", 2, {}), ("kskipmrr", "box512x16x12", 7, {}),
                ("kskipmrr", "aniso512x16x12", 4, {}), ("adaptivekskipmrr", "box512x16x12", 8, {}),
                ("adaptivekskipmrr", "box512x16x64", 6, {}),
+               ("adaptivekskipmrr", "aniso512x16x12", 3, {}),
                ("kskipmrr", "box512x16x64", 4, {"KR_STEP2_Z": "1"}),
                ("kskipmrr", "box512x16x64", 4, {"KR_STEP2_Z": "3"}),
+               ("kskipmrr", "box512x16x12", 4, {"KR_STEP3": "0"}),
+               ("kskipmrr", "box512x16x12", 5, {"KR_STEP3": "0"}),
                ("kskipmrr", "box512x16x12", 4, {"KR_FUSE_FIRST": "0"}),
+               ("kskipmrr", "box512x16x12", 5, {"KR_FUSE_FIRST": "0"}),
+               ("adaptivekskipmrr", "box512x16x12", 6, {"KR_FUSE_FIRST": "0"}),
                ("kskipmrr", "box512x16x12", 4, {"KR_ST2": "0"})]
 
 
@@ -183,9 +190,10 @@ STEP2_CASES = [("kskipmrr", "box512x16x12", 4, {}), ("kskipmrr", "box512x16x12",
 @pytest.mark.parametrize("method,name,k,env", STEP2_CASES,
                          ids=[f"{m}-{n}-k{k}-{'-'.join(e)}" for m, n, k, e in STEP2_CASES])
 def test_box_step_pair_bitwise_equal_steps(monkeypatch, method, name, k, env):
-    """Histories and x bit for bit against the two step launches (KR_STEP2=0):
-    even and odd k, adaptive rollbacks, walks of 1 / 3 segments, without the
-    fused first steps, with the dual launches instead of the box pair."""
+    """Histories and x bit for bit against the step launches (KR_STEP2=0):
+    even and odd k (every pair of step kinds, the deferred x), adaptive
+    rollbacks, walks of 1 / 3 segments, pairs without the triple, without
+    the fused first steps, with the dual launches instead of the box pair."""
     A = MATRICES[name]()
     b = np.random.default_rng(7).standard_normal(A.shape[0])
     kw = dict(tol=1e-10, maxiter=400, k=k)
@@ -207,10 +215,12 @@ def test_box_step_pair_bitwise_equal_steps(monkeypatch, method, name, k, env):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("k,pairs", [(4, 1), (5, 2), (2, 0), (3, 1)])
-def test_box_step_pair_is_used(monkeypatch, k, pairs):
-    """k-skip MrR on a box shard: one step-pair launch per outer iteration
-    for each (even j >= 2, j+1 <= k) pair of steps after the fused first two."""
+@pytest.mark.parametrize("k,triples,pairs", [(4, 1, 1), (5, 1, 1), (2, 1, 0), (3, 1, 0),
+                                             (6, 1, 2), (1, 0, 0)])
+def test_box_step_pair_is_used(monkeypatch, k, triples, pairs):
+    """k-skip MrR on a box shard: per outer iteration one step-triple launch
+    (steps 0-2) and one step-pair launch per later pair of steps."""
     monkeypatch.delenv("KR_STEP2", raising=False)
     st = _launches(MATRICES["box512x16x12"](), "kskipmrr", k, "3", monkeypatch)
+    assert st.get("spmv_step3_mrr_stencil", 0) == 4 * triples, st
     assert st.get("spmv_step2_mrr_stencil", 0) == 4 * pairs, st
