@@ -64,7 +64,8 @@
 
 // Ablations (timing-only library builds, wrong results; same-box A/B, never
 // the library build): bit 0 no level-2 sums or stores, 1 no products, 2 the
-// +-1 operands from the own rows (no LDS reads for them), 3 no second barrier.
+// +-1 operands from the own rows (no LDS reads for them), 3 no second barrier,
+// 4 no level-0 LDS stores, 5 no level-1 LDS stores, 6 no product exchange stores.
 #ifndef KR_ST2B_AB
 #define KR_ST2B_AB 0
 #endif
@@ -256,10 +257,11 @@ __device__ __forceinline__ void st2b_walk(const SpmvArgs& a, St2bLds<XS>& L, int
     // s-1 to chain 0), then the next plane's loads into the stage registers
 #pragma unroll
     for (int jj = 0; jj < 3; ++jj) {
-      lds2_st(&L.x0[C][3 * H + jj][tl], st[jj]);
+      if constexpr (!(KR_ST2B_AB & 16)) lds2_st(&L.x0[C][3 * H + jj][tl], st[jj]);
+      else if (st[jj].x == 1234.5) lds2_st(&L.x0[C][3 * H + jj][tl], st[jj]);
       if (wig == 0 && lane < 2) lds2_st(&L.x0[C][3 * H + jj][(lane & 1) ? SL + 2 : 0], sth[jj]);
     }
-    if constexpr (C == 1) lds2_st(&L.xa[s & 1][H][2 * t], l0p[IO]);
+    if constexpr (C == 1 && !(KR_ST2B_AB & 64)) lds2_st(&L.xa[s & 1][H][2 * t], l0p[IO]);
     issue(s + 1);
     __syncthreads();
     // (2) dual m+1's products of plane s-3
@@ -281,7 +283,9 @@ __device__ __forceinline__ void st2b_walk(const SpmvArgs& a, St2bLds<XS>& L, int
     }
     // (4) level 1 of plane s-1 to LDS, with the own line's halo rows
 #pragma unroll
-    for (int i = 0; i < 2; ++i) lds2_st(&L.x1[C][2 * H + i][tl], l1[i]);
+    for (int i = 0; i < 2; ++i)
+      if constexpr (!(KR_ST2B_AB & 32)) lds2_st(&L.x1[C][2 * H + i][tl], l1[i]);
+      else if (l1[i].x == 1234.5) lds2_st(&L.x1[C][2 * H + i][tl], l1[i]);
     if (hlane) {
       const double* ln = &L.x0[C][J2][hr + 2];
       const double own = ln[0];
@@ -315,8 +319,12 @@ __device__ __forceinline__ void st2b_walk(const SpmvArgs& a, St2bLds<XS>& L, int
           __builtin_nontemporal_store(l2, reinterpret_cast<dbl2v*>(ydst + (int64_t)(s - 2) * W));
       }
       if constexpr (C == 0) {
-        lds2_st(&L.xb[H][0][2 * t], l1p);
-        lds2_st(&L.xb[H][1][2 * t], l2);
+        if constexpr (!(KR_ST2B_AB & 64)) {
+          lds2_st(&L.xb[H][0][2 * t], l1p);
+          lds2_st(&L.xb[H][1][2 * t], l2);
+        } else {
+          acc[1] += l2.x;
+        }
       } else {
         k1 = l1p;
         k2 = l2;

@@ -56,7 +56,10 @@ int main(int argc, char** argv) {
   // capture-crash bisection (round 5): 0 the engine's pattern; 1 no waits on
   // the neighbours' events (each comm / compute stream waits its own shard's
   // only); 2 a fresh event for every record (no event recorded twice in one
-  // capture); 3 both
+  // capture); 3 both. Round 6, one edge class at a time: 4 no cross waits on
+  // the comm streams only (lines 94-95), 8 on the compute streams only
+  // (117-118), 16 no D2H copy per stream (138), 32 no capture-info harvest
+  // of the step launches' nodes (107, 127)
   const int MODE = argc > 5 ? atoi(argv[5]) : 0;
   std::vector<hipStream_t> st(S), cs(S);
   std::vector<hipEvent_t> ev_in(S), ev_out(S), ev_join(2 * S);
@@ -86,19 +89,20 @@ int main(int argc, char** argv) {
       a.c[0] = m;
       const bool fresh = capture && (MODE & 2);
       const bool cross = !(MODE & 1);
+      const bool cross_comm = cross && !(MODE & 4), cross_comp = cross && !(MODE & 8);
       auto EI = [&](int s) { return fresh ? ev_in_m[m * S + s] : ev_in[s]; };
       auto EO = [&](int s) { return fresh ? ev_out_m[m * S + s] : ev_out[s]; };
       for (int s = 0; s < S; ++s) CK(hipEventRecord(EI(s), st[s]));
       for (int s = 0; s < S; ++s) {
         CK(hipStreamWaitEvent(cs[s], EI(s), 0));
-        if (cross && s > 0) CK(hipStreamWaitEvent(cs[s], EI(s - 1), 0));
-        if (cross && s + 1 < S) CK(hipStreamWaitEvent(cs[s], EI(s + 1), 0));
+        if (cross_comm && s > 0) CK(hipStreamWaitEvent(cs[s], EI(s - 1), 0));
+        if (cross_comm && s + 1 < S) CK(hipStreamWaitEvent(cs[s], EI(s + 1), 0));
         if (g_trace) printf("> launch gather s=%d m=%d\n", s, m);
         work<<<G, 256, 0, cs[s]>>>(a);
         CK(hipEventRecord(EO(s), cs[s]));
         if (g_trace) printf("> launch interior s=%d m=%d\n", s, m);
         work<<<G, 256, 0, st[s]>>>(a);
-        if (capture && step && coef) {
+        if (capture && step && coef && !(MODE & 32)) {
           hipStreamCaptureStatus cst;
           unsigned long long cid = 0;
           hipGraph_t cg = nullptr;
@@ -114,11 +118,11 @@ int main(int argc, char** argv) {
       }
       for (int s = 0; s < S; ++s) {
         CK(hipStreamWaitEvent(st[s], EO(s), 0));
-        if (cross && s > 0) CK(hipStreamWaitEvent(st[s], EO(s - 1), 0));
-        if (cross && s + 1 < S) CK(hipStreamWaitEvent(st[s], EO(s + 1), 0));
+        if (cross_comp && s > 0) CK(hipStreamWaitEvent(st[s], EO(s - 1), 0));
+        if (cross_comp && s + 1 < S) CK(hipStreamWaitEvent(st[s], EO(s + 1), 0));
         if (g_trace) printf("> launch boundary s=%d m=%d\n", s, m);
         work<<<G / 8 + 1, 256, 0, st[s]>>>(a);
-        if (capture && step && coef) {
+        if (capture && step && coef && !(MODE & 32)) {
           hipStreamCaptureStatus cst;
           unsigned long long cid = 0;
           hipGraph_t cg = nullptr;
@@ -135,7 +139,8 @@ int main(int argc, char** argv) {
     }
     for (int s = 0; s < S; ++s) {
       work<<<1, 256, 0, st[s]>>>(a);
-      CK(hipMemcpyAsync(host + 64 * s, dbuf + 64 * s, 64, hipMemcpyDeviceToHost, st[s]));
+      if (!(MODE & 16))
+        CK(hipMemcpyAsync(host + 64 * s, dbuf + 64 * s, 64, hipMemcpyDeviceToHost, st[s]));
     }
   };
 
