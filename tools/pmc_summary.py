@@ -26,6 +26,14 @@ EW = ["dot", "update_mrr_first", "update_mrr", "update_cg", "update_cg_p", "upda
 
 
 def short(name):
+    # the box fused walks (kr_pair.hip), named as System::spmv_pair / spmv_step2 book them
+    m = re.search(r"spmv_stencil2b_kernel<(\d+), (\w+), \d+>", name)
+    if m:
+        base = "spmv2x2_gram_" + ("kcg" if int(m.group(1)) == 8 else "mrr")
+        return base + ("_last" if m.group(2) == "true" else "")
+    m = re.search(r"spmv_step2b_kernel<(\w+), \d+>", name)
+    if m:
+        return "spmv_step3_mrr_stencil" if m.group(1) == "true" else "spmv_step2_mrr_stencil"
     m = re.search(r"spmv_kernel2_po<(\w+), (\d+), (\w+)", name)
     if m:  # the plain-CSR row walk's products-only dual (engine name ..._last)
         return EPI[int(m.group(2))] + "_last" + ("" if m.group(1) == "int" else "_rp64")
