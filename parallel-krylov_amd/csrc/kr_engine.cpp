@@ -717,13 +717,15 @@ void System::spmv_step2(int r_in, int r_out, int y_in, int y_out, int z, int xs,
   a.st_box = 1;
   for (int k = 0; k < 8; ++k) a.st_v[k] = s.st_v[k];
   a.stop = dev_stop ? s.st + ST_STOP : nullptr;
-  // walk segments: 16 per plane column at 512 planes (32-plane walks), fewer
-  // on thinner boxes (>= 8 planes per walk); KR_STEP2_Z overrides
+  // walk segments: 8 per plane column at 512 planes (64-plane walks), fewer
+  // on thinner boxes (>= 8 planes per walk); KR_STEP2_Z overrides. Measured
+  // on C4 (one box, twice each, profiles/r06c): 8 / 16 / 32 segments give the
+  // triple 1.617 / 1.65-1.79 / 1.68 ms and 826-831 / 807-821 / 805-809 it/s
   const int64_t planes = s.n / ((int64_t)s.st_P * kStencilBlock);
   int zw = KR_ENV("KR_STEP2_Z", 0);
   if (zw <= 0) {
     zw = 1;
-    while (zw < 16 && planes / (2 * zw) >= 8) zw *= 2;
+    while (zw < 8 && planes / (2 * zw) >= 8) zw *= 2;
   }
   zw = (int)std::min<int64_t>(zw, planes);
   launch_spmv_step2b(a, (s.st_P / 2) * zw, virt ? 1 : 0, xm, s.stream);

@@ -121,6 +121,9 @@ __device__ __forceinline__ void st2b_walk(const SpmvArgs& a, St2bLds<XS>& L, int
                                           int q, int zs, int Zw) {
   using Lds = St2bLds<XS>;
   constexpr int SL = Lds::SL;
+  // XS = 1: whole lines, every halo row an x face -- no halo loads, stores or
+  // halo-row sums (their LDS slots are zeroed once, spmv_stencil2b_kernel)
+  constexpr bool XH = XS > 1;
   constexpr int G = SL / 2;      // lanes per group
   constexpr int NWG = G / 64;    // waves per group
   constexpr int NP = 7;
@@ -169,7 +172,7 @@ __device__ __forceinline__ void st2b_walk(const SpmvArgs& a, St2bLds<XS>& L, int
       const uint32_t m = zm & lok[jj], mh = m & hm;
       const uint32_t u = lbase[jj] + zo;
       st[jj] = st_bld2(rx, ((u & m) | (kOut & ~m)) + lb);
-      sth[jj] = st_bld2(rx, ((u + hb) & mh) | (kOut & ~mh));
+      if constexpr (XH) sth[jj] = st_bld2(rx, ((u + hb) & mh) | (kOut & ~mh));
     }
   };
   // level-1 lines outside [0, P) are 0 (the -n / +n of the y faces)
@@ -259,7 +262,8 @@ __device__ __forceinline__ void st2b_walk(const SpmvArgs& a, St2bLds<XS>& L, int
     for (int jj = 0; jj < 3; ++jj) {
       if constexpr (!(KR_ST2B_AB & 16)) lds2_st(&L.x0[C][3 * H + jj][tl], st[jj]);
       else if (st[jj].x == 1234.5) lds2_st(&L.x0[C][3 * H + jj][tl], st[jj]);
-      if (wig == 0 && lane < 2) lds2_st(&L.x0[C][3 * H + jj][(lane & 1) ? SL + 2 : 0], sth[jj]);
+      if constexpr (XH)
+        if (wig == 0 && lane < 2) lds2_st(&L.x0[C][3 * H + jj][(lane & 1) ? SL + 2 : 0], sth[jj]);
     }
     if constexpr (C == 1 && !(KR_ST2B_AB & 64)) lds2_st(&L.xa[s & 1][H][2 * t], l0p[IO]);
     issue(s + 1);
@@ -286,7 +290,7 @@ __device__ __forceinline__ void st2b_walk(const SpmvArgs& a, St2bLds<XS>& L, int
     for (int i = 0; i < 2; ++i)
       if constexpr (!(KR_ST2B_AB & 32)) lds2_st(&L.x1[C][2 * H + i][tl], l1[i]);
       else if (l1[i].x == 1234.5) lds2_st(&L.x1[C][2 * H + i][tl], l1[i]);
-    if (hlane) {
+    if (XH && hlane) {
       const double* ln = &L.x0[C][J2][hr + 2];
       const double own = ln[0];
       const double c = hp1 + v[6] * own;
@@ -343,7 +347,7 @@ __device__ __forceinline__ void st2b_walk(const SpmvArgs& a, St2bLds<XS>& L, int
   for (int i = 0; i < 2; ++i) l0p[i] = st[1 - H + i];
   // the own line's halo rows of plane z0-2 (lane 0: row -1, lane 1: row SL):
   // from the halo chunk (rows -2, -1 / SL, SL+1)
-  hl0p = (lane & 1) ? sth[1 - H + IO].x : sth[1 - H + IO].y;
+  if constexpr (XH) hl0p = (lane & 1) ? sth[1 - H + IO].x : sth[1 - H + IO].y;
   issue(z0 - 1);
   for (int s = z0 - 1; s <= z1 + 1; ++s) step(s);
   __syncthreads();
@@ -360,6 +364,16 @@ void spmv_stencil2b_kernel(SpmvArgs a) {
   if (a.stop && *a.stop != 0.0) return;
   extern __shared__ __attribute__((aligned(16))) double s2b_dyn[];
   St2bLds<XS>& L = *reinterpret_cast<St2bLds<XS>*>(s2b_dyn);
+  if constexpr (XS == 1) {
+    // the x-face pads (rows -2, -1, 512, 513) of every line, read as 0.0;
+    // visible after the first step's barrier, never written again
+    constexpr int LL = St2bLds<XS>::LL;
+    if (threadIdx.x < 80) {
+      const int i = threadIdx.x >> 2, e = threadIdx.x & 3;  // line i of 20, pad e
+      double* line = i < 12 ? &L.x0[i / 6][i % 6][0] : &L.x1[(i - 12) / 4][(i - 12) % 4][0];
+      line[e < 2 ? e : LL - 4 + e] = 0.0;
+    }
+  }
   // XCD q = B & 7 walks the position pairs of [q P/8, (q+1) P/8): the x
   // segments of a tile, then the tiles, then the plane segments
   const int P = a.st_P, PP = P >> 3;
