@@ -636,9 +636,11 @@ void System::spmv_pair(int in1, int in2, int out1, int out2, int slot0, SpmvEpi 
     const int g1 = s.spmv_grid, g2 = po ? s.spmv_grid_po : s.spmv_grid;
     const int z1 = g1 / s.st_P, z2 = g2 / s.st_P;
     const char* ze = getenv(mode == 3 ? "KR_ST2B_Z" : "KR_ST2T_Z");
-    // the box pair: 64-plane walks at 512^3 (3 of every 64 planes re-walked;
-    // KR_ST2B_Z 4 / 8 / 16 / 32: 1.385 / 1.395 / 1.444 / 1.542 ms, profiles/r06a)
-    const int zcap = ze && atoi(ze) > 0 ? atoi(ze) : (mode == 3 ? 8 : 16);
+    // the box pair: 128-plane walks at 512^3 (KR_ST2B_Z 4 / 8 / 16 / 32: the
+    // storing pair 1.385 / 1.395 / 1.444 / 1.542 ms in the first build; same
+    // box, twice each, profiles/r06d: 4 / 8 / 16 give the products-only pair
+    // 1.013-1.019 / 1.046-1.054 / 1.102-1.107 ms, the storing pair equal)
+    const int zcap = ze && atoi(ze) > 0 ? atoi(ze) : (mode == 3 ? 4 : 16);
     const int zg = std::gcd(z1, z2);
     int zw = 1;
     for (int d = 1; d <= zg; ++d)
@@ -717,15 +719,16 @@ void System::spmv_step2(int r_in, int r_out, int y_in, int y_out, int z, int xs,
   a.st_box = 1;
   for (int k = 0; k < 8; ++k) a.st_v[k] = s.st_v[k];
   a.stop = dev_stop ? s.st + ST_STOP : nullptr;
-  // walk segments: 8 per plane column at 512 planes (64-plane walks), fewer
+  // walk segments: 4 per plane column at 512 planes (128-plane walks), fewer
   // on thinner boxes (>= 8 planes per walk); KR_STEP2_Z overrides. Measured
-  // on C4 (one box, twice each, profiles/r06c): 8 / 16 / 32 segments give the
-  // triple 1.617 / 1.65-1.79 / 1.68 ms and 826-831 / 807-821 / 805-809 it/s
+  // on C4 (same box, twice each, profiles/r06c, r06d): 4 / 8 / 16 / 32
+  // segments give the step pair 1.36-1.38 / 1.37-1.41 / 1.39-1.42 / 1.43-1.45
+  // ms (the triple varies 1.57-1.79 ms from run to run at any count)
   const int64_t planes = s.n / ((int64_t)s.st_P * kStencilBlock);
   int zw = KR_ENV("KR_STEP2_Z", 0);
   if (zw <= 0) {
     zw = 1;
-    while (zw < 8 && planes / (2 * zw) >= 8) zw *= 2;
+    while (zw < 4 && planes / (2 * zw) >= 8) zw *= 2;
   }
   zw = (int)std::min<int64_t>(zw, planes);
   launch_spmv_step2b(a, (s.st_P / 2) * zw, virt ? 1 : 0, xm, s.stream);

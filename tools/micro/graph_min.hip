@@ -9,6 +9,15 @@
 //            forked stream waits on ANOTHER forked stream); join s1, s2.
 // pattern 1: as 0, but s2 waits on an event recorded on the ORIGIN s0.
 // pattern 2: as 0 with s1 waiting on s2's event too (a two-way edge).
+// Round 6: the smallest crashing graph_cost variant (2 shards, ONE split SpMV,
+// only the comm-stream cross waits: `graph_cost 2 1 200 64 56`), restated:
+// streams st0 (origin), st1 (compute), cs0, cs1 (comm), all forked from st0;
+// ev_in(s) recorded on st(s); cs(s) waits ev_in(s) and the neighbour's
+// ev_in; gather kernel on cs(s), ev_out(s) recorded there; interior kernel
+// on st(s); st(s) waits ev_out(s); boundary kernel; join everything to st0.
+// pattern 3: both cross waits (cs0 on ev_in(1), cs1 on ev_in(0));
+// pattern 4: only cs1 waits on ev_in(0) (the ORIGIN's event);
+// pattern 5: only cs0 waits on ev_in(1) (a forked stream's event).
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -41,6 +50,42 @@ int main(int argc, char** argv) {
   int* d = nullptr;
   CK(hipMalloc(&d, 64));
   hipGraph_t g;
+  if (pat >= 3) {
+    hipStream_t st[2] = {s0, s1}, cs[2] = {s2, nullptr};
+    CK(hipStreamCreateWithFlags(&cs[1], hipStreamNonBlocking));
+    hipEvent_t ein[2], eout[2], jn[3];
+    for (hipEvent_t* e : {&ein[0], &ein[1], &eout[0], &eout[1], &jn[0], &jn[1], &jn[2]})
+      CK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    CK(hipStreamBeginCapture(s0, hipStreamCaptureModeRelaxed));
+    CK(hipEventRecord(fork, s0));
+    CK(hipStreamWaitEvent(st[1], fork, 0));
+    CK(hipStreamWaitEvent(cs[0], fork, 0));
+    CK(hipStreamWaitEvent(cs[1], fork, 0));
+    for (int q = 0; q < 2; ++q) CK(hipEventRecord(ein[q], st[q]));
+    for (int q = 0; q < 2; ++q) {
+      CK(hipStreamWaitEvent(cs[q], ein[q], 0));
+      const bool cross = pat == 3 || (pat == 4 && q == 1) || (pat == 5 && q == 0);
+      if (cross) CK(hipStreamWaitEvent(cs[q], ein[1 - q], 0));
+      k<<<1, 64, 0, cs[q]>>>(d, 10 + q);
+      CK(hipEventRecord(eout[q], cs[q]));
+      k<<<1, 64, 0, st[q]>>>(d, 20 + q);
+    }
+    for (int q = 0; q < 2; ++q) {
+      CK(hipStreamWaitEvent(st[q], eout[q], 0));
+      k<<<1, 64, 0, st[q]>>>(d, 30 + q);
+    }
+    CK(hipEventRecord(jn[0], st[1]));
+    CK(hipEventRecord(jn[1], cs[0]));
+    CK(hipEventRecord(jn[2], cs[1]));
+    for (int q = 0; q < 3; ++q) CK(hipStreamWaitEvent(s0, jn[q], 0));
+    CK(hipStreamEndCapture(s0, &g));
+    hipGraphExec_t x;
+    CK(hipGraphInstantiate(&x, g, nullptr, nullptr, 0));
+    CK(hipGraphLaunch(x, s0));
+    CK(hipStreamSynchronize(s0));
+    printf("pattern %d ok\n", pat);
+    return 0;
+  }
   CK(hipStreamBeginCapture(s0, hipStreamCaptureModeRelaxed));
   CK(hipEventRecord(fork, s0));
   CK(hipStreamWaitEvent(s1, fork, 0));
