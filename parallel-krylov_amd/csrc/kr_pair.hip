@@ -349,6 +349,10 @@ __device__ __forceinline__ void st2b_walk(const SpmvArgs& a, St2bLds<XS>& L, int
   // from the halo chunk (rows -2, -1 / SL, SL+1)
   if constexpr (XH) hl0p = (lane & 1) ? sth[1 - H + IO].x : sth[1 - H + IO].y;
   issue(z0 - 1);
+  // one step per trip: two per trip (the carried state alternating registers
+  // instead of being copied) measured slower for the products-only pair,
+  // 1.015-1.030 -> 1.056-1.064 ms (same box, profiles/r06f), and the storing
+  // walks spill at 128 VGPRs
   for (int s = z0 - 1; s <= z1 + 1; ++s) step(s);
   __syncthreads();
   level2_products(z1 - 1);  // the last plane's, written by the last step

@@ -18,6 +18,9 @@
 // pattern 3: both cross waits (cs0 on ev_in(1), cs1 on ev_in(0));
 // pattern 4: only cs1 waits on ev_in(0) (the ORIGIN's event);
 // pattern 5: only cs0 waits on ev_in(1) (a forked stream's event).
+// pattern 6: as 4 with a kernel on st0 before the ev_in records (the origin's
+//            event then carries a captured node);
+// pattern 7: as 4 with cs1 waiting on ev_in(0) BEFORE its own ev_in(1).
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -61,11 +64,14 @@ int main(int argc, char** argv) {
     CK(hipStreamWaitEvent(st[1], fork, 0));
     CK(hipStreamWaitEvent(cs[0], fork, 0));
     CK(hipStreamWaitEvent(cs[1], fork, 0));
+    if (pat == 6) k<<<1, 64, 0, st[0]>>>(d, 9);
     for (int q = 0; q < 2; ++q) CK(hipEventRecord(ein[q], st[q]));
     for (int q = 0; q < 2; ++q) {
+      const bool cross = pat == 3 || ((pat == 4 || pat == 6 || pat == 7) && q == 1) ||
+                         (pat == 5 && q == 0);
+      if (cross && pat == 7) CK(hipStreamWaitEvent(cs[q], ein[1 - q], 0));
       CK(hipStreamWaitEvent(cs[q], ein[q], 0));
-      const bool cross = pat == 3 || (pat == 4 && q == 1) || (pat == 5 && q == 0);
-      if (cross) CK(hipStreamWaitEvent(cs[q], ein[1 - q], 0));
+      if (cross && pat != 7) CK(hipStreamWaitEvent(cs[q], ein[1 - q], 0));
       k<<<1, 64, 0, cs[q]>>>(d, 10 + q);
       CK(hipEventRecord(eout[q], cs[q]));
       k<<<1, 64, 0, st[q]>>>(d, 20 + q);
