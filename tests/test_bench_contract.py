@@ -67,13 +67,14 @@ def test_pmc_traffic_from_committed_profile():
     with open(os.path.join(REPO, "profiles", "pmc", "C4.json")) as f:
         prof = json.load(f)
     assert prof["_meta"]["config"] == "C4"
-    t = bench.pmc_traffic("C4", "spmv2_gram_mrr")
-    assert t == prof["kernels"]["spmv2_gram_mrr"]["traffic_bytes"] and t > 1e9
+    # the headline's box walks (the step triple is C4's roofline kernel)
+    kern = "spmv_step3_mrr_stencil"
+    t = bench.pmc_traffic("C4", kern)
+    assert t == prof["kernels"][kern]["traffic_bytes"] and t > 1e9
     assert bench.pmc_traffic("C4", "no_such_kernel") is None
     # another config never borrows C4's bytes
-    assert bench.pmc_traffic("C1", "spmv2_gram_mrr") is None
-    assert bench.pmc_traffic("C5", "spmv2_gram_mrr") is None or \
-        bench.pmc_traffic("C5", "spmv2_gram_mrr") != t
+    assert bench.pmc_traffic("C1", kern) is None
+    assert bench.pmc_traffic("C5", kern) is None or bench.pmc_traffic("C5", kern) != t
 
 
 def test_history_parity_contract():
