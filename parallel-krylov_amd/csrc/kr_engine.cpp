@@ -725,16 +725,92 @@ void System::spmv_step2(int r_in, int r_out, int y_in, int y_out, int z, int xs,
   // segments give the step pair 1.36-1.38 / 1.37-1.41 / 1.39-1.42 / 1.43-1.45
   // ms (the triple varies 1.57-1.79 ms from run to run at any count)
   const int64_t planes = s.n / ((int64_t)s.st_P * kStencilBlock);
+  launch_spmv_step2b(a, (s.st_P / 2) * step2_segments(planes, 0), virt ? 1 : 0, xm, s.stream);
+  // algorithmic bytes in CSR terms: A once, r, y, (Ar1,) z, x in and r, y,
+  // z, x out (x neither way when no step of the pair touches it)
+  const double vecs = (virt ? 9.0 : 8.0) - (virt || xm != 0 ? 0.0 : 2.0);
+  const double bytes = 12.0 * s.nnz + 4.0 * (s.n + 1) + 8.0 * vecs * s.n;
+  prof_end(s, nm, t0, bytes);
+}
+
+bool System::step2h_ok() const {
+  if (!step2_ok() || KR_ENV("KR_STEP2H", 1) == 0) return false;
+  const Shard& s = shards[0];
+  if (s.spmv_grid % s.st_P != 0) return false;
+  // walk segments (spmv_step2h) dividing the head grid's plane segments
+  const int64_t planes = s.n / ((int64_t)s.st_P * kStencilBlock);
+  const int zh = s.spmv_grid / s.st_P;
+  return zh >= 1 && planes >= zh && step2_segments(planes, zh) > 0;
+}
+
+// Walk segments of the box step walks: KR_STEP2_Z, else 4 per plane column at
+// 512 planes (128-plane walks), fewer on thinner boxes (>= 8 planes per
+// walk). With zh > 0 (the step pair + head) the largest count <= that which
+// divides zh (0: none).
+int System::step2_segments(int64_t planes, int zh) const {
   int zw = KR_ENV("KR_STEP2_Z", 0);
   if (zw <= 0) {
     zw = 1;
     while (zw < 4 && planes / (2 * zw) >= 8) zw *= 2;
   }
   zw = (int)std::min<int64_t>(zw, planes);
-  launch_spmv_step2b(a, (s.st_P / 2) * zw, virt ? 1 : 0, xm, s.stream);
-  // algorithmic bytes in CSR terms: A once, r, y, (Ar1,) z, x in and r, y,
-  // z, x out (x neither way when no step of the pair touches it)
-  const double vecs = (virt ? 9.0 : 8.0) - (virt || xm != 0 ? 0.0 : 2.0);
+  if (zh > 0) {
+    while (zw > 1 && zh % zw != 0) --zw;
+    if (zh % zw != 0) return 0;
+  }
+  return zw;
+}
+
+void System::spmv_step2h(int r_in, int r_out, int y_in, int y_out, int z, int xs, int xd, int xm,
+                         const double* c, int ar1) {
+  KR_REQUIRE(step2h_ok(), "box step pair + head: shard not eligible");
+  KR_REQUIRE(r_out != r_in && y_out != y_in && y_out != r_in && r_out != y_in && ar1 != r_in &&
+                 ar1 != r_out && ar1 != y_in && ar1 != y_out,
+             "box step pair + head: outputs alias their gathered inputs");
+  Shard& s = shards[0];
+  KR_HIP_CHECK(hipSetDevice(s.dev));
+  const char* nm = "spmv_step2h_mrr_stencil";
+  hipEvent_t t0 = nullptr;
+  prof_begin(s, nm, t0);
+  SpmvArgs a;
+  a.n = s.n;
+  a.x1 = s.vec[r_in];
+  a.x2 = s.vec[y_in];
+  a.xoff = s.pad;
+  a.xlen = s.ld;
+  a.y1 = s.own(r_out);
+  a.y2 = s.own(ar1);
+  a.u1 = s.own(y_out);
+  a.u2 = s.own(z);
+  a.us = s.own(xs);
+  a.ud = s.own(xd);
+  a.c0 = c[0];
+  a.c1 = c[1];
+  a.c2 = c[2];
+  a.c3 = c[3];
+  a.st_P = s.st_P;
+  a.st_box = 1;
+  for (int k = 0; k < 8; ++k) a.st_v[k] = s.st_v[k];
+  a.stop = dev_stop ? s.st + ST_STOP : nullptr;
+  a.partials = s.partials;  // the head's slots 0..4
+  a.grid = s.pstride;
+  if (!s.pairq) {
+    const size_t bytes = sizeof(double) * 14 * 4 * (size_t)s.pstride;
+    KR_HIP_CHECK(hipMalloc(&s.pairq, bytes));
+    s.owned.push_back(s.pairq);
+    fresh_fill(s.pairq, bytes, s.stream);
+  }
+  a.partq = s.pairq;
+  const int64_t planes = s.n / ((int64_t)s.st_P * kStencilBlock);
+  const int zh = s.spmv_grid / s.st_P;
+  a.st2_z1 = zh;
+  const int zw = step2_segments(planes, zh);
+  launch_spmv_step2h(a, (s.st_P / 2) * zw, xm, s.spmv_grid, s.stream);
+  for (int p = 0; p < 5; ++p) s.slot_n[p] = s.spmv_grid;
+  // algorithmic bytes in CSR terms, like the other walks' (A once: bench.py
+  // subtracts the stored format's saving once per launch): r, y, z, x in (x
+  // only when a step touches it) and r, y, z, x, Ar1 out
+  const double vecs = 9.0 - (xm != 0 ? 0.0 : 2.0);
   const double bytes = 12.0 * s.nnz + 4.0 * (s.n + 1) + 8.0 * vecs * s.n;
   prof_end(s, nm, t0, bytes);
 }
@@ -3288,8 +3364,23 @@ class KskipMrrSession : public Base {
     } else {
       ew_step(0);
     }
+    bool headed = false;  // the head ran inside the last step walk
     for (int j = j1; j <= k; ++j) {
       const int ka = step_kind(j), kb = j + 1 <= k ? step_kind(j + 1) : -1;
+      if (step2 && kb >= 0 && ka != 2 && j + 1 == k && sys->step2h_ok()) {
+        // the last pair of steps and the next head in one walk (the head's
+        // Ar1 = A r and products at slots 0..4, as head() writes them)
+        const int xm = (ka == 1 ? 3 : 0) | (kb == 1 ? 2 : 0) | (kb >= 1 ? 4 : 0);
+        const double c[4] = {eta[j], zeta[j], eta[j + 1], zeta[j + 1]};
+        sys->spmv_step2h(r0, r_alt, y0, y_alt, Z, xsrc, cur, xm, c, AR(1));
+        if (xm != 0) xsrc = cur;
+        if (kb == 0) xpend = true;  // xdefer: left to the next outer iteration
+        std::swap(r0, r_alt);
+        std::swap(y0, y_alt);
+        headed = true;
+        ++j;
+        continue;
+      }
       if (step2 && kb >= 0 && ka != 2) {
         // steps j and j+1 in one walk on a box shard: r and y into their
         // other buffers, z and x as the two step kernels write them
@@ -3328,7 +3419,7 @@ class KskipMrrSession : public Base {
         ew_step(j);
       }
     }
-    head();
+    if (!headed) head();
     i += k + 1;
     index += 1;
     set_nosl(index, i);

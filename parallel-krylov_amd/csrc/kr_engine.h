@@ -320,6 +320,16 @@ struct System {
   // triple (steps 0-2, Ar1_0 = ar1, c[4..5] step 2's, xpend)
   void spmv_step2(int r_in, int r_out, int y_in, int y_out, int z, int xs, int xd, int xm,
                   const double* c, int ar1 = -1, int xpend = 0);
+  // The box step pair + head (kr_pair.hip, launch_spmv_step2h): the last two
+  // steps of an outer iteration (spmv_step2's operands; xm 3, 7 or 6) and
+  // the next head SpMV (EPI_HEAD_MRR: Ar1 into vector ar1 from the new r,
+  // with the new y as e; products at slots 0..4) in one walk. KR_STEP2H=0
+  // disables.
+  bool step2h_ok() const;
+  void spmv_step2h(int r_in, int r_out, int y_in, int y_out, int z, int xs, int xd, int xm,
+                   const double* c, int ar1);
+  // walk segments of the box step walks (zh > 0: dividing zh; 0: none)
+  int step2_segments(int64_t planes, int zh) const;
   // Shard::st_box from the code patterns (host copies h: the codes of every
   // row block, pid / first: the pattern ids and a block holding each)
   void build_box(Shard& s, const std::vector<uint8_t>& h, const std::vector<uint32_t>& pid,

@@ -338,6 +338,13 @@ void launch_spmv_stencil2b(SpmvEpi epi, const SpmvArgs& a, int nblocks, int xs, 
 // 2 (FIRST2 + the next): x3 = Ar1_0, c4 c5 step 2's, xpend, xm 0 or 4 (x minus
 // z_3). nblocks = P/2 x walk segments. Bitwise the step launches.
 void launch_spmv_step2b(const SpmvArgs& a, int nblocks, int virt, int xm, hipStream_t s);
+// The box step pair + head (kr_pair.hip): the last two k-skip MrR steps of
+// an outer iteration (launch_spmv_step2b's operands, xm 3, 7 or 6) and the
+// head SpMV of the next (y2 = Ar1 = A r_c; EPI_HEAD_MRR products of the head
+// grid -- nhead = P x st2_z1 workgroups -- through partq into partials) in
+// one walk; nblocks = P/2 x walk segments. Bitwise the step-pair launch
+// followed by the head launch.
+void launch_spmv_step2h(const SpmvArgs& a, int nblocks, int xm, int nhead, hipStream_t s);
 // x segments per line of the box pair (1, 2 or 4; kr_pair.hip)
 int st2b_xsegments(bool products_only);
 

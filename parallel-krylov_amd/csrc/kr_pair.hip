@@ -706,6 +706,294 @@ void sp2b_launch_t(const SpmvArgs& a, int nblocks, hipStream_t s) {
   KR_HIP_CHECK(hipGetLastError());
 }
 
+// ---------------------------------------------------------------------------
+// The box step pair + head: the LAST two k-skip MrR steps of an outer
+// iteration (k-1, k) and the next outer iteration's head SpMV (EPI_HEAD_MRR,
+// v3/gpu/kskipmrr.py:40-44: Ar1 = A r, products <r,r> <r,Ar1> <Ar1,Ar1>
+// <y,Ar1> <y,y>) in ONE walk. Levels 1 and 2 are spmv_step2b_kernel's
+// statements (r_b, y_b; r_c, y_c, z_c, x); level 3 is the head at the two
+// output lines, its Ar1 summed in stored order and its products accumulated
+// per (x quarter, head-grid segment) exactly as the head launch's waves
+// accumulate them (flushed at its segment boundaries, combined by
+// sp3_combine_kernel in block_reduce_store's order). So the results are
+// bitwise the step-pair launch followed by the head launch, and the HBM
+// traffic is 9 vectors (r, y, z, x in; r, y, z, x, Ar1 out) instead of 8 + 3.
+//
+// Lines (positions p0 - 3 + j): level 0 (r_a) j = 0..7, level 1 (r_b) j =
+// 1..6, level 2 (r_c) j = 2..5, level 3 (Ar1) j = 3, 4. Four groups of 256
+// lanes (rows 2t, 2t+1 of whole 512-row lines): group G loads level-0 lines
+// 2G, 2G+1; level 1 of lines {1,2}, {3}, {4}, {5,6}; level 2 of line G + 2;
+// groups 1 and 2 also level 3 and the stores. Three barriers per plane step.
+// ---------------------------------------------------------------------------
+struct Sp3Lds {
+  double x0[8][kSBlock + 4];  // level 0 of plane s: [line][row + 2], zero pads
+  double x1[6][kSBlock + 4];  // level 1 of plane s-1, lines 1..6
+  double x2[4][kSBlock + 4];  // level 2 of plane s-2, lines 2..5
+};
+
+template <int G, int XM>
+__device__ __forceinline__ void sp3_walk(const SpmvArgs& a, Sp3Lds& L, int t, int p0, int q, int zs,
+                                         int Zw) {
+  constexpr bool OUT = G == 1 || G == 2;              // levels 2's stores, level 3
+  constexpr int N1 = (G == 0 || G == 3) ? 2 : 1;     // level-1 lines
+  constexpr int J1 = G == 0 ? 1 : G == 3 ? 5 : G + 2;  // the first of them
+  constexpr int J2 = G + 2;                           // the level-2 (and level-3) line
+  constexpr int I2 = J2 - J1;                         // its index among the level-1 lines
+  constexpr int NP = 5;
+  const int lane = t & 63, quarter = t >> 6;
+  const int P = a.st_P, PP = P >> 3;
+  const int W = P * kSBlock;
+  const int planes = (int)(a.n / W);
+  const int z0 = (int)((int64_t)planes * zs / Zw), z1 = (int)((int64_t)planes * (zs + 1) / Zw);
+  double v[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) v[k] = a.st_v[k];
+  const double e1 = a.c0, f1 = a.c1, e2 = a.c2, f2 = a.c3;
+
+  const __amdgpu_buffer_rsrc_t rr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(a.x1), 0, (int)(a.xlen * 8), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ry =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(a.x2), 0, (int)(a.xlen * 8), 0x00020000);
+  const uint32_t lb = (uint32_t)t * 16u;
+  const uint32_t wbytes = (uint32_t)W * 8u;
+  constexpr uint32_t kOut = 0x80000000u;
+  auto line_base = [&](int j) { return (uint32_t)((a.xoff + (int64_t)(p0 - 3 + j) * kSBlock) * 8); };
+  auto line_ok = [&](int j) { return p0 - 3 + j >= 0 && p0 - 3 + j < P; };
+  uint32_t lbase[2], lok[2], ybase[N1], yok[N1];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    lbase[i] = line_base(2 * G + i);
+    lok[i] = -(uint32_t)line_ok(2 * G + i);
+  }
+  bool l1ok[N1];
+#pragma unroll
+  for (int i = 0; i < N1; ++i) {
+    ybase[i] = line_base(J1 + i);
+    yok[i] = -(uint32_t)line_ok(J1 + i);
+    l1ok[i] = line_ok(J1 + i);
+  }
+  const bool l2ok = line_ok(J2);
+  const int pown = p0 - 3 + J2;  // OUT: the output line's position
+  const int64_t orow = (int64_t)pown * kSBlock + 2 * t;
+
+  dbl2v st[2], sty[N1];
+  auto issue = [&](int z) {  // level 0 of plane z, y_a of plane z-1
+    const uint32_t zm = -(uint32_t)((unsigned)z < (unsigned)planes);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const uint32_t m = zm & lok[i];
+      st[i] = st_bld2(rr, (((lbase[i] + (uint32_t)z * wbytes) & m) | (kOut & ~m)) + lb);
+    }
+    const uint32_t ym = -(uint32_t)((unsigned)(z - 1) < (unsigned)planes);
+#pragma unroll
+    for (int i = 0; i < N1; ++i) {
+      const uint32_t m = ym & yok[i];
+      sty[i] = st_bld2(ry, (((ybase[i] + (uint32_t)(z - 1) * wbytes) & m) | (kOut & ~m)) + lb);
+    }
+  };
+
+  // ---- level-3 products (OUT): each wave's shuffle-reduced value to its x
+  // quarter of the head launch's workgroup (position, grid segment)
+  const int Zh = a.st2_z1;  // the head grid's plane segments
+  int seg = zs * (Zh / Zw);
+  int nb = (int)((int64_t)planes * (seg + 1) / Zh);
+  double acc[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) acc[k] = 0.0;
+  auto flush = [&]() {
+    const int64_t vwg = 8 * ((int64_t)seg * PP + (pown - q * PP)) + q;
+    double* const dst = a.partq + vwg * 4 + quarter;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      double r = acc[k];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) r += __shfl_down(r, off, 64);
+      if (lane == 0) dst[(int64_t)k * a.grid * 4] = r;
+      acc[k] = 0.0;
+    }
+  };
+
+  // ---- carried state (step s: level 0 of plane s arrives)
+  dbl2v l0p[N1], p1[N1];                          // level 0 of plane s-1, partial level 1 of s-1
+  dbl2v yb2 = dbl2v{0.0, 0.0};                    // y_b of plane s-2 (line J2)
+  dbl2v l1p = dbl2v{0.0, 0.0};                    // r_b of plane s-2 (line J2)
+  dbl2v p2 = dbl2v{0.0, 0.0};                     // partial level 2 of plane s-2
+  dbl2v ra2 = dbl2v{0.0, 0.0};                    // OUT: r_a of plane s-2 (line J2)
+  dbl2v l2p = dbl2v{0.0, 0.0};                    // OUT: r_c of plane s-3
+  dbl2v yc1 = dbl2v{0.0, 0.0};                    // OUT: y_c of plane s-3
+  dbl2v p3 = dbl2v{0.0, 0.0};                     // OUT: partial head sums of plane s-3
+#pragma unroll
+  for (int i = 0; i < N1; ++i) p1[i] = l0p[i] = dbl2v{0.0, 0.0};
+  const int tl = 2 + 2 * t;
+
+  auto step = [&](int s) {
+    // (1) level 0 of plane s to LDS; keep y_a (s-1), z_a and x (s-2); next loads
+#pragma unroll
+    for (int i = 0; i < 2; ++i) lds2_st(&L.x0[2 * G + i][tl], st[i]);
+    dbl2v ya[N1];
+#pragma unroll
+    for (int i = 0; i < N1; ++i) ya[i] = sty[i];
+    // OUT: z_a and x of plane s-2, loaded in this step (used after two
+    // barriers): one step ahead they held 8 more registers across the loop
+    dbl2v za = dbl2v{0.0, 0.0}, xa = dbl2v{0.0, 0.0};
+    if constexpr (OUT) {
+      const int zz = (unsigned)(s - 2) < (unsigned)planes ? s - 2 : 0;  // past a face: unused
+      za = *reinterpret_cast<const dbl2v*>(a.u2 + orow + (int64_t)zz * W);
+      if constexpr (XM != 0) xa = *reinterpret_cast<const dbl2v*>(a.us + orow + (int64_t)zz * W);
+    }
+    issue(s + 1);
+    __syncthreads();
+    // (2) level 1 at plane s-1: Ar1 completed by its +W term, y_b, r_b; plane
+    // s's sums started
+    const bool pok1 = (unsigned)(s - 1) < (unsigned)planes;
+    dbl2v yb[N1], rb[N1];
+    const dbl2v ra_now = l0p[I2];  // r_a of plane s-1 at line J2
+#pragma unroll
+    for (int i = 0; i < N1; ++i) {
+      const int j = J1 + i;
+      const double* line = &L.x0[j][tl];
+      const dbl2v own = lds2(line);
+      const dbl2v ar = dbl2v{p1[i].x + v[6] * own.x, p1[i].y + v[6] * own.y};
+      const double t1l = e1 * ya[i].x, t1h = e1 * ya[i].y;
+      const double t2l = f1 * ar.x, t2h = f1 * ar.y;
+      yb[i] = dbl2v{t1l + t2l, t1h + t2h};
+      rb[i] = dbl2v{l0p[i].x - yb[i].x, l0p[i].y - yb[i].y};
+      if (!(pok1 && l1ok[i])) rb[i] = dbl2v{0.0, 0.0};  // off the box: the absent operand
+      p1[i] = st2b_part(v, l0p[i], lds2(&L.x0[j - 1][tl]), line[-1], own, line[2],
+                        lds2(&L.x0[j + 1][tl]));
+      l0p[i] = own;
+      lds2_st(&L.x1[j - 1][tl], rb[i]);
+    }
+    __syncthreads();
+    // (3) level 2 at plane s-2 (Ar1' completed by r_b of plane s-1): y_c, r_c
+    // (and OUT: z_c, x, the stores); plane s-1's sums started
+    const bool pok2 = (unsigned)(s - 2) < (unsigned)planes;
+    const dbl2v rbo = rb[I2];
+    const dbl2v ar2 = dbl2v{p2.x + v[6] * rbo.x, p2.y + v[6] * rbo.y};
+    const double s1l = e2 * yb2.x, s1h = e2 * yb2.y;
+    const double s2l = f2 * ar2.x, s2h = f2 * ar2.y;
+    const dbl2v yc = dbl2v{s1l + s2l, s1h + s2h};
+    dbl2v rc = dbl2v{l1p.x - yc.x, l1p.y - yc.y};
+    if constexpr (OUT) {
+      if (s - 2 >= z0 && s - 2 < z1) {
+        // step j: z_b = eta_j z_a - zeta_j r_a; x2: x - z_a, then - z_b
+        const double t3l = e1 * za.x, t3h = e1 * za.y;
+        const double t4l = f1 * ra2.x, t4h = f1 * ra2.y;
+        const dbl2v zb = dbl2v{t3l - t4l, t3h - t4h};
+        dbl2v xn = xa;
+        if constexpr (XM & 1) xn = dbl2v{xn.x - za.x, xn.y - za.y};
+        if constexpr (XM & 2) xn = dbl2v{xn.x - zb.x, xn.y - zb.y};
+        const double s3l = e2 * zb.x, s3h = e2 * zb.y;
+        const double s4l = f2 * l1p.x, s4h = f2 * l1p.y;
+        const dbl2v zc = dbl2v{s3l - s4l, s3h - s4h};
+        if constexpr (XM & 4) xn = dbl2v{xn.x - zc.x, xn.y - zc.y};
+        const int64_t row = orow + (int64_t)(s - 2) * W;
+        __builtin_nontemporal_store(yc, reinterpret_cast<dbl2v*>(a.u1 + row));
+        __builtin_nontemporal_store(zc, reinterpret_cast<dbl2v*>(a.u2 + row));
+        if constexpr (XM != 0) __builtin_nontemporal_store(xn, reinterpret_cast<dbl2v*>(a.ud + row));
+        __builtin_nontemporal_store(rc, reinterpret_cast<dbl2v*>(a.y1 + row));
+      }
+      ra2 = ra_now;
+    }
+    if (!(pok2 && l2ok)) rc = dbl2v{0.0, 0.0};  // off the box: the head's absent operand
+    {
+      const double* lx = &L.x1[J2 - 1][tl];
+      p2 = st2b_part(v, l1p, lds2(&L.x1[J2 - 2][tl]), lx[-1], rbo, lx[2], lds2(&L.x1[J2][tl]));
+    }
+    l1p = rbo;
+    yb2 = yb[I2];
+    lds2_st(&L.x2[J2 - 2][tl], rc);
+    __syncthreads();
+    // (4) level 3 (the head) at plane s-3: Ar1 completed by r_c of plane s-2,
+    // products, the store; plane s-2's sums started
+    if constexpr (OUT) {
+      const dbl2v ar3 = dbl2v{p3.x + v[6] * rc.x, p3.y + v[6] * rc.y};
+      const int zh = s - 3;
+      if (zh >= z0 && zh < z1) {
+        if (zh >= nb) {
+          flush();
+          ++seg;
+          nb = (int)((int64_t)planes * (seg + 1) / Zh);
+        }
+        epi_products<EPI_HEAD_MRR>(l2p.x, 0.0, ar3.x, 0.0, yc1.x, acc);
+        epi_products<EPI_HEAD_MRR>(l2p.y, 0.0, ar3.y, 0.0, yc1.y, acc);
+        __builtin_nontemporal_store(ar3, reinterpret_cast<dbl2v*>(a.y2 + orow + (int64_t)zh * W));
+      }
+      const double* lx = &L.x2[J2 - 2][tl];
+      p3 = st2b_part(v, l2p, lds2(&L.x2[J2 - 3][tl]), lx[-1], rc, lx[2], lds2(&L.x2[J2 - 1][tl]));
+      l2p = rc;
+      yc1 = yc;
+    }
+  };
+
+  // prologue: level 0 of plane z0-3 (the -W operand of plane z0-2's level 1),
+  // plane z0-2 in flight; the LDS lines are overwritten by the first step
+  // before any read
+  issue(z0 - 3);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) lds2_st(&L.x0[2 * G + i][tl], st[i]);
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < N1; ++i) l0p[i] = lds2(&L.x0[J1 + i][tl]);
+  __syncthreads();
+  issue(z0 - 2);
+  for (int s = z0 - 2; s <= z1 + 2; ++s) step(s);
+  if constexpr (OUT) flush();
+}
+
+template <int XM>
+__global__ __launch_bounds__(4 * kBlock) __attribute__((amdgpu_waves_per_eu(4)))
+void spmv_step2h_kernel(SpmvArgs a) {
+  if (a.stop && *a.stop != 0.0) return;
+  extern __shared__ __attribute__((aligned(16))) double sp3_dyn[];
+  Sp3Lds& L = *reinterpret_cast<Sp3Lds*>(sp3_dyn);
+  // the x-face pads of every line (rows -2, -1, 512, 513), read as 0.0;
+  // visible after the prologue's barrier, never written again
+  if (threadIdx.x < 72) {
+    const int i = threadIdx.x >> 2, e = threadIdx.x & 3;  // line i of 18, pad e
+    double* line = i < 8 ? &L.x0[i][0] : i < 14 ? &L.x1[i - 8][0] : &L.x2[i - 14][0];
+    line[e < 2 ? e : kSBlock + e] = 0.0;
+  }
+  const int P = a.st_P, PP = P >> 3;
+  const int B = blockIdx.x, q = B & 7, w2 = B >> 3;
+  const int half = PP >> 1, Zw = gridDim.x / (P >> 1);
+  const int p0 = q * PP + 2 * (w2 % half);
+  const int zs = w2 / half;
+  const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kBlock));
+  const int t = (int)(threadIdx.x % kBlock);
+  switch (g) {
+    case 0: sp3_walk<0, XM>(a, L, t, p0, q, zs, Zw); break;
+    case 1: sp3_walk<1, XM>(a, L, t, p0, q, zs, Zw); break;
+    case 2: sp3_walk<2, XM>(a, L, t, p0, q, zs, Zw); break;
+    default: sp3_walk<3, XM>(a, L, t, p0, q, zs, Zw); break;
+  }
+}
+
+// partials[kk * grid + v] = ((q0 + q1) + q2) + q3 over the four x quarters of
+// the head launch's workgroup v (block_reduce_store's order), kk < nk, v < n.
+__global__ __launch_bounds__(kBlock) void sp3_combine_kernel(const double* __restrict__ partq,
+                                                              double* __restrict__ partials,
+                                                              int grid, int nk, int n) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int kk = (int)(i / grid), v = (int)(i % grid);
+  if (kk >= nk || v >= n) return;
+  const dbl2v lo = *reinterpret_cast<const dbl2v*>(partq + ((int64_t)kk * grid + v) * 4);
+  const dbl2v hi = *reinterpret_cast<const dbl2v*>(partq + ((int64_t)kk * grid + v) * 4 + 2);
+  double s = lo.x;
+  s = s + lo.y;
+  s = s + hi.x;
+  s = s + hi.y;
+  partials[(int64_t)kk * grid + v] = s;
+}
+
+template <int XM>
+void sp3_launch_t(const SpmvArgs& a, int nblocks, hipStream_t s) {
+  static std::atomic<uint64_t> opted{0};
+  opt_in_lds(opted, reinterpret_cast<const void*>(spmv_step2h_kernel<XM>), sizeof(Sp3Lds));
+  spmv_step2h_kernel<XM><<<nblocks, 4 * kBlock, sizeof(Sp3Lds), s>>>(a);
+  KR_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace
 
 // x segments per line (KR_ST2B_XS for the storing pair, KR_ST2B_XS_PO for
@@ -769,6 +1057,32 @@ void launch_spmv_step2b(const SpmvArgs& a, int nblocks, int virt, int xm, hipStr
     case 7: sp2b_launch_t<false, 7>(a, nblocks, s); return;  // (x2, x)
     default: throw Failure(KR_ERR_INVALID, "box step pair: unsupported step kinds");
   }
+}
+
+void launch_spmv_step2h(const SpmvArgs& a, int nblocks, int xm, int nhead, hipStream_t s) {
+  const int64_t W = (int64_t)a.st_P * kSBlock;
+  const int64_t planes = a.st_P > 0 ? a.n / W : 0;
+  const int tiles = a.st_P / 2;
+  const int zw = tiles > 0 ? nblocks / tiles : 0;
+  KR_REQUIRE(a.st_box && a.st_P % 16 == 0 && a.n == planes * W && planes >= 1 && a.rb_gap == 0 &&
+                 zw > 0 && nblocks == tiles * zw && zw <= planes && a.st2_z1 > 0 &&
+                 a.st2_z1 % zw == 0 && planes >= a.st2_z1 && nhead == a.st_P * a.st2_z1 &&
+                 nhead <= a.grid && a.partq && a.partials && a.x1 && a.x2 && a.u1 && a.u2 &&
+                 a.y1 && a.y2 && (xm == 0 || (a.us && a.ud)) && a.u1 != a.x2 + a.xoff &&
+                 a.y1 != a.x1 + a.xoff && (a.xlen + W) * 8 < (int64_t(1) << 31),
+             "box step pair + head: constant-coefficient 7-point box with n = 512, P % 16 == 0, "
+             "whole planes, walk segments dividing the head grid's; y and r written to other "
+             "buffers than they are read from");
+  switch (xm) {
+    case 3: sp3_launch_t<3>(a, nblocks, s); break;  // (x2, nox)
+    case 7: sp3_launch_t<7>(a, nblocks, s); break;  // (x2, x)
+    case 6: sp3_launch_t<6>(a, nblocks, s); break;  // (nox, x2)
+    default: throw Failure(KR_ERR_INVALID, "box step pair + head: unsupported step kinds");
+  }
+  const int64_t total = (int64_t)5 * a.grid;
+  sp3_combine_kernel<<<(int)((total + kBlock - 1) / kBlock), kBlock, 0, s>>>(a.partq, a.partials,
+                                                                             a.grid, 5, nhead);
+  KR_HIP_CHECK(hipGetLastError());
 }
 
 }  // namespace kr

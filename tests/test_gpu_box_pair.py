@@ -183,7 +183,10 @@ STEP2_CASES = [("kskipmrr", "box512x16x12", 4, {}), ("kskipmrr", "box512x16x12",
                ("kskipmrr", "box512x16x12", 4, {"KR_FUSE_FIRST": "0"}),
                ("kskipmrr", "box512x16x12", 5, {"KR_FUSE_FIRST": "0"}),
                ("adaptivekskipmrr", "box512x16x12", 6, {"KR_FUSE_FIRST": "0"}),
-               ("kskipmrr", "box512x16x12", 4, {"KR_ST2": "0"})]
+               ("kskipmrr", "box512x16x12", 4, {"KR_ST2": "0"}),
+               ("kskipmrr", "box512x16x12", 4, {"KR_STEP2H": "0"}),
+               ("kskipmrr", "box512x16x64", 6, {"KR_STENCIL_Z": "16"}),
+               ("adaptivekskipmrr", "box512x16x64", 4, {"KR_STENCIL_Z": "8"})]
 
 
 @pytest.mark.gpu
@@ -215,12 +218,55 @@ def test_box_step_pair_bitwise_equal_steps(monkeypatch, method, name, k, env):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("k,triples,pairs", [(4, 1, 1), (5, 1, 1), (2, 1, 0), (3, 1, 0),
-                                             (6, 1, 2), (1, 0, 0)])
-def test_box_step_pair_is_used(monkeypatch, k, triples, pairs):
+@pytest.mark.parametrize("k,triples,pairs,fused", [(4, 1, 0, 1), (5, 1, 1, 0), (2, 1, 0, 0),
+                                                   (3, 1, 0, 0), (6, 1, 1, 1), (1, 0, 0, 0)])
+def test_box_step_pair_is_used(monkeypatch, k, triples, pairs, fused):
     """k-skip MrR on a box shard: per outer iteration one step-triple launch
-    (steps 0-2) and one step-pair launch per later pair of steps."""
+    (steps 0-2), one step-pair launch per later pair of steps, and the last
+    pair of steps (steps k-1, k) with the next head SpMV in one walk
+    (spmv_step2h) -- then no separate head launch."""
     monkeypatch.delenv("KR_STEP2", raising=False)
     st = _launches(MATRICES["box512x16x12"](), "kskipmrr", k, "3", monkeypatch)
     assert st.get("spmv_step3_mrr_stencil", 0) == 4 * triples, st
     assert st.get("spmv_step2_mrr_stencil", 0) == 4 * pairs, st
+    assert st.get("spmv_step2h_mrr_stencil", 0) == 4 * fused, st
+    # (plus the solve's first head, before the first outer iteration)
+    assert st.get("spmv_head_mrr", 0) == 1 + 4 * (1 - fused), st
+
+
+# the step pair + head against the step pair and the head launch, bitwise,
+# over head grids whose segments flush inside one walk (KR_STENCIL_Z), walk
+# segment counts (KR_STEP2_Z), the x kinds (xdefer, adaptive)
+STEP2H_CASES = [("kskipmrr", "box512x16x12", 4, {}), ("kskipmrr", "box512x32x10", 6, {}),
+                ("kskipmrr", "box512x16x64", 4, {"KR_STENCIL_Z": "16"}),
+                ("kskipmrr", "box512x16x64", 4, {"KR_STENCIL_Z": "8", "KR_STEP2_Z": "2"}),
+                ("kskipmrr", "box512x16x64", 4, {"KR_STEP2_Z": "1"}),
+                ("kskipmrr", "aniso512x16x12", 4, {}),
+                ("adaptivekskipmrr", "box512x16x12", 4, {}),
+                ("adaptivekskipmrr", "box512x16x64", 6, {"KR_STENCIL_Z": "4"})]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method,name,k,env", STEP2H_CASES,
+                         ids=[f"{m}-{n}-k{k}-{'-'.join(e)}" for m, n, k, e in STEP2H_CASES])
+def test_box_step_pair_head_bitwise_equal(monkeypatch, method, name, k, env):
+    """Histories and x bit for bit against KR_STEP2H=0 (the step pair, then
+    the head launch)."""
+    A = MATRICES[name]()
+    b = np.random.default_rng(11).standard_normal(A.shape[0])
+    kw = dict(tol=1e-10, maxiter=400, k=k)
+    monkeypatch.setenv("KRYLOV_AMD_SHARDS", "0")
+    for key, val in env.items():
+        monkeypatch.setenv(key, val)
+    out = []
+    for on in ("0", "1"):
+        monkeypatch.setenv("KR_STEP2H", on)
+        with contextlib.redirect_stdout(io.StringIO()):
+            x, info = _solver(method)(A, b, **kw)
+        out.append((x.cpu().numpy(), info))
+    (x0, i0), (x1, i1) = out
+    np.testing.assert_array_equal(i1["nosl"], i0["nosl"])
+    if "khistory" in i0:
+        np.testing.assert_array_equal(i1["khistory"], i0["khistory"])
+    np.testing.assert_array_equal(i1["residual"], i0["residual"])
+    np.testing.assert_array_equal(x1, x0)
