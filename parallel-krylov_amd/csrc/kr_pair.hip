@@ -42,8 +42,8 @@
 // operands of level 2's end rows) is computed by two lanes of the group.
 // XS = 4: 256-thread workgroups, ~29 KB of LDS, four per CU, so one
 // workgroup's barriers overlap the others' work; XS = 1: one 1024-thread
-// workgroup per CU, halo rows always x faces. Measured (st2b_xsegments):
-// XS = 4 for the storing pair, XS = 1 for the products-only one.
+// workgroup per CU, halo rows always x faces (no halo loads, stores or
+// sums at all). Measured (st2b_xsegments): XS = 1 for both pairs.
 //
 // Step s (level 0 of plane s arrives, loaded one step ahead): level 1 of
 // plane s-1 is completed by its +W term and plane s's sum started (-W .. +n);
@@ -997,12 +997,14 @@ void sp3_launch_t(const SpmvArgs& a, int nblocks, hipStream_t s) {
 }  // namespace
 
 // x segments per line (KR_ST2B_XS for the storing pair, KR_ST2B_XS_PO for
-// the products-only one: 1, 2 or 4). Measured on C4 (one box, twice,
-// profiles/r06x): storing pair 1.29 / 1.28 / 1.32 ms at 4 / 2 / 1 segments,
-// products-only pair 1.26 / 1.24 / 1.13 ms (no stores to hide behind, the
-// halo loads cost more than the overlap gains).
+// the products-only one: 1, 2 or 4). Measured on C4: first (one box, twice,
+// profiles/r06x) storing pair 1.29 / 1.28 / 1.32 ms at 4 / 2 / 1 segments,
+// products-only pair 1.26 / 1.24 / 1.13 ms; once whole-line walks stopped
+// issuing the x-halo loads they never need (profiles/r06c, r06h, same box,
+// twice each) the storing pair runs 1.334-1.361 ms at 1 segment against
+// 1.428-1.452 at 4 (C4 826-827 -> 842-845 it/s): whole lines for both.
 int st2b_xsegments(bool products_only) {
-  const int x = products_only ? KR_ENV("KR_ST2B_XS_PO", 1) : KR_ENV("KR_ST2B_XS", 4);
+  const int x = products_only ? KR_ENV("KR_ST2B_XS_PO", 1) : KR_ENV("KR_ST2B_XS", 1);
   return x == 1 || x == 2 ? x : 4;
 }
 

@@ -95,11 +95,11 @@ BOX_CASES = [("kskipmrr", "box512x16x12", 4, {}), ("kskipmrr", "box512x16x12", 5
              ("kskipmrr", "box512x16x64", 6, {"KR_ST2B_Z": "2"}),
              ("kskipcg", "box512x16x64", 4, {"KR_PO_ZMAX": "2", "KR_ST2B_Z": "1"}),
              ("adaptivekskipmrr", "box512x16x64", 6, {}),
-             # x segments per line (KR_ST2B_XS, default 4): whole lines, halves
-             ("kskipmrr", "box512x16x12", 4, {"KR_ST2B_XS": "1", "KR_ST2B_XS_PO": "4"}),
+             # x segments per line (KR_ST2B_XS, default 1): quarters, halves
+             ("kskipmrr", "box512x16x12", 4, {"KR_ST2B_XS": "4", "KR_ST2B_XS_PO": "4"}),
              ("kskipmrr", "box512x32x10", 5, {"KR_ST2B_XS": "2"}),
              ("kskipcg", "box512x16x12", 4, {"KR_ST2B_XS": "2", "KR_ST2B_XS_PO": "2"}),
-             ("adaptivekskipmrr", "aniso512x16x12", 6, {"KR_ST2B_XS": "1"}),
+             ("adaptivekskipmrr", "aniso512x16x12", 6, {"KR_ST2B_XS": "4"}),
              ("kskipmrr", "box512x16x64", 4, {"KR_PO_ZMAX": "1", "KR_ST2B_Z": "1",
                                               "KR_ST2B_XS": "2"})]
 
