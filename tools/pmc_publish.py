@@ -25,7 +25,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def engine_name(name):
-    if name.startswith(("spmv_step2_mrr_stencil", "spmv_step3_mrr_stencil")):
+    if name.startswith(("spmv_step2_mrr_stencil", "spmv_step3_mrr_stencil", "spmv_step2h_mrr_stencil")):
         return name  # the box step walks: the engine books them under these names
     return re.sub(r"(_rp64)?(_dia|_dense|_stencil)?$", "", name)
 

@@ -34,6 +34,8 @@ def short(name):
     m = re.search(r"spmv_step2b_kernel<(\w+), \d+>", name)
     if m:
         return "spmv_step3_mrr_stencil" if m.group(1) == "true" else "spmv_step2_mrr_stencil"
+    if re.search(r"spmv_step2h_kernel<\d+>", name):
+        return "spmv_step2h_mrr_stencil"
     m = re.search(r"spmv_kernel2_po<(\w+), (\d+), (\w+)", name)
     if m:  # the plain-CSR row walk's products-only dual (engine name ..._last)
         return EPI[int(m.group(2))] + "_last" + ("" if m.group(1) == "int" else "_rp64")
