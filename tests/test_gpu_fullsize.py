@@ -253,3 +253,21 @@ def test_c4_fullsize_partitions_match_oracle():
     for h in (h1, h8):
         p = bench.history_parity(h, ref)
         assert p["ok"] and p["entries"] == 4, p
+
+
+@pytest.mark.timeout(600)
+def test_c4_fullsize_box_walks_bitwise_dual_path(monkeypatch):
+    """C4 at full size, one shard: the box walks (the default on the 512^3
+    constant-coefficient box: box pairs, step triple, step pair + head)
+    against the dual and step launches (KR_BOX=0), 3 outer iterations --
+    residual history and nosl bit for bit (the small-box cases of
+    tests/test_gpu_box_pair.py, at the headline size)."""
+    k, outer = 4, 3
+    maxiter = 1 + outer * (k + 1)
+    monkeypatch.setenv("KR_BOX", "0")
+    hd = _c4_history(1, maxiter)
+    monkeypatch.delenv("KR_BOX")
+    hb = _c4_history(1, maxiter)
+    assert list(hb["nosl"]) == list(hd["nosl"]) == [0, 1, 6, 11, 16]
+    np.testing.assert_array_equal(np.asarray(hb["residual"]), np.asarray(hd["residual"]))
+
