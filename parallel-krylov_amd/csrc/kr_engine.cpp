@@ -569,8 +569,10 @@ int System::pair_mode() const {
   const int mode = env < 0 ? 3 : env;
   if (mode != 1 && mode != 2 && mode != 3) return 0;
   const Shard& s = shards[0];
+  // (the box pair writes the partials in the position-major dual grids'
+  // workgroup order: KR_STENCIL_PM=0 keeps the duals)
   if (mode == 3)
-    return s.st_box && s.st_P % 16 == 0 && s.spmv_grid % s.st_P == 0 &&
+    return s.st_box && s.st_P % 16 == 0 && stencil_pm(s.st_P) && s.spmv_grid % s.st_P == 0 &&
                    s.spmv_grid_po % s.st_P == 0
                ? 3 : 0;
   if (!s.scode || !stencil_pm(s.st_P) || s.nm != 7 || s.st_nfar != 2) return 0;
@@ -736,7 +738,8 @@ void System::spmv_step2(int r_in, int r_out, int y_in, int y_out, int z, int xs,
 bool System::step2h_ok() const {
   if (!step2_ok() || KR_ENV("KR_STEP2H", 1) == 0) return false;
   const Shard& s = shards[0];
-  if (s.spmv_grid % s.st_P != 0) return false;
+  // the head's partials in its position-major grid's workgroup order
+  if (!stencil_pm(s.st_P) || s.spmv_grid % s.st_P != 0) return false;
   // walk segments (spmv_step2h) dividing the head grid's plane segments
   const int64_t planes = s.n / ((int64_t)s.st_P * kStencilBlock);
   const int zh = s.spmv_grid / s.st_P;
