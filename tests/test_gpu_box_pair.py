@@ -270,3 +270,42 @@ def test_box_step_pair_head_bitwise_equal(monkeypatch, method, name, k, env):
         np.testing.assert_array_equal(i1["khistory"], i0["khistory"])
     np.testing.assert_array_equal(i1["residual"], i0["residual"])
     np.testing.assert_array_equal(x1, x0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method,name,k", [("kskipmrr", "box512x16x12", 4),
+                                           ("adaptivekskipmrr", "box512x32x10", 4),
+                                           ("kskipmrr", "aniso512x16x12", 6)])
+def test_box_walks_low_residual_vs_oracle(method, name, k):
+    """The box walks (pairs, step triple, step pair + head) against the oracle
+    itself (oracle.v3cpu, bitwise the reference's v3/cpu) down to tol =
+    1e-12, the low-residual regime of SURVEY.md 8(c) at the headline's
+    n = 512 line geometry: nosl (and khistory) identical, entries >= 1e-8
+    within 1e-12 relative, entries below within max(1e-12, 10x the oracle's
+    reordering envelope: its dots summed in 256-element blocks), x within
+    max(1e-11, 10x its envelope)."""
+    from oracle import v3cpu
+    from test_gpu_fullsize import _oracle_blocked_dots
+    A = MATRICES[name]()
+    b = np.random.default_rng(13).standard_normal(A.shape[0])
+    kw = dict(tol=1e-12, k=k)
+    with contextlib.redirect_stdout(io.StringIO()):
+        x, info = _solver(method)(A, b, **kw)
+    x = x.cpu().numpy()
+    fn = getattr(v3cpu, method)
+    x_ref, ref = fn(A, b, **kw)
+    x_p, ref_p = _oracle_blocked_dots(fn, A, b, **kw)
+    assert len(ref_p["residual"]) == len(ref["residual"])
+    env = np.abs(ref_p["residual"] - ref["residual"]) / np.abs(ref["residual"])
+    x_env = np.linalg.norm(x_p - x_ref) / np.linalg.norm(x_ref)
+    res = np.asarray(info["residual"])
+    assert ref["residual"][-1] < 1e-12 and np.sum(ref["residual"] < 1e-8) >= 2
+    np.testing.assert_array_equal(info["nosl"], ref["nosl"])
+    if "khistory" in ref:
+        np.testing.assert_array_equal(info["khistory"], ref["khistory"])
+    rel = np.abs(res - ref["residual"]) / np.abs(ref["residual"])
+    contract = np.abs(ref["residual"]) >= 1e-8
+    assert np.all(rel[contract] <= 1e-12), rel[contract].max()
+    assert np.all(rel[~contract] <= np.maximum(1e-12, 10.0 * env[~contract])), (rel, env)
+    xrel = np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref)
+    assert xrel <= max(1e-11, 10.0 * x_env), (xrel, x_env)
