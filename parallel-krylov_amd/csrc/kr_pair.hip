@@ -1,4 +1,11 @@
-// The box fused basis pair (gfx950): two chained k-skip basis SpMVs in ONE
+// The box walks (gfx950): matrix-free multi-level plane walks for a
+// constant-coefficient 7-point stencil on a box with n = 512, each bitwise
+// the launches it replaces (DESIGN.md section 5 "Box walks"):
+//   spmv_stencil2b_kernel  two k-skip basis duals (+ both Gram products)
+//   spmv_step2b_kernel     two k-skip MrR steps (VIRT: steps 0-2)
+//   spmv_step2h_kernel     the last two steps + the next outer iteration's head
+//
+// The box fused basis pair: two chained k-skip basis SpMVs in ONE
 // walk for a constant-coefficient 7-point stencil on a box with n = 512
 // (System::build_box checks it entry by entry: Shard::st_box).
 //
