@@ -309,3 +309,33 @@ def test_box_walks_low_residual_vs_oracle(method, name, k):
     assert np.all(rel[~contract] <= np.maximum(1e-12, 10.0 * env[~contract])), (rel, env)
     xrel = np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref)
     assert xrel <= max(1e-11, 10.0 * x_env), (xrel, x_env)
+
+
+# thin and short boxes: 1-3 planes (walk and grid segment counts clamp to
+# the plane count), P = 16 / 32, every box-walk kind against the dual path
+THIN = [("kskipmrr", 512, 16, 1, 4), ("kskipmrr", 512, 16, 2, 4), ("kskipmrr", 512, 16, 3, 5),
+        ("kskipmrr", 512, 32, 2, 6), ("adaptivekskipmrr", 512, 16, 3, 4),
+        ("kskipcg", 512, 16, 2, 4), ("kskipmrr", 512, 16, 5, 2)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method,nx,ny,nz,k", THIN,
+                         ids=[f"{m}-{nx}x{ny}x{nz}-k{k}" for m, nx, ny, nz, k in THIN])
+def test_box_walks_thin_boxes_bitwise_dual_path(monkeypatch, method, nx, ny, nz, k):
+    """Histories and x bit for bit against KR_BOX=0 (no box walks)."""
+    A = box(nx, ny, nz)
+    b = np.random.default_rng(17).standard_normal(A.shape[0])
+    kw = dict(tol=1e-10, maxiter=300, k=k)
+    monkeypatch.setenv("KRYLOV_AMD_SHARDS", "0")
+    out = []
+    for on in ("0", "1"):
+        monkeypatch.setenv("KR_BOX", on)
+        with contextlib.redirect_stdout(io.StringIO()):
+            x, info = _solver(method)(A, b, **kw)
+        out.append((x.cpu().numpy(), info))
+    (x0, i0), (x1, i1) = out
+    np.testing.assert_array_equal(i1["nosl"], i0["nosl"])
+    if "khistory" in i0:
+        np.testing.assert_array_equal(i1["khistory"], i0["khistory"])
+    np.testing.assert_array_equal(i1["residual"], i0["residual"])
+    np.testing.assert_array_equal(x1, x0)
