@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 out=gpurun_out/r06p
 mkdir -p $out
 for rep in 1 2; do
-  for ab in 0 1 2 8 48; do
+  for ab in 0 $ABS; do
     lib=parallel-krylov_amd/libkrylov_amd.so
     [ $ab != 0 ] && lib=parallel-krylov_amd/libkrylov_amd_ab$ab.so
     KRYLOV_AMD_LIB=$(realpath $lib) timeout -k 10 200 python bench.py --steps 6 --warmup 2 \
