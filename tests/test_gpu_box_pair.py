@@ -339,3 +339,25 @@ def test_box_walks_thin_boxes_bitwise_dual_path(monkeypatch, method, nx, ny, nz,
         np.testing.assert_array_equal(i1["khistory"], i0["khistory"])
     np.testing.assert_array_equal(i1["residual"], i0["residual"])
     np.testing.assert_array_equal(x1, x0)
+
+
+@pytest.mark.gpu
+def test_box_walks_need_position_major_grids(monkeypatch):
+    """KR_STENCIL_PM=0 (plane-major stencil grids): the box walks that write
+    Gram partials (the pairs, the step pair + head) write them in the
+    position-major grids' workgroup order, so they step aside; the step
+    walks (no partials) stay. The history equals KR_BOX=0's bit for bit."""
+    A = MATRICES["box512x16x12"]()
+    monkeypatch.setenv("KR_STENCIL_PM", "0")
+    st = _launches(A, "kskipmrr", 4, "3", monkeypatch)
+    assert not any(k.startswith(("spmv2x2", "spmv_step2h")) for k in st), st
+    assert st.get("spmv_step3_mrr_stencil", 0) > 0 and st.get("spmv_step2_mrr_stencil", 0) > 0, st
+    b = np.random.default_rng(19).standard_normal(A.shape[0])
+    out = []
+    for on in ("0", "1"):
+        monkeypatch.setenv("KR_BOX", on)
+        with contextlib.redirect_stdout(io.StringIO()):
+            x, info = _solver("kskipmrr")(A, b, tol=1e-10, maxiter=200, k=4)
+        out.append((x.cpu().numpy(), info))
+    np.testing.assert_array_equal(out[1][1]["residual"], out[0][1]["residual"])
+    np.testing.assert_array_equal(out[1][0], out[0][0])
