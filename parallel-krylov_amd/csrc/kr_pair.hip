@@ -76,6 +76,16 @@
 #ifndef KR_ST2B_AB
 #define KR_ST2B_AB 0
 #endif
+// The +-1 operands of the level-1 / level-2 sums: by DPP from the own rows
+// (wave_shr / wave_shl, the wave's two edge rows from LDS by uniform reads)
+// or by per-lane LDS reads of rows 2t-1 and 2t+2 (16-byte lane stride: bank
+// conflicts). KR_ST2B_DPP 1: DPP in the storing pair only, 2: in both, 0: in
+// neither. Same-box A/B (profiles/r06u): DPP storing pair -0.04 ms of ~1.38,
+// products-only pair +0.015 of ~1.06 (the shifts' VALU cost more there than
+// the conflicts they remove); the reads' whole price (ablation 4) 0.07 / 0.04.
+#ifndef KR_ST2B_DPP
+#define KR_ST2B_DPP 1
+#endif
 #if KR_ST2B_AB && !defined(KR_ALLOW_WRONG_RESULTS)
 #error "KR_ST2B_AB builds give wrong results: define KR_ALLOW_WRONG_RESULTS (A/B libraries only)"
 #endif
@@ -134,9 +144,10 @@ __device__ __forceinline__ void st2b_walk(const SpmvArgs& a, St2bLds<XS>& L, int
   constexpr int G = SL / 2;      // lanes per group
   constexpr int NWG = G / 64;    // waves per group
   constexpr int NP = 7;
+  constexpr bool kDpp = KR_ST2B_DPP == 2 || (KR_ST2B_DPP == 1 && !PO);
   constexpr int IO = H == 0 ? 1 : 0;  // own line among the group's two level-1 lines
   constexpr int J2 = 2 + H;           // own line's level-0 index (x0), x1 index 1 + H
-  const int lane = t & 63, wig = t >> 6;
+  const int lane = t & 63, wig = __builtin_amdgcn_readfirstlane(t >> 6);
   const int quarter = xs * NWG + wig;  // the dual workgroup's wave this wave stands for
   const int P = a.st_P, PP = P >> 3;
   const int W = P * kSBlock;
@@ -288,8 +299,16 @@ __device__ __forceinline__ void st2b_walk(const SpmvArgs& a, St2bLds<XS>& L, int
       const dbl2v own = lds2(line);
       const dbl2v c = dbl2v{p1[i].x + v[6] * own.x, p1[i].y + v[6] * own.y};
       l1[i] = (pok && l1ok[i]) ? c : dbl2v{0.0, 0.0};
-      p1[i] = st2b_part(v, l0p[i], lds2(&L.x0[C][j - 1][tl]), (KR_ST2B_AB & 4) ? own.y : line[-1],
-                        own, (KR_ST2B_AB & 4) ? own.x : line[2], lds2(&L.x0[C][j + 1][tl]));
+      double m1, q2;
+      if constexpr (kDpp) {
+        const double* we = &L.x0[C][j][2 + 128 * wig];  // the wave's first row
+        m1 = st_dpp_shr1(own.y, we[-1]);
+        q2 = st_dpp_shl1(own.x, we[128]);
+      } else {
+        m1 = (KR_ST2B_AB & 4) ? own.y : line[-1];
+        q2 = (KR_ST2B_AB & 4) ? own.x : line[2];
+      }
+      p1[i] = st2b_part(v, l0p[i], lds2(&L.x0[C][j - 1][tl]), m1, own, q2, lds2(&L.x0[C][j + 1][tl]));
       l0p[i] = own;
     }
     // (4) level 1 of plane s-1 to LDS, with the own line's halo rows
@@ -341,8 +360,16 @@ __device__ __forceinline__ void st2b_walk(const SpmvArgs& a, St2bLds<XS>& L, int
         k2 = l2;
       }
       const double* lx = &L.x1[C][1 + H][tl];
-      p2 = st2b_part(v, l1p, lds2(&L.x1[C][H][tl]), (KR_ST2B_AB & 4) ? own.y : lx[-1], own,
-                     (KR_ST2B_AB & 4) ? own.x : lx[2], lds2(&L.x1[C][2 + H][tl]));
+      double m1, q2;
+      if constexpr (kDpp) {
+        const double* we = &L.x1[C][1 + H][2 + 128 * wig];
+        m1 = st_dpp_shr1(own.y, we[-1]);
+        q2 = st_dpp_shl1(own.x, we[128]);
+      } else {
+        m1 = (KR_ST2B_AB & 4) ? own.y : lx[-1];
+        q2 = (KR_ST2B_AB & 4) ? own.x : lx[2];
+      }
+      p2 = st2b_part(v, l1p, lds2(&L.x1[C][H][tl]), m1, own, q2, lds2(&L.x1[C][2 + H][tl]));
       l1p = own;
     }
   };
