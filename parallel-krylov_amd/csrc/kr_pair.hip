@@ -79,12 +79,12 @@
 // The +-1 operands of the level-1 / level-2 sums: by DPP from the own rows
 // (wave_shr / wave_shl, the wave's two edge rows from LDS by uniform reads)
 // or by per-lane LDS reads of rows 2t-1 and 2t+2 (16-byte lane stride: bank
-// conflicts). KR_ST2B_DPP 1: DPP in the storing pair only, 2: in both, 0: in
-// neither. Same-box A/B (profiles/r06u): DPP storing pair -0.04 ms of ~1.38,
+// conflicts). KR_ST2B_DPP bits: 0 the storing pair's level-1 sums, 1 its
+// level-2 sums, 2 / 3 the products-only pair's. Same-box A/B (profiles/r06u): DPP storing pair -0.04 ms of ~1.38,
 // products-only pair +0.015 of ~1.06 (the shifts' VALU cost more there than
 // the conflicts they remove); the reads' whole price (ablation 4) 0.07 / 0.04.
 #ifndef KR_ST2B_DPP
-#define KR_ST2B_DPP 1
+#define KR_ST2B_DPP 3
 #endif
 #if KR_ST2B_AB && !defined(KR_ALLOW_WRONG_RESULTS)
 #error "KR_ST2B_AB builds give wrong results: define KR_ALLOW_WRONG_RESULTS (A/B libraries only)"
@@ -144,7 +144,8 @@ __device__ __forceinline__ void st2b_walk(const SpmvArgs& a, St2bLds<XS>& L, int
   constexpr int G = SL / 2;      // lanes per group
   constexpr int NWG = G / 64;    // waves per group
   constexpr int NP = 7;
-  constexpr bool kDpp = KR_ST2B_DPP == 2 || (KR_ST2B_DPP == 1 && !PO);
+  constexpr bool kDpp1 = (KR_ST2B_DPP >> (PO ? 2 : 0)) & 1;  // level 1's +-1 operands by DPP
+  constexpr bool kDpp2 = (KR_ST2B_DPP >> (PO ? 3 : 1)) & 1;  // level 2's
   constexpr int IO = H == 0 ? 1 : 0;  // own line among the group's two level-1 lines
   constexpr int J2 = 2 + H;           // own line's level-0 index (x0), x1 index 1 + H
   const int lane = t & 63, wig = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -300,7 +301,7 @@ __device__ __forceinline__ void st2b_walk(const SpmvArgs& a, St2bLds<XS>& L, int
       const dbl2v c = dbl2v{p1[i].x + v[6] * own.x, p1[i].y + v[6] * own.y};
       l1[i] = (pok && l1ok[i]) ? c : dbl2v{0.0, 0.0};
       double m1, q2;
-      if constexpr (kDpp) {
+      if constexpr (kDpp1) {
         const double* we = &L.x0[C][j][2 + 128 * wig];  // the wave's first row
         m1 = st_dpp_shr1(own.y, we[-1]);
         q2 = st_dpp_shl1(own.x, we[128]);
@@ -361,7 +362,7 @@ __device__ __forceinline__ void st2b_walk(const SpmvArgs& a, St2bLds<XS>& L, int
       }
       const double* lx = &L.x1[C][1 + H][tl];
       double m1, q2;
-      if constexpr (kDpp) {
+      if constexpr (kDpp2) {
         const double* we = &L.x1[C][1 + H][2 + 128 * wig];
         m1 = st_dpp_shr1(own.y, we[-1]);
         q2 = st_dpp_shl1(own.x, we[128]);
