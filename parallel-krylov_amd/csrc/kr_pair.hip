@@ -86,6 +86,15 @@
 #ifndef KR_ST2B_DPP
 #define KR_ST2B_DPP 3
 #endif
+// The same choice in the step walks, KR_STEP_DPP bits: 0 / 1 the step pair's
+// (sp2b_walk) level 1 / 2, 2 / 3 / 4 the step pair + head's (sp3_walk)
+// level 1 / 2 / 3. Same-box A/B (profiles/r06x, r06y): the step pair + head
+// with DPP at all three levels -0.126 ms of ~1.78 over four reps (the pairs
+// after it +0.03 ms each: the stores' drain moves into them), the step pair
+// no measurable change.
+#ifndef KR_STEP_DPP
+#define KR_STEP_DPP 28
+#endif
 #if KR_ST2B_AB && !defined(KR_ALLOW_WRONG_RESULTS)
 #error "KR_ST2B_AB builds give wrong results: define KR_ALLOW_WRONG_RESULTS (A/B libraries only)"
 #endif
@@ -105,6 +114,22 @@ struct St2bLds {
 
 __device__ __forceinline__ dbl2v lds2(const double* p) { return *reinterpret_cast<const dbl2v*>(p); }
 __device__ __forceinline__ void lds2_st(double* p, dbl2v v) { *reinterpret_cast<dbl2v*>(p) = v; }
+
+// Rows 2t-1 and 2t+2 of an LDS line (row0: its row 0; own: rows 2t, 2t+1 of
+// lane t, wave wig of the line): DPP from the own rows with the wave's edge
+// rows by uniform reads, or per-lane reads.
+template <bool DPP>
+__device__ __forceinline__ void st2b_nbrs(const double* row0, int t, int wig, dbl2v own,
+                                          double& m1, double& q2) {
+  if constexpr (DPP) {
+    const double* we = row0 + 128 * wig;
+    m1 = st_dpp_shr1(own.y, we[-1]);
+    q2 = st_dpp_shl1(own.x, we[128]);
+  } else {
+    m1 = row0[2 * t - 1];
+    q2 = row0[2 * t + 2];
+  }
+}
 
 // One row pair of a 7-point row sum over slots -W .. +n (the +W term is added
 // when the next plane arrives): operands xw (-W), mn / pn (-n / +n lines),
@@ -521,6 +546,7 @@ __device__ __forceinline__ void sp2b_walk(const SpmvArgs& a, Sp2bLds& L, int t, 
   const int W = P * kSBlock;
   const int planes = (int)(a.n / W);
   const int z0 = (int)((int64_t)planes * zs / Zw), z1 = (int)((int64_t)planes * (zs + 1) / Zw);
+  const int wig = __builtin_amdgcn_readfirstlane(t >> 6);  // the lane's wave in its line
   double v[7];
 #pragma unroll
   for (int k = 0; k < 7; ++k) v[k] = a.st_v[k];
@@ -633,7 +659,9 @@ __device__ __forceinline__ void sp2b_walk(const SpmvArgs& a, Sp2bLds& L, int t, 
     const bool pok = (unsigned)(s - 1) < (unsigned)planes;
     if (!(pok && jok)) rb = dbl2v{0.0, 0.0};  // level 1 off the box: the absent operand
     const dbl2v ra1 = l0p;  // level 0 of plane s-1
-    p1 = st2b_part(v, l0p, lds2(&L.x0[J - 1][tl]), line[-1], own, line[2], lds2(&L.x0[J + 1][tl]));
+    double m1, q2;
+    st2b_nbrs<(KR_STEP_DPP & 1) != 0>(&L.x0[J][2], t, wig, own, m1, q2);
+    p1 = st2b_part(v, l0p, lds2(&L.x0[J - 1][tl]), m1, own, q2, lds2(&L.x0[J + 1][tl]));
     l0p = own;
     if constexpr (VIRT) ya1 = yj;
     lds2_st(&L.x1[G][tl], rb);
@@ -681,8 +709,9 @@ __device__ __forceinline__ void sp2b_walk(const SpmvArgs& a, Sp2bLds& L, int t, 
           __builtin_nontemporal_store(xn, reinterpret_cast<dbl2v*>(a.ud + row));
         __builtin_nontemporal_store(rc, reinterpret_cast<dbl2v*>(a.y1 + row));
       }
-      const double* lx = &L.x1[G][tl];
-      p2 = st2b_part(v, l1p, lds2(&L.x1[G - 1][tl]), lx[-1], rb, lx[2], lds2(&L.x1[G + 1][tl]));
+      double n1, n2;
+      st2b_nbrs<(KR_STEP_DPP & 2) != 0>(&L.x1[G][2], t, wig, rb, n1, n2);
+      p2 = st2b_part(v, l1p, lds2(&L.x1[G - 1][tl]), n1, rb, n2, lds2(&L.x1[G + 1][tl]));
       l1p = rb;
       yb2 = yb;
       ra2 = ra1;
@@ -776,6 +805,7 @@ __device__ __forceinline__ void sp3_walk(const SpmvArgs& a, Sp3Lds& L, int t, in
   constexpr int I2 = J2 - J1;                         // its index among the level-1 lines
   constexpr int NP = 5;
   const int lane = t & 63, quarter = t >> 6;
+  const int wig = __builtin_amdgcn_readfirstlane(t >> 6);  // the lane's wave in its line
   const int P = a.st_P, PP = P >> 3;
   const int W = P * kSBlock;
   const int planes = (int)(a.n / W);
@@ -894,8 +924,9 @@ __device__ __forceinline__ void sp3_walk(const SpmvArgs& a, Sp3Lds& L, int t, in
       yb[i] = dbl2v{t1l + t2l, t1h + t2h};
       rb[i] = dbl2v{l0p[i].x - yb[i].x, l0p[i].y - yb[i].y};
       if (!(pok1 && l1ok[i])) rb[i] = dbl2v{0.0, 0.0};  // off the box: the absent operand
-      p1[i] = st2b_part(v, l0p[i], lds2(&L.x0[j - 1][tl]), line[-1], own, line[2],
-                        lds2(&L.x0[j + 1][tl]));
+      double m1, q2;
+      st2b_nbrs<(KR_STEP_DPP & 4) != 0>(&L.x0[j][2], t, wig, own, m1, q2);
+      p1[i] = st2b_part(v, l0p[i], lds2(&L.x0[j - 1][tl]), m1, own, q2, lds2(&L.x0[j + 1][tl]));
       l0p[i] = own;
       lds2_st(&L.x1[j - 1][tl], rb[i]);
     }
@@ -932,8 +963,9 @@ __device__ __forceinline__ void sp3_walk(const SpmvArgs& a, Sp3Lds& L, int t, in
     }
     if (!(pok2 && l2ok)) rc = dbl2v{0.0, 0.0};  // off the box: the head's absent operand
     {
-      const double* lx = &L.x1[J2 - 1][tl];
-      p2 = st2b_part(v, l1p, lds2(&L.x1[J2 - 2][tl]), lx[-1], rbo, lx[2], lds2(&L.x1[J2][tl]));
+      double n1, n2;
+      st2b_nbrs<(KR_STEP_DPP & 8) != 0>(&L.x1[J2 - 1][2], t, wig, rbo, n1, n2);
+      p2 = st2b_part(v, l1p, lds2(&L.x1[J2 - 2][tl]), n1, rbo, n2, lds2(&L.x1[J2][tl]));
     }
     l1p = rbo;
     yb2 = yb[I2];
@@ -954,8 +986,9 @@ __device__ __forceinline__ void sp3_walk(const SpmvArgs& a, Sp3Lds& L, int t, in
         epi_products<EPI_HEAD_MRR>(l2p.y, 0.0, ar3.y, 0.0, yc1.y, acc);
         __builtin_nontemporal_store(ar3, reinterpret_cast<dbl2v*>(a.y2 + orow + (int64_t)zh * W));
       }
-      const double* lx = &L.x2[J2 - 2][tl];
-      p3 = st2b_part(v, l2p, lds2(&L.x2[J2 - 3][tl]), lx[-1], rc, lx[2], lds2(&L.x2[J2 - 1][tl]));
+      double n1, n2;
+      st2b_nbrs<(KR_STEP_DPP & 16) != 0>(&L.x2[J2 - 2][2], t, wig, rc, n1, n2);
+      p3 = st2b_part(v, l2p, lds2(&L.x2[J2 - 3][tl]), n1, rc, n2, lds2(&L.x2[J2 - 1][tl]));
       l2p = rc;
       yc1 = yc;
     }
