@@ -249,7 +249,7 @@ System::~System() {
     for (auto* list : {&s.send, &s.recv})
       for (auto& p : *list)
         if (p.stage) (void)hipFree(p.stage);
-    for (double* v : s.vec) (void)hipFree(v);
+    for (double* v : s.vec_base) (void)hipFree(v);
     for (void* p : s.owned) (void)hipFree(p);
     if (s.partials) (void)hipFree(s.partials);
     if (s.slots) (void)hipFree(s.slots);
@@ -1649,11 +1649,19 @@ void System::alloc_vectors(int count) {
   for (auto& s : shards) {
     KR_HIP_CHECK(hipSetDevice(s.dev));
     KR_HIP_CHECK(hipStreamSynchronize(s.stream));
-    for (double* v : s.vec) KR_HIP_CHECK(hipFree(v));
+    for (double* v : s.vec_base) KR_HIP_CHECK(hipFree(v));
     s.vec.assign(count, nullptr);
+    s.vec_base.assign(count, nullptr);
+    // KR_VEC_STAGGER (bytes, a multiple of 256): vector i's rows start i x
+    // that far into its allocation, so the vectors a walk streams together
+    // do not share their low address bits
+    const int64_t stagger = KR_ENV("KR_VEC_STAGGER", 0);
+    KR_REQUIRE(stagger >= 0 && stagger % 256 == 0, "KR_VEC_STAGGER: a multiple of 256 bytes");
     for (int i = 0; i < count; ++i) {
-      if (hipMalloc(&s.vec[i], sizeof(double) * (size_t)s.ld) != hipSuccess)
+      const size_t off = (size_t)stagger * (size_t)i;
+      if (hipMalloc(&s.vec_base[i], sizeof(double) * (size_t)s.ld + off) != hipSuccess)
         throw Failure(KR_ERR_NOMEM, "vector allocation failed");
+      s.vec[i] = s.vec_base[i] + off / sizeof(double);
       // zeros (NaN under KR_POISON_ALLOC): pad and halo rows included, so a
       // halo row read before its exchange, or a pad row read as an operand,
       // is a NaN in the poison run. x0 = 0 is written explicitly (load_bx).

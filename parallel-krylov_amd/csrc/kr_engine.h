@@ -143,8 +143,9 @@ struct Shard {
   double* host = nullptr;       // pinned [nranks][kMaxSlots]
   double* st = nullptr;         // device-resident CG/MrR scalars [kScalarState]
   double* hst = nullptr;        // pinned copy of st
-  // vectors, each ld doubles, zero-initialised
-  std::vector<double*> vec;
+  // vectors, each ld doubles, zero-initialised; vector i starts i x
+  // KR_VEC_STAGGER bytes into its allocation (vec_base)
+  std::vector<double*> vec, vec_base;
   int st_flip = 0;  // the next stencil walk launch runs reversed (SpmvArgs::st_rev)
   hipEvent_t ev_a = nullptr, ev_b = nullptr;
   // profiling (event pairs pending until the next sync)
